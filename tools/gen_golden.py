@@ -1,0 +1,272 @@
+"""Generate golden input/output vectors from the reference (THIS container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [--only NAME ...]
+
+Imports pyabc 0.10.1 from /root/reference through ``tools/ref_stub.py`` and
+writes small ``.npz`` fixtures under ``tests/golden/``.  Only arrays (inputs and
+the reference's outputs) are written; no reference source travels.  The GPU box
+never runs this script: the committed fixtures are what the tests read there.
+
+Every fixture records the call site it pins (reference file:line) in the
+``_ref`` string entry.
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import pandas as pd
+
+sys.path.insert(0, os.path.dirname(__file__))
+import ref_stub  # noqa: E402
+
+pyabc = ref_stub.import_pyabc()
+from pyabc.transition import (MultivariateNormalTransition,  # noqa: E402
+                              LocalTransition)
+from pyabc.distance import (PNormDistance, AdaptivePNormDistance,  # noqa: E402
+                            median_absolute_deviation, standard_deviation)
+from pyabc.weighted_statistics import weighted_quantile  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
+    __file__))), "tests", "golden")
+
+
+def pnames(d):
+    # zero-padded so pandas' name-sorted columns equal the natural order
+    # (history.py:307 pivots -> columns sorted by name)
+    return [f"p{k:02d}" for k in range(d)]
+
+
+def save(name, **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print(f"  wrote {path} ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
+def make_population(rng, n, d, offset=3.0):
+    """Correlated, offset population with non-uniform weights."""
+    L = np.tril(rng.normal(size=(d, d)) * 0.3) + np.eye(d)
+    X = rng.normal(size=(n, d)) @ L.T + offset * rng.uniform(-1, 1, size=d)
+    w = rng.uniform(0.5, 1.5, size=n)
+    w = w / w.sum()
+    return X, w
+
+
+# --------------------------------------------------------------------------
+# (a1) + (a3): MVN fit and KDE transition density / importance weight
+# --------------------------------------------------------------------------
+def gen_kde():
+    cases = [(4096, 1024, 8, 0), (2048, 512, 20, 1), (1024, 1024, 1, 2),
+             (2048, 512, 4, 3), (1, 16, 3, 4), (2, 16, 2, 5)]
+    for N, M, d, seed in cases:
+        rng = np.random.default_rng(100 + seed)
+        X, w = make_population(rng, N, d)
+        cols = pnames(d)
+        tr = MultivariateNormalTransition()
+        df = pd.DataFrame(X, columns=cols)
+        w_in = w.copy()
+        tr.fit(df, w_in)                      # transitionmeta.py:9-20
+        np.random.seed(1000 + seed)
+        theta = tr.rvs(size=M).values         # multivariatenormal.py:87-95
+        pd_df = tr.pdf(pd.DataFrame(theta, columns=cols))   # :102-125
+        pd_df = np.atleast_1d(np.asarray(pd_df, dtype=float))
+        # single-row Series path (smc.py:726-727) on a few rows
+        k = min(8, M)
+        pd_series = np.array([tr.pdf(pd.Series(dict(zip(cols, theta[i]))))
+                              for i in range(k)])
+        # prior U(-10, 20)^d (box containing the data); weight = prior/transition
+        lo = np.full(d, -10.0)
+        sc = np.full(d, 30.0)
+        prior = pyabc.Distribution(**{c: pyabc.RV("uniform", lo[j], sc[j])
+                                      for j, c in enumerate(cols)})
+        prior_pd = np.array([prior.pdf(pd.Series(dict(zip(cols, th))))
+                             for th in theta])
+        weight = prior_pd / pd_df            # smc.py:776-792
+        wsum = sum(weight)                   # population.py:127-128 (sequential)
+        weight_norm = weight / wsum
+        save(f"kde_N{N}_M{M}_d{d}",
+             X=X, w=w, theta=theta, cov=tr.cov, transition_pd=pd_df,
+             transition_pd_series=pd_series, prior_lo=lo, prior_scale=sc,
+             prior_pd=prior_pd, weight=weight, weight_norm=weight_norm,
+             _ref=np.array("pyabc/transition/multivariatenormal.py:67-125; "
+                           "pyabc/smc.py:709-792; pyabc/population.py:120-142"))
+
+
+# --------------------------------------------------------------------------
+# (a2): resample + perturb + prior-support test
+# --------------------------------------------------------------------------
+def gen_resample():
+    for N, d, B, seed in [(4096, 8, 3000, 0), (1000, 3, 2000, 1),
+                          (50, 1, 500, 2), (2048, 20, 1000, 3)]:
+        rng = np.random.default_rng(200 + seed)
+        X, w = make_population(rng, N, d, offset=1.0)
+        # make a few weights tiny / zero-ish to exercise the CDF plateaus
+        w[:5] = 0.0
+        w = w / w.sum()
+        cols = pnames(d)
+        tr = MultivariateNormalTransition(scaling=1.3)
+        tr.fit(pd.DataFrame(X, columns=cols), w.copy())
+        s = 5000 + seed
+        np.random.seed(s)
+        theta_batch = tr.rvs(size=B).values
+        np.random.seed(s)
+        u = np.random.random_sample(B)
+        z = np.random.standard_normal((B, d))
+        # scalar path: u then z(d) per call
+        np.random.seed(s + 1)
+        theta_single = np.array([np.asarray(tr.rvs(), dtype=float)
+                                 for _ in range(8)])
+        np.random.seed(s + 1)
+        u_single, z_single = [], []
+        for _ in range(8):
+            u_single.append(np.random.random_sample())
+            z_single.append(np.random.standard_normal(d))
+        cdf = np.cumsum(tr.w)
+        cdf /= cdf[-1]
+        idx = cdf.searchsorted(u, side="right")
+        # prior box: centred at the population mean, narrow enough that
+        # a fraction of proposals falls outside; plus exact-boundary probes
+        lo = X.mean(0) - 2.0 * X.std(0)
+        sc = 4.0 * X.std(0)
+        prior = pyabc.Distribution(**{c: pyabc.RV("uniform", lo[j], sc[j])
+                                      for j, c in enumerate(cols)})
+        probes = np.repeat(X.mean(0)[None, :], 4 * d, axis=0)
+        for j in range(d):
+            hi = lo[j] + sc[j]
+            probes[4 * j + 0, j] = lo[j]
+            probes[4 * j + 1, j] = np.nextafter(lo[j], -np.inf)
+            probes[4 * j + 2, j] = hi
+            probes[4 * j + 3, j] = np.nextafter(hi, np.inf)
+        all_theta = np.concatenate([theta_batch, probes])
+        in_support = np.array([
+            prior.pdf(pd.Series(dict(zip(cols, th)))) > 0
+            for th in all_theta])
+        save(f"resample_N{N}_d{d}_B{B}",
+             X=X, w=tr.w, cov=tr.cov, u=u, z=z, idx=idx,
+             theta=theta_batch, u_single=np.array(u_single),
+             z_single=np.array(z_single), theta_single=theta_single,
+             prior_lo=lo, prior_scale=sc, probes=probes,
+             in_support=in_support.astype(np.uint8),
+             _ref=np.array("pyabc/transition/multivariatenormal.py:87-95; "
+                           "pyabc/smc.py:629-645; "
+                           "pyabc/random_variables.py:425-452"))
+
+
+# --------------------------------------------------------------------------
+# (a5) + (a6): p-norm distances, accept mask, adaptive MAD / std weights
+# --------------------------------------------------------------------------
+def gen_distance():
+    rng = np.random.default_rng(300)
+    S = 100
+    keys = [f"s{k:03d}" for k in range(S)]
+    order = rng.permutation(S)           # x_0 insertion order != sorted
+    keys = [keys[k] for k in order]
+    x0 = {k: float(v) for k, v in zip(keys, rng.normal(size=S))}
+    for n_rec, tag in [(1000, "even"), (999, "odd")]:
+        scale = np.exp(rng.normal(size=S))
+        data = rng.normal(size=(n_rec, S)) * scale + rng.normal(size=S)
+        # a constant column -> isclose(scale, 0) -> weight 0 (distance.py:272)
+        data[:, 7] = 1.25
+        recs = [dict(zip(keys, row)) for row in data]
+        out = {}
+        for name, sf in [("mad", median_absolute_deviation),
+                         ("std", None)]:
+            dist = AdaptivePNormDistance(p=2, scale_function=sf)
+            dist.initialize(0, lambda: recs, x0)   # distance.py:216-235
+            out["w_" + name] = np.array([dist.weights[0][k] for k in keys])
+        save(f"adaptive_{tag}_n{n_rec}_S{S}", data=data,
+             x0=np.array([x0[k] for k in keys]), **out,
+             _ref=np.array("pyabc/distance/distance.py:216-338; "
+                           "pyabc/distance/scale.py:38-65"))
+    # distances for B particles under several p, with adaptive weights
+    B = 1500
+    data = rng.normal(size=(B, S)) * 1.5 + np.array(list(x0.values()))
+    recs = [dict(zip(keys, row)) for row in data]
+    dist = AdaptivePNormDistance(p=2, scale_function=median_absolute_deviation)
+    dist.initialize(0, lambda: recs[:1000], x0)
+    wvec = np.array([dist.weights[0][k] for k in keys])
+    res = {"stats": data, "x0": np.array([x0[k] for k in keys]),
+           "fw": wvec}
+    for p in [1, 2, 3, np.inf]:
+        dp = PNormDistance(p=p, weights={0: dist.weights[0]})
+        dp.initialize(0, lambda: recs, x0)
+        dvals = np.array([dp(r, x0, 0) for r in recs])   # distance.py:76-102
+        tag = "inf" if p == np.inf else str(p)
+        res["d_p" + tag] = dvals
+    eps = weighted_quantile(res["d_p2"], np.ones(B) / B, alpha=0.5)
+    res["eps_p2"] = np.array(eps)
+    res["accept_p2"] = (res["d_p2"] <= eps).astype(np.uint8)  # acceptor.py:241
+    # python-pow semantics check: how often pow(a,2) != a*a here
+    save(f"pnorm_B{B}_S{S}", **res,
+         _ref=np.array("pyabc/distance/distance.py:76-102; "
+                       "pyabc/acceptor/acceptor.py:235-244"))
+
+
+# --------------------------------------------------------------------------
+# (a7): weighted quantile epsilon
+# --------------------------------------------------------------------------
+def gen_quantile():
+    rng = np.random.default_rng(400)
+    res = {}
+    alphas = np.array([0.1, 0.5, 0.9, 1.0, 0.25, 0.01])
+    for N in [3, 4, 1000, 100000]:
+        d = np.abs(rng.normal(size=N)) * 3 + rng.uniform(0, 1e-3, size=N)
+        assert len(np.unique(d)) == N
+        w = rng.uniform(0.1, 2.0, size=N)
+        w = w / w.sum()
+        q = np.array([weighted_quantile(d, w, alpha=a) for a in alphas])
+        qu = np.array([weighted_quantile(d, None, alpha=a) for a in alphas])
+        res[f"d_{N}"] = d
+        res[f"w_{N}"] = w
+        res[f"q_{N}"] = q
+        res[f"qu_{N}"] = qu
+    # QuantileEpsilon semantics incl. multiplier (epsilon.py:202-228)
+    eps = pyabc.QuantileEpsilon(alpha=0.5, quantile_multiplier=1.1,
+                                weighted=True)
+    df = pd.DataFrame({"distance": res["d_1000"], "w": res["w_1000"] * 7.0})
+    eps.initialize(0, lambda: df, lambda: None, None, None)
+    res["eps_mult"] = np.array(eps(0))
+    save("quantile", alphas=alphas, **res,
+         _ref=np.array("pyabc/weighted_statistics.py:26-43; "
+                       "pyabc/epsilon/epsilon.py:138-228"))
+
+
+# --------------------------------------------------------------------------
+# (a8): LocalTransition kNN covariances and density
+# --------------------------------------------------------------------------
+def gen_local():
+    for N, d, k, seed in [(2000, 6, 50, 0), (300, 3, 10, 1), (500, 2, 20, 2)]:
+        rng = np.random.default_rng(500 + seed)
+        X = rng.normal(size=(N, d)) * rng.uniform(0.5, 2.0, size=d)
+        w = rng.uniform(0.0, 1.0, size=N)
+        w = w / w.sum()
+        cols = pnames(d)
+        tr = LocalTransition(k=k, k_fraction=None, scaling=1.0)
+        t0 = time.time()
+        tr.fit(pd.DataFrame(X, columns=cols), w.copy())   # :77-96
+        from scipy.spatial import cKDTree
+        _, nbr = cKDTree(X).query(X, k=min(tr.k + 1, N))
+        pts = X[rng.integers(0, N, 64)] + rng.normal(size=(64, d)) * 0.2
+        pdf = tr.pdf(pd.DataFrame(pts, columns=cols))     # :98-110
+        save(f"local_N{N}_d{d}_k{k}", X=X, w=w, k=np.array(tr.k),
+             nbr=np.sort(nbr[:, 1:], axis=1).astype(np.int32),
+             covs=tr.covs, inv_covs=tr.inv_covs, dets=tr.determinants,
+             pts=pts, pdf=np.asarray(pdf, dtype=float),
+             _ref=np.array("pyabc/transition/local_transition.py:50-145"))
+        print(f"    local fit {time.time() - t0:.2f}s")
+
+
+GENS = {"kde": gen_kde, "resample": gen_resample, "distance": gen_distance,
+        "quantile": gen_quantile, "local": gen_local}
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    args = ap.parse_args()
+    for name, fn in GENS.items():
+        if args.only and name not in args.only:
+            continue
+        print(f"[{name}]")
+        fn()

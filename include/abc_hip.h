@@ -1,0 +1,196 @@
+/*
+ * libabc_hip — C-ABI of the MI355X (gfx950) per-generation ABC-SMC particle
+ * update.  The host side is Python (pyabc_amd/_native.py binds this file with
+ * ctypes); any other FFI can bind the same symbols.
+ *
+ * Every entry point replaces a numpy/scipy expression of the reference
+ * chrhck/pyABC 0.10.1 (paths relative to the reference checkout):
+ *
+ *   conventions
+ *   -----------
+ *   * all array pointers are DEVICE pointers owned by the caller;
+ *   * row-major; statistics are stat-major [S][ld] (one column per particle);
+ *   * the last argument is the hipStream_t the work is enqueued on; calls are
+ *     asynchronous and never allocate or synchronise (graph-capturable);
+ *   * scratch memory is passed as (ws, ws_bytes), sized by the matching
+ *     abc_*_workspace_bytes() query;
+ *   * return 0 on success, < 0 on error (-1 invalid argument, -2 HIP error,
+ *     -3 unsupported dimension); abc_last_error() describes the last failure
+ *     of the calling thread.
+ */
+#ifndef ABC_HIP_H_
+#define ABC_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* abc_last_error(void);
+int abc_version(void);
+
+/* ---------------- (a1) MultivariateNormalTransition.fit ------------------
+ * Replaces smart_cov = np.cov(X, aweights=w)        transition/util.py:4-15
+ * and the weight sums of fit_cov                     multivariatenormal.py:67-73
+ * out = [sum w, sum w^2, mu[d], C[d*d]] with C = sum w (x-mu)(x-mu)^T; the host
+ * finishes cov = C / (sum w - sum w^2 / sum w) * bw(ESS)^2 * scaling. */
+size_t abc_moments_workspace_bytes(int d);
+int abc_weighted_moments_f64(const double* X, const double* w, int64_t n,
+                             int d, double* out, void* ws, size_t ws_bytes,
+                             hipStream_t stream);
+
+/* ---------------- (a2) MultivariateNormalTransition.rvs + prior support ----
+ * Replaces np.random.choice(p=w) (cumsum, /= cdf[-1], searchsorted 'right')
+ * + np.random.multivariate_normal (z @ sqrt(s)V)     multivariatenormal.py:87-95
+ * and the support test prior.pdf(theta) > 0         smc.py:643-645,
+ *                                                    random_variables.py:425-452
+ * lo/scale may be NULL (no support test). */
+int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf,
+                         hipStream_t stream);
+int abc_resample_perturb_f64(const double* X, int64_t N, int d,
+                             const double* cdf, const double* u,
+                             const double* z, const double* A,
+                             const double* lo, const double* scale, int64_t B,
+                             double* theta, int64_t* idx, uint8_t* in_support,
+                             hipStream_t stream);
+/* production variant: u, z drawn from Philox4x32-10 (seed, streams 2*sid and
+ * 2*sid+1, counter offset) inside the kernel */
+int abc_propose_philox_f64(const double* X, int64_t N, int d,
+                           const double* cdf, const double* A,
+                           const double* lo, const double* scale,
+                           uint64_t seed, uint64_t sid, uint64_t offset,
+                           int64_t B, double* theta, int64_t* idx,
+                           uint8_t* in_support, hipStream_t stream);
+/* t = 0 prior draws, RV('uniform', lo, scale).rvs()  random_variables.py:434 */
+int abc_prior_uniform_f64(const double* lo, const double* scale, int d,
+                          uint64_t seed, uint64_t sid, uint64_t offset,
+                          int64_t B, double* theta, hipStream_t stream);
+int abc_philox_uniform_f64(uint64_t seed, uint64_t sid, uint64_t offset,
+                           int64_t n, double* u, hipStream_t stream);
+int abc_philox_normal_f64(uint64_t seed, uint64_t sid, uint64_t offset,
+                          int64_t n, double* z, hipStream_t stream);
+/* order-preserving compaction: proposal ids for in-support draws only
+ * (out-of-support redraws are not evaluations, smc.py:629-645) */
+size_t abc_compact_workspace_bytes(int64_t n);
+int abc_compact_flags(const uint8_t* flags, int64_t n, int64_t* out_idx,
+                      int64_t* out_count, void* ws, size_t ws_bytes,
+                      hipStream_t stream);
+int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
+                        int64_t n, double* out, hipStream_t stream);
+
+/* ---------------- (a3) KDE importance-weight pass ------------------------
+ * Replaces MultivariateNormalTransition.pdf / pdf_static
+ *   sum_j w_j N(theta; X_j, cov) (scipy multivariate_normal(allow_singular))
+ *                                                    multivariatenormal.py:102-125
+ * called once per accepted particle by transition_pdf smc.py:722-733.
+ * Us = U * sqrt(log2(e)/2) with U the scipy _PSD pseudo-inverse root of cov;
+ * P is the packed previous population [npad][D+1], D = abc_kde_padded_dim(d),
+ * npad a multiple of abc_kde_row_pad(); Ynew is [M][D].
+ * out_logpd[i] = log pdf(theta_i) when log_const = -(rank ln 2pi + log_pdet)/2. */
+int abc_kde_padded_dim(int d);
+int abc_kde_row_pad(void);
+int abc_kde_split(int64_t M, int64_t npad, int d);
+size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d);
+int abc_whiten_f32(const double* X, int64_t n, int d, const double* mu,
+                   const double* Us, float* Y, hipStream_t stream);
+int abc_whiten_f64(const double* X, int64_t n, int d, const double* mu,
+                   const double* Us, double* Y, hipStream_t stream);
+int abc_kde_pack_prev_f32(const double* X, const double* w, int64_t n, int d,
+                          const double* mu, const double* Us, float* P,
+                          int64_t npad, double* lw2max, void* ws,
+                          hipStream_t stream);
+int abc_kde_pack_prev_f64(const double* X, const double* w, int64_t n, int d,
+                          const double* mu, const double* Us, double* P,
+                          int64_t npad, double* lw2max, void* ws,
+                          hipStream_t stream);
+int abc_kde_logpdf_f32(const float* Ynew, int64_t M, const float* P,
+                       int64_t npad, int d, const double* lw2max,
+                       double log_const, double* out_logpd, void* ws,
+                       size_t ws_bytes, hipStream_t stream);
+int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
+                       int64_t npad, int d, const double* lw2max,
+                       double log_const, double* out_logpd, void* ws,
+                       size_t ws_bytes, hipStream_t stream);
+/* w = prior_pd / exp(logpd)                          smc.py:776-792
+ * prior may be NULL (then prior_const is used for every row) */
+int abc_importance_weights_f64(const double* logpd, const double* prior,
+                               double prior_const, int64_t M, double* w,
+                               hipStream_t stream);
+
+/* ---------------- (a4) weight normalisation / ESS ------------------------
+ * Replaces Population._normalize_weights            population.py:120-142
+ * and effective_sample_size                         weighted_statistics.py:73-83 */
+size_t abc_reduce_workspace_bytes(void);
+int abc_sum_f64(const double* x, int64_t n, int squares, double* out,
+                void* ws, hipStream_t stream);
+int abc_scale_inplace_f64(double* x, int64_t n, const double* divisor,
+                          hipStream_t stream);
+
+/* ---------------- (a5) PNormDistance + UniformAcceptor -------------------
+ * Replaces PNormDistance.__call__                   distance/distance.py:76-102
+ * and accept_use_current_time (d <= eps)            acceptor/acceptor.py:235-244
+ * stats_T is [S][ld]; fw = factors * weights in x_0 key order. */
+int abc_pnorm_distance_f64(const double* stats_T, int64_t ld,
+                           const double* x0, const double* fw, int64_t B,
+                           int S, double p, double eps, double* d_out,
+                           uint8_t* accept, uint8_t* guard,
+                           hipStream_t stream);
+
+/* ---------------- (a6) AdaptivePNormDistance scale functions -------------
+ * Replaces median_absolute_deviation / standard_deviation per statistic
+ *                                                    distance/scale.py:38-65
+ * as gathered by AdaptivePNormDistance._update      distance/distance.py:253-297 */
+size_t abc_column_select_workspace_bytes(int S);
+int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
+                              int S, double* median_out, double* mad_out,
+                              void* ws, size_t ws_bytes, hipStream_t stream);
+int abc_column_std_f64(const double* data_T, int64_t ld, int64_t n, int S,
+                       double* mean_out, double* std_out, hipStream_t stream);
+
+/* ---------------- (a7) weighted-quantile epsilon -------------------------
+ * Replaces weighted_quantile                        weighted_statistics.py:26-43
+ * used by QuantileEpsilon._update                   epsilon/epsilon.py:202-228
+ * w may be NULL (uniform weights).  out4 = [eps, p_k, cs_{k-1}, w_k]. */
+size_t abc_wquantile_workspace_bytes(void);
+int abc_wquantile_f64(const double* d, const double* w, int64_t n,
+                      double alpha, double* out4, void* ws, size_t ws_bytes,
+                      hipStream_t stream);
+
+/* ---------------- (a8) LocalTransition -----------------------------------
+ * Replaces cKDTree(X).query(X, k+1)                 local_transition.py:82-83
+ * _cov_and_inv / _cov per particle                  local_transition.py:112-139
+ * and _pdf_single                                   local_transition.py:103-110 */
+size_t abc_knn_workspace_bytes(int64_t N, int k);
+int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
+                double* nbr_d2, void* ws, size_t ws_bytes, hipStream_t stream);
+int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
+                      const int32_t* nbr, int k, double scaling,
+                      double* covs, double* inv_covs, double* dets,
+                      hipStream_t stream);
+int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
+                         const double* w, const double* inv_covs,
+                         const double* dets, int64_t N, int d,
+                         double* out_logpdf, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N);
+
+/* ---------------- synthetic batch simulators (benchmark models) ----------
+ * linear-Gaussian y = A theta + c + sigma eps (SURVEY configs C2/C5) and the
+ * quickstart Gaussian mean model (doc/examples/parameter_inference.ipynb). */
+int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
+                                const double* A, const double* c, int S,
+                                double sigma, uint64_t seed, uint64_t sid,
+                                uint64_t offset, double* out_T, int64_t ld,
+                                hipStream_t stream);
+int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
+                              uint64_t seed, uint64_t sid, uint64_t offset,
+                              double* out, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ABC_HIP_H_ */

@@ -1,0 +1,116 @@
+// Shared helpers for the libabc_hip C-ABI (gfx950 / CDNA4 only).
+//
+// Conventions of every exported entry point (see include/abc_hip.h):
+//   * all pointers are device pointers owned by the caller (torch tensors);
+//   * the last argument is the hipStream_t the work is enqueued on (async);
+//   * the return value is 0 on success, <0 on failure; abc_last_error()
+//     returns a thread-local message for the failing call;
+//   * no allocation, no synchronisation, no host<->device copies inside a
+//     call (graph-capturable), except where a function's comment says so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <cmath>
+
+namespace abc {
+
+enum Status : int {
+  kOk = 0,
+  kInvalidArg = -1,
+  kHipError = -2,
+  kUnsupported = -3,
+};
+
+void set_error(const char* fmt, ...);
+
+#define ABC_REQUIRE(cond, ...)              \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::abc::set_error(__VA_ARGS__);        \
+      return ::abc::kInvalidArg;            \
+    }                                       \
+  } while (0)
+
+#define ABC_LAUNCH_CHECK(what)                                              \
+  do {                                                                      \
+    hipError_t e_ = hipGetLastError();                                      \
+    if (e_ != hipSuccess) {                                                 \
+      ::abc::set_error("%s: %s", what, hipGetErrorString(e_));              \
+      return ::abc::kHipError;                                              \
+    }                                                                       \
+  } while (0)
+
+#define ABC_HIP(call)                                                       \
+  do {                                                                      \
+    hipError_t e_ = (call);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      ::abc::set_error("%s: %s", #call, hipGetErrorString(e_));             \
+      return ::abc::kHipError;                                              \
+    }                                                                       \
+  } while (0)
+
+constexpr int kWave = 64;
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) {
+  return (a + b - 1) / b;
+}
+
+// grid size for a grid-stride streaming kernel (Guideline 11: cap ~2048)
+inline unsigned stream_grid(int64_t n, int block, int cap = 4096) {
+  int64_t g = ceil_div(n, block);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<unsigned>(g);
+}
+
+// ---- wave / block reductions (64-lane waves) -------------------------------
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ inline T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+// Block sum with a fixed reduction tree (deterministic for a fixed blockDim).
+template <typename T, int BLOCK>
+__device__ inline T block_sum(T v, T* lds /* >= BLOCK/64 */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  T r = 0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; ++i) r += lds[i];
+    lds[0] = r;
+  }
+  __syncthreads();
+  r = lds[0];
+  __syncthreads();
+  return r;
+}
+
+// Order-preserving map of an IEEE double to uint64 (total order, -0 < +0).
+__device__ inline uint64_t f64_key(double x) {
+  uint64_t b = __double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double key_f64(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double(b);
+}
+
+}  // namespace abc

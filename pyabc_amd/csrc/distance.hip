@@ -1,0 +1,157 @@
+// Batched summary-statistic distances, acceptance, and the synthetic batch
+// simulators used by the benchmark configurations.
+//
+// PNormDistance.__call__ (pyabc/distance/distance.py:76-102):
+//   d = pow( sum_{key in x_0 order} pow(|(f*w)[key] * (x[key] - x0[key])|, p), 1/p )
+//   p = inf: max_key |(f*w) (x - x0)|
+// UniformAcceptor (pyabc/acceptor/acceptor.py:235-244): accept iff d <= eps.
+//
+// Layout: statistics are STAT-MAJOR, stats_T[S][ld] with one column per
+// proposal, so lane b reads x[s, b] for s = 0..S-1 with fully coalesced rows;
+// the sum over keys is sequential in key order per lane (as the reference's
+// Python sum).  Powers p = 1, 2 use t, t*t and sqrt (the reference's glibc
+// pow differs from these by at most 1 ulp); the kernel flags every particle
+// whose distance lies within 4 ulp of eps (guard band), where that ulp could
+// flip the decision; parity tests assert the band is empty.
+#include "common.hpp"
+#include "philox.hpp"
+
+namespace abc {
+
+__device__ inline double ulp_of(double x) {
+  const double a = fabs(x);
+  return nextafter(a, INFINITY) - a;
+}
+
+template <int PMODE>  // 1: p=1, 2: p=2, 0: general p, 3: p=inf
+__global__ __launch_bounds__(256) void pnorm_kernel(
+    const double* __restrict__ stats_T, int64_t ld,
+    const double* __restrict__ x0, const double* __restrict__ fw, int64_t B,
+    int S, double p, double eps, double* __restrict__ d_out,
+    uint8_t* __restrict__ accept, uint8_t* __restrict__ guard) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double acc = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double t = fabs(fw[s] * (stats_T[static_cast<int64_t>(s) * ld + b] - x0[s]));
+    if (PMODE == 1)
+      acc += t;
+    else if (PMODE == 2)
+      acc += t * t;
+    else if (PMODE == 3)
+      acc = fmax(acc, t);
+    else
+      acc += pow(t, p);
+  }
+  double d;
+  if (PMODE == 1 || PMODE == 3)
+    d = acc;
+  else if (PMODE == 2)
+    d = sqrt(acc);
+  else
+    d = pow(acc, 1.0 / p);
+  d_out[b] = d;
+  if (accept) accept[b] = d <= eps ? 1 : 0;
+  if (guard) guard[b] = fabs(d - eps) <= 4.0 * ulp_of(eps) ? 1 : 0;
+}
+
+// y[s, b] = sum_k A[s, k] theta[b, k] + c[s] + sigma * z(b, s)
+// z(b, s) = philox_normal(seed, sid, (offset + b) * S + s)
+__global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
+    const double* __restrict__ theta, int64_t B, int d,
+    const double* __restrict__ A, const double* __restrict__ c, int S,
+    double sigma, uint64_t seed, uint64_t sid, uint64_t offset,
+    double* __restrict__ out_T, int64_t ld) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double th[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) th[k] = k < d ? theta[b * d + k] : 0.0;
+  const uint64_t base = (offset + static_cast<uint64_t>(b)) * static_cast<uint64_t>(S);
+  double zpair[2] = {0.0, 0.0};
+  uint64_t have = ~0ull;
+  for (int s = 0; s < S; ++s) {
+    double acc = c ? c[s] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < d) acc = fma(A[s * d + k], th[k], acc);
+    const uint64_t zi = base + s;
+    if ((zi >> 1) != have) {
+      box_muller(philox_block(seed, sid, zi >> 1), zpair[0], zpair[1]);
+      have = zi >> 1;
+    }
+    const double z = (zi & 1) ? zpair[1] : zpair[0];
+    out_T[static_cast<int64_t>(s) * ld + b] = acc + sigma * z;
+  }
+}
+
+// quickstart model (doc/examples/parameter_inference.ipynb cell 2):
+// y = mean + 0.5 * N(0,1), one statistic
+__global__ __launch_bounds__(256) void sim_gaussian_mean_kernel(
+    const double* __restrict__ theta, int64_t B, double sigma, uint64_t seed,
+    uint64_t sid, uint64_t offset, double* __restrict__ out) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t zi = offset + static_cast<uint64_t>(b);
+  double z0, z1;
+  box_muller(philox_block(seed, sid, zi >> 1), z0, z1);
+  out[b] = theta[b] + sigma * ((zi & 1) ? z1 : z0);
+}
+
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+int abc_pnorm_distance_f64(const double* stats_T, int64_t ld, const double* x0,
+                           const double* fw, int64_t B, int S, double p,
+                           double eps, double* d_out, uint8_t* accept,
+                           uint8_t* guard, hipStream_t st) {
+  ABC_REQUIRE(B >= 0 && S >= 0 && ld >= B, "pnorm: bad sizes");
+  ABC_REQUIRE(p >= 1.0, "pnorm: It must be p >= 1");
+  if (B == 0) return kOk;
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+  if (std::isinf(p))
+    hipLaunchKernelGGL(pnorm_kernel<3>, dim3(g), dim3(256), 0, st, stats_T, ld,
+                       x0, fw, B, S, p, eps, d_out, accept, guard);
+  else if (p == 1.0)
+    hipLaunchKernelGGL(pnorm_kernel<1>, dim3(g), dim3(256), 0, st, stats_T, ld,
+                       x0, fw, B, S, p, eps, d_out, accept, guard);
+  else if (p == 2.0)
+    hipLaunchKernelGGL(pnorm_kernel<2>, dim3(g), dim3(256), 0, st, stats_T, ld,
+                       x0, fw, B, S, p, eps, d_out, accept, guard);
+  else
+    hipLaunchKernelGGL(pnorm_kernel<0>, dim3(g), dim3(256), 0, st, stats_T, ld,
+                       x0, fw, B, S, p, eps, d_out, accept, guard);
+  ABC_LAUNCH_CHECK("pnorm_kernel");
+  return kOk;
+}
+
+int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
+                                const double* A, const double* c, int S,
+                                double sigma, uint64_t seed, uint64_t sid,
+                                uint64_t offset, double* out_T, int64_t ld,
+                                hipStream_t st) {
+  ABC_REQUIRE(d >= 1 && d <= 32 && S >= 1 && B >= 0 && ld >= B,
+              "sim_linear_gaussian: bad sizes (d <= 32)");
+  if (B == 0) return kOk;
+  hipLaunchKernelGGL(sim_linear_gaussian_kernel, dim3(ceil_div(B, 256)),
+                     dim3(256), 0, st, theta, B, d, A, c, S, sigma, seed, sid,
+                     offset, out_T, ld);
+  ABC_LAUNCH_CHECK("sim_linear_gaussian_kernel");
+  return kOk;
+}
+
+int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
+                              uint64_t seed, uint64_t sid, uint64_t offset,
+                              double* out, hipStream_t st) {
+  ABC_REQUIRE(B >= 0, "sim_gaussian_mean: bad sizes");
+  if (B == 0) return kOk;
+  hipLaunchKernelGGL(sim_gaussian_mean_kernel, dim3(ceil_div(B, 256)),
+                     dim3(256), 0, st, theta, B, sigma, seed, sid, offset, out);
+  ABC_LAUNCH_CHECK("sim_gaussian_mean_kernel");
+  return kOk;
+}
+
+}  // extern "C"

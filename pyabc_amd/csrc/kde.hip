@@ -1,0 +1,479 @@
+// KDE importance-weight pass: the O(M*N*d) transition density of
+// MultivariateNormalTransition.pdf (reference: pyabc/transition/
+// multivariatenormal.py:102-125, called per accepted particle from
+// pyabc/smc.py:722-733 and 776-792).
+//
+//   pd(theta_i) = sum_j w_j N(theta_i; X_j, cov)
+//               = exp(c) * sum_j 2^(lw2_j - |y_i - y_j|^2)      (*)
+//
+// with y = (x - mu) U sqrt(log2(e)/2) (U = scipy _PSD pseudo-inverse root of
+// cov, built on the host), lw2_j = log2 w_j - L, L = max_j log2 w_j and
+// c = ln2 L - (rank ln 2pi + log_pdet)/2.  The previous population is packed
+// once per generation as P[Npad][D+1] = (y_j, lw2_j) rows; padding rows have
+// lw2 = -1e30 so they contribute exactly 0.
+//
+// Main kernel (VALU-bound, no MFMA: D <= 32 is too thin): each thread keeps R
+// new rows y_i in VGPRs; the block's j-range streams through the SCALAR path
+// (wave-uniform s_load of P rows, SGPR operands of v_sub/v_fma), so there is
+// no LDS traffic and no barrier in the inner loop.  Per pair: D subs, D FMAs
+// (the first seeded with lw2_j), one v_exp_f32, one add.  fp32 sums are
+// flushed into fp64 every CH pairs.  The j-range is split over SPLIT blocks
+// (split index = block % SPLIT, so with SPLIT % 8 == 0 every XCD streams its
+// own j-ranges through its own L2), and per-split fp64 partials are summed in
+// fixed order by the finalize kernel (deterministic).  Rows whose sum falls
+// below 2^-60 (f32) are re-evaluated by an exact two-pass (max, then sum)
+// fixup kernel, so underflow of the fixed global offset never loses a row.
+#include "common.hpp"
+
+namespace abc {
+
+constexpr double kLn2 = 0.6931471805599453;
+constexpr float kPadLw = -1.0e30f;
+
+template <typename T>
+struct KdeCfg;
+template <>
+struct KdeCfg<float> {
+  static constexpr double underflow = 8.673617379884035e-19;  // 2^-60
+};
+template <>
+struct KdeCfg<double> {
+  static constexpr double underflow = 1.0e-280;
+};
+
+__device__ __forceinline__ float fast_exp2(float x) {
+  return __builtin_amdgcn_exp2f(x);
+}
+__device__ __forceinline__ double fast_exp2(double x) { return exp2(x); }
+
+// ---------------------------------------------------------------------------
+// packing: whitening of new rows and of the previous population
+// ---------------------------------------------------------------------------
+template <typename T, int D>
+__global__ __launch_bounds__(256) void whiten_kernel(
+    const double* __restrict__ X, int64_t n, int d,
+    const double* __restrict__ mu, const double* __restrict__ Us,
+    T* __restrict__ Y, int ldy) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double xc[D];
+#pragma unroll
+  for (int l = 0; l < D; ++l) xc[l] = l < d ? X[i * d + l] - mu[l] : 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < D; ++l)
+      if (l < d && k < d) acc = fma(xc[l], Us[l * d + k], acc);
+    Y[i * ldy + k] = static_cast<T>(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void max_key_kernel(
+    const double* __restrict__ w, int64_t n,
+    unsigned long long* __restrict__ out_key) {
+  uint64_t m = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    m = max(m, f64_key(w[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t u = __shfl_xor(m, o, 64);
+    m = u > m ? u : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out_key, static_cast<unsigned long long>(m));
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void pack_prev_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    int d, const double* __restrict__ mu, const double* __restrict__ Us,
+    T* __restrict__ P, int64_t npad,
+    const unsigned long long* __restrict__ max_key,
+    double* __restrict__ lw2max_out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const double L = log2(key_f64(*max_key));
+  if (i == 0 && lw2max_out) *lw2max_out = L;
+  if (i >= npad) return;
+  T* row = P + i * (D + 1);
+  if (i >= n) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) row[k] = T(0);
+    row[D] = static_cast<T>(kPadLw);
+    return;
+  }
+  double xc[D];
+#pragma unroll
+  for (int l = 0; l < D; ++l) xc[l] = l < d ? X[i * d + l] - mu[l] : 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < D; ++l)
+      if (l < d && k < d) acc = fma(xc[l], Us[l * d + k], acc);
+    row[k] = static_cast<T>(acc);
+  }
+  const double wi = w[i];
+  double lw = wi > 0.0 ? log2(wi) - L : -1.0e300;
+  if (lw < static_cast<double>(kPadLw)) lw = kPadLw;
+  row[D] = static_cast<T>(lw);
+}
+
+// ---------------------------------------------------------------------------
+// main pass
+// ---------------------------------------------------------------------------
+template <typename T, int D, int R, int U, int CH>
+__global__ __launch_bounds__(256) void kde_main_kernel(
+    const T* __restrict__ Ynew, int64_t M, const T* __restrict__ P,
+    int64_t npad, int split, int64_t jchunk, double* __restrict__ partial) {
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t rows_per_block = 256 * R;
+  const int64_t j0 = static_cast<int64_t>(s) * jchunk;
+  int64_t j1 = j0 + jchunk;
+  if (j1 > npad) j1 = npad;
+
+  T yi[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int64_t row = rb * rows_per_block + r * 256 + threadIdx.x;
+    if (row >= M) row = M - 1;
+#pragma unroll
+    for (int k = 0; k < D; ++k) yi[r][k] = Ynew[row * D + k];
+  }
+  double S[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) S[r] = 0.0;
+
+  for (int64_t jc = j0; jc < j1; jc += CH) {
+    int64_t je = jc + CH;
+    if (je > j1) je = j1;
+    T sacc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) sacc[r] = T(0);
+    for (int64_t j = jc; j < je; j += U) {
+      const T* __restrict__ pj = P + j * (D + 1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const T lw = pj[u * (D + 1) + D];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          T acc = lw;
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const T df = yi[r][k] - pj[u * (D + 1) + k];
+            acc = fma(-df, df, acc);
+          }
+          sacc[r] += fast_exp2(acc);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) S[r] += static_cast<double>(sacc[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = rb * rows_per_block + r * 256 + threadIdx.x;
+    if (row < M) partial[static_cast<int64_t>(s) * M + row] = S[r];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void kde_finalize_kernel(
+    const double* __restrict__ partial, int64_t M, int split,
+    const double* __restrict__ lw2max, double log_const,
+    double* __restrict__ out_logpd, int* __restrict__ n_fix,
+    int* __restrict__ fix_rows) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  double S = 0.0;
+  for (int s = 0; s < split; ++s) S += partial[static_cast<int64_t>(s) * M + i];
+  const double off = kLn2 * (*lw2max) + log_const;
+  if (!(S >= KdeCfg<T>::underflow)) {
+    const int slot = atomicAdd(n_fix, 1);
+    fix_rows[slot] = static_cast<int>(i);
+    out_logpd[i] = -INFINITY;
+  } else {
+    out_logpd[i] = log(S) + off;
+  }
+}
+
+// exact two-pass evaluation for rows whose fixed-offset sum underflowed
+template <typename T, int D>
+__global__ __launch_bounds__(256) void kde_fixup_kernel(
+    const T* __restrict__ Ynew, const T* __restrict__ P, int64_t npad,
+    const double* __restrict__ lw2max, double log_const,
+    const int* __restrict__ n_fix, const int* __restrict__ fix_rows,
+    double* __restrict__ out_logpd) {
+  __shared__ double red[4];
+  const int count = *n_fix;
+  const double off = kLn2 * (*lw2max) + log_const;
+  for (int f = blockIdx.x; f < count; f += gridDim.x) {
+    const int64_t i = fix_rows[f];
+    T yi[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) yi[k] = Ynew[i * D + k];
+    double m = -INFINITY;
+    for (int64_t j = threadIdx.x; j < npad; j += 256) {
+      const T* pj = P + j * (D + 1);
+      T acc = pj[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const T df = yi[k] - pj[k];
+        acc = fma(-df, df, acc);
+      }
+      m = fmax(m, static_cast<double>(acc));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    double sum = 0.0;
+    if (m > -1.0e29) {
+      for (int64_t j = threadIdx.x; j < npad; j += 256) {
+        const T* pj = P + j * (D + 1);
+        T acc = pj[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const T df = yi[k] - pj[k];
+          acc = fma(-df, df, acc);
+        }
+        sum += exp2(static_cast<double>(acc) - m);
+      }
+    }
+    sum = block_sum<double, 256>(sum, red);
+    if (threadIdx.x == 0)
+      out_logpd[i] = (m > -1.0e29) ? kLn2 * (m + log2(sum)) + off : -INFINITY;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static int padded_dim(int d) {
+  static const int dims[] = {1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32};
+  for (int v : dims)
+    if (d <= v) return v;
+  return -1;
+}
+
+constexpr int kRowPad = 64;  // Npad multiple (>= U, == CH)
+constexpr int kCH = 64;
+
+template <int D>
+struct RowsPerThread {
+  static constexpr int value = D <= 8 ? 4 : 2;
+};
+
+struct Plan {
+  int split;
+  int64_t jchunk;
+  int64_t row_blocks;
+};
+
+template <int D>
+static Plan make_plan(int64_t M, int64_t npad) {
+  constexpr int R = RowsPerThread<D>::value;
+  Plan p;
+  p.row_blocks = ceil_div(M, 256 * R);
+  const int64_t target_blocks = 8192;  // ~4 waves of 2048 resident blocks
+  int64_t split = ceil_div(target_blocks, p.row_blocks);
+  if (split > 8) split = ceil_div(split, 8) * 8;  // XCD-aligned
+  const int64_t max_split = npad / kCH;
+  if (split > max_split) split = max_split;
+  if (split < 1) split = 1;
+  p.split = static_cast<int>(split);
+  p.jchunk = ceil_div(ceil_div(npad, split), kCH) * kCH;
+  return p;
+}
+
+template <typename T>
+static size_t ws_bytes_impl(int64_t M, int64_t npad, int d) {
+  // partial[split*M] doubles + n_fix (16 B) + fix_rows[M] ints
+  const int D = padded_dim(d);
+  if (D < 0) return 0;
+  int64_t split;
+  switch (D) {
+#define CASE(DD) \
+  case DD: split = make_plan<DD>(M, npad).split; break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default: return 0;
+  }
+  return static_cast<size_t>(split * M) * 8 + 16 + static_cast<size_t>(M) * 4 + 256;
+}
+
+template <typename T, int D>
+static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
+                       const double* lw2max, double log_const,
+                       double* out_logpd, void* ws, size_t ws_bytes,
+                       hipStream_t stream) {
+  constexpr int R = RowsPerThread<D>::value;
+  const Plan p = make_plan<D>(M, npad);
+  const size_t need = static_cast<size_t>(p.split * M) * 8 + 16 +
+                      static_cast<size_t>(M) * 4;
+  ABC_REQUIRE(ws_bytes >= need, "kde: workspace too small (%zu < %zu)",
+              ws_bytes, need);
+  char* base = static_cast<char*>(ws);
+  double* partial = reinterpret_cast<double*>(base);
+  int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.split * M) * 8);
+  int* fix_rows = n_fix + 4;
+  ABC_HIP(hipMemsetAsync(n_fix, 0, 16, stream));
+  const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
+  hipLaunchKernelGGL((kde_main_kernel<T, D, R, 2, kCH>), dim3(grid), dim3(256),
+                     0, stream, Ynew, M, P, npad, p.split, p.jchunk, partial);
+  ABC_LAUNCH_CHECK("kde_main_kernel");
+  hipLaunchKernelGGL((kde_finalize_kernel<T>), dim3(ceil_div(M, 256)),
+                     dim3(256), 0, stream, partial, M, p.split, lw2max,
+                     log_const, out_logpd, n_fix, fix_rows);
+  ABC_LAUNCH_CHECK("kde_finalize_kernel");
+  hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(64), dim3(256), 0, stream,
+                     Ynew, P, npad, lw2max, log_const, n_fix, fix_rows,
+                     out_logpd);
+  ABC_LAUNCH_CHECK("kde_fixup_kernel");
+  return kOk;
+}
+
+template <typename T>
+static int logpdf_dispatch(const T* Ynew, int64_t M, const T* P, int64_t npad,
+                           int d, const double* lw2max, double log_const,
+                           double* out, void* ws, size_t wsb,
+                           hipStream_t st) {
+  ABC_REQUIRE(M >= 0 && npad >= 0, "kde: negative size");
+  ABC_REQUIRE(npad % kRowPad == 0, "kde: npad must be a multiple of %d", kRowPad);
+  if (M == 0) return kOk;
+  ABC_REQUIRE(npad > 0, "kde: empty previous population");
+  ABC_REQUIRE(Ynew && P && lw2max && out && ws, "kde: null pointer");
+  switch (padded_dim(d)) {
+#define CASE(DD) \
+  case DD:       \
+    return logpdf_impl<T, DD>(Ynew, M, P, npad, lw2max, log_const, out, ws, wsb, st);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default:
+      set_error("kde: unsupported dimension d=%d (max 32)", d);
+      return kUnsupported;
+  }
+}
+
+template <typename T>
+static int whiten_dispatch(const double* X, int64_t n, int d, const double* mu,
+                           const double* Us, T* Y, hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "whiten: negative n");
+  if (n == 0) return kOk;
+  const int D = padded_dim(d);
+  const unsigned g = static_cast<unsigned>(ceil_div(n, 256));
+  switch (D) {
+#define CASE(DD)                                                             \
+  case DD:                                                                   \
+    hipLaunchKernelGGL((whiten_kernel<T, DD>), dim3(g), dim3(256), 0, st, X, \
+                       n, d, mu, Us, Y, DD);                                 \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default:
+      set_error("whiten: unsupported dimension d=%d", d);
+      return kUnsupported;
+  }
+  ABC_LAUNCH_CHECK("whiten_kernel");
+  return kOk;
+}
+
+template <typename T>
+static int pack_dispatch(const double* X, const double* w, int64_t n, int d,
+                         const double* mu, const double* Us, T* P,
+                         int64_t npad, double* lw2max, void* ws,
+                         hipStream_t st) {
+  ABC_REQUIRE(n > 0 && npad >= n && npad % kRowPad == 0,
+              "pack_prev: need 0 < n <= npad, npad %% %d == 0", kRowPad);
+  ABC_REQUIRE(ws != nullptr, "pack_prev: null workspace");
+  unsigned long long* key = static_cast<unsigned long long*>(ws);
+  ABC_HIP(hipMemsetAsync(key, 0, 8, st));
+  hipLaunchKernelGGL(max_key_kernel, dim3(stream_grid(n, 256, 1024)),
+                     dim3(256), 0, st, w, n, key);
+  ABC_LAUNCH_CHECK("max_key_kernel");
+  const unsigned g = static_cast<unsigned>(ceil_div(npad, 256));
+  switch (padded_dim(d)) {
+#define CASE(DD)                                                            \
+  case DD:                                                                  \
+    hipLaunchKernelGGL((pack_prev_kernel<T, DD>), dim3(g), dim3(256), 0, st, \
+                       X, w, n, d, mu, Us, P, npad, key, lw2max);           \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default:
+      set_error("pack_prev: unsupported dimension d=%d", d);
+      return kUnsupported;
+  }
+  ABC_LAUNCH_CHECK("pack_prev_kernel");
+  return kOk;
+}
+
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+int abc_kde_padded_dim(int d) { return padded_dim(d); }
+int abc_kde_row_pad(void) { return kRowPad; }
+
+size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d) {
+  return ws_bytes_impl<float>(M, npad, d);
+}
+
+int abc_kde_split(int64_t M, int64_t npad, int d) {
+  switch (padded_dim(d)) {
+#define CASE(DD) \
+  case DD: return make_plan<DD>(M, npad).split;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default: return -1;
+  }
+}
+
+int abc_whiten_f32(const double* X, int64_t n, int d, const double* mu,
+                   const double* Us, float* Y, hipStream_t st) {
+  return whiten_dispatch<float>(X, n, d, mu, Us, Y, st);
+}
+int abc_whiten_f64(const double* X, int64_t n, int d, const double* mu,
+                   const double* Us, double* Y, hipStream_t st) {
+  return whiten_dispatch<double>(X, n, d, mu, Us, Y, st);
+}
+
+int abc_kde_pack_prev_f32(const double* X, const double* w, int64_t n, int d,
+                          const double* mu, const double* Us, float* P,
+                          int64_t npad, double* lw2max, void* ws,
+                          hipStream_t st) {
+  return pack_dispatch<float>(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
+}
+int abc_kde_pack_prev_f64(const double* X, const double* w, int64_t n, int d,
+                          const double* mu, const double* Us, double* P,
+                          int64_t npad, double* lw2max, void* ws,
+                          hipStream_t st) {
+  return pack_dispatch<double>(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
+}
+
+int abc_kde_logpdf_f32(const float* Ynew, int64_t M, const float* P,
+                       int64_t npad, int d, const double* lw2max,
+                       double log_const, double* out_logpd, void* ws,
+                       size_t ws_bytes, hipStream_t st) {
+  return logpdf_dispatch<float>(Ynew, M, P, npad, d, lw2max, log_const,
+                                out_logpd, ws, ws_bytes, st);
+}
+int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
+                       int64_t npad, int d, const double* lw2max,
+                       double log_const, double* out_logpd, void* ws,
+                       size_t ws_bytes, hipStream_t st) {
+  return logpdf_dispatch<double>(Ynew, M, P, npad, d, lw2max, log_const,
+                                 out_logpd, ws, ws_bytes, st);
+}
+
+}  // extern "C"

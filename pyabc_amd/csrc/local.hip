@@ -1,0 +1,498 @@
+// LocalTransition (reference: pyabc/transition/local_transition.py:13-145):
+//   fit:  nbr = cKDTree(X).query(X, k+1)[:, 1:]                       (:82-83)
+//         C_n = np.cov(X[nbr_n] - X_n, aweights = w[nbr_n]/sum) * scaling
+//         (|sum C| == 0 -> C_kk = |X_0k|); while det(C) <= 0: C += 1e-3 I
+//         inv_n = inv(C_n), det_n                                     (:112-139)
+//   pdf:  sum_n w_n exp(-q_n/2) / sqrt((2 pi)^d det_n) / sum w,
+//         q_n = (theta - X_n)^T inv_n (theta - X_n)                   (:103-110)
+//
+// kNN: fp64 squared distances (sequential over dimensions, no FMA
+// contraction, as the reference tree computes them), one WAVE per group of
+// R rows; candidate tiles of X are staged in LDS and shared by the block's
+// waves; every lane tests one candidate against the R rows and appends it to
+// the row's LDS buffer when it beats the row's current k-th distance tau;
+// a full buffer is bitonic-sorted by the wave and cut back to k (tau shrinks),
+// so the kernel makes ONE pass over the candidates.  k <= kMaxK.
+// cov/det/inv: one thread per particle, weighted moments of the k neighbour
+// deltas, LU with partial pivoting for det and inverse (fp64).
+// pdf: one thread per evaluation point; the previous population's
+// (X_n, inv_n, log(w_n / norm_n)) stream through the scalar path (wave-
+// uniform), d^2 FMAs per pair for the quadratic form, online log-sum-exp
+// in fp64.
+#include "common.hpp"
+
+namespace abc {
+
+constexpr int kKnnRows = 8;     // rows per wave
+constexpr int kKnnWaves = 4;    // waves per block
+constexpr int kKnnCap = 256;    // buffer capacity per row (power of two)
+constexpr int kMaxK = kKnnCap - 64;
+constexpr int kKnnTile = 256;   // candidates staged per LDS tile
+
+__device__ inline double dsub(double a, double b) { return __dsub_rn(a, b); }
+__device__ inline double dadd(double a, double b) { return __dadd_rn(a, b); }
+__device__ inline double dmul(double a, double b) { return __dmul_rn(a, b); }
+
+// bitonic sort (ascending by d2, ties by index) of one row buffer by a wave
+__device__ inline void wave_bitonic(double* bd, int* bi, int lane) {
+  for (int size = 2; size <= kKnnCap; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = lane; t < kKnnCap / 2; t += 64) {
+        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const double a = bd[lo], b = bd[hi];
+        const int ia = bi[lo], ib = bi[hi];
+        const bool gt = (a > b) || (a == b && ia > ib);
+        if (gt == up) {
+          bd[lo] = b;
+          bd[hi] = a;
+          bi[lo] = ib;
+          bi[hi] = ia;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void knn_kernel(const double* __restrict__ X,
+                                                  int64_t N, int k,
+                                                  int32_t* __restrict__ nbr,
+                                                  double* __restrict__ nbr_d2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* tile = reinterpret_cast<double*>(smem);                 // [kKnnTile][D]
+  double* bufd = tile + kKnnTile * D;                              // [rows][cap]
+  int* bufi = reinterpret_cast<int*>(bufd + kKnnWaves * kKnnRows * kKnnCap);
+  int* bufn = bufi + kKnnWaves * kKnnRows * kKnnCap;               // [rows]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kKnnWaves + wid) * kKnnRows;
+
+  double xr[kKnnRows][D];
+  double tau[kKnnRows];
+#pragma unroll
+  for (int r = 0; r < kKnnRows; ++r) {
+    const int64_t row = row0 + r < N ? row0 + r : N - 1;
+#pragma unroll
+    for (int q = 0; q < D; ++q) xr[r][q] = X[row * D + q];
+    tau[r] = INFINITY;
+  }
+  double* myd = bufd + wid * kKnnRows * kKnnCap;
+  int* myi = bufi + wid * kKnnRows * kKnnCap;
+  int* myn = bufn + wid * kKnnRows;
+  if (lane < kKnnRows) myn[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+
+  for (int64_t base = 0; base < N; base += kKnnTile) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < kKnnTile * D; t += 256) {
+      const int64_t j = base + t / D;
+      tile[t] = j < N ? X[base * D + t] : 0.0;
+    }
+    __syncthreads();
+    for (int c0 = 0; c0 < kKnnTile; c0 += 64) {
+      const int64_t j = base + c0 + lane;
+      const bool valid = j < N;
+      double xj[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) xj[q] = tile[(c0 + lane) * D + q];
+#pragma unroll
+      for (int r = 0; r < kKnnRows; ++r) {
+        double d2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          const double df = dsub(xj[q], xr[r][q]);
+          d2 = dadd(d2, dmul(df, df));
+        }
+        const bool take = valid && j != row0 + r && d2 < tau[r];
+        const uint64_t m = __ballot(take);
+        if (m) {
+          int cnt = myn[r];
+          if (cnt + __popcll(m) > kKnnCap) {
+            // sort + cut back to k, shrinking tau; pad with +inf
+            for (int t = cnt + lane; t < kKnnCap; t += 64) {
+              myd[r * kKnnCap + t] = INFINITY;
+              myi[r * kKnnCap + t] = 0x7fffffff;
+            }
+            __builtin_amdgcn_wave_barrier();
+            wave_bitonic(myd + r * kKnnCap, myi + r * kKnnCap, lane);
+            cnt = k;
+            tau[r] = myd[r * kKnnCap + k - 1];
+            if (lane == 0) myn[r] = k;
+            __builtin_amdgcn_wave_barrier();
+          }
+          const bool take2 = take && d2 < tau[r];
+          const uint64_t m2 = __ballot(take2);
+          const int pos = cnt + __popcll(m2 & ((1ull << lane) - 1ull));
+          if (take2) {
+            myd[r * kKnnCap + pos] = d2;
+            myi[r * kKnnCap + pos] = static_cast<int>(j);
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) myn[r] = cnt + __popcll(m2);
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    }
+  }
+  // final selection
+  for (int r = 0; r < kKnnRows; ++r) {
+    const int64_t row = row0 + r;
+    const int cnt = myn[r];
+    for (int t = cnt + lane; t < kKnnCap; t += 64) {
+      myd[r * kKnnCap + t] = INFINITY;
+      myi[r * kKnnCap + t] = 0x7fffffff;
+    }
+    __builtin_amdgcn_wave_barrier();
+    wave_bitonic(myd + r * kKnnCap, myi + r * kKnnCap, lane);
+    if (row < N) {
+      for (int t = lane; t < k; t += 64) {
+        nbr[row * k + t] = myi[r * kKnnCap + t];
+        if (nbr_d2) nbr_d2[row * k + t] = myd[r * kKnnCap + t];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ inline double lu_det_inv(double (&a)[D][D], double (&inv)[D][D],
+                                    int d, bool want_inv) {
+  int piv[D];
+  double det = 1.0;
+  for (int i = 0; i < d; ++i) piv[i] = i;
+  for (int c = 0; c < d; ++c) {
+    int p = c;
+    double best = fabs(a[c][c]);
+    for (int r = c + 1; r < d; ++r)
+      if (fabs(a[r][c]) > best) {
+        best = fabs(a[r][c]);
+        p = r;
+      }
+    if (p != c) {
+      for (int q = 0; q < d; ++q) {
+        const double t = a[c][q];
+        a[c][q] = a[p][q];
+        a[p][q] = t;
+      }
+      const int t = piv[c];
+      piv[c] = piv[p];
+      piv[p] = t;
+      det = -det;
+    }
+    const double diag = a[c][c];
+    det *= diag;
+    if (diag == 0.0) continue;
+    for (int r = c + 1; r < d; ++r) {
+      const double f = a[r][c] / diag;
+      a[r][c] = f;
+      for (int q = c + 1; q < d; ++q) a[r][q] = fma(-f, a[c][q], a[r][q]);
+    }
+  }
+  if (want_inv) {
+    for (int col = 0; col < d; ++col) {
+      double y[D];
+      for (int i = 0; i < d; ++i) {
+        double s = piv[i] == col ? 1.0 : 0.0;
+        for (int q = 0; q < i; ++q) s = fma(-a[i][q], y[q], s);
+        y[i] = s;
+      }
+      for (int i = d - 1; i >= 0; --i) {
+        double s = y[i];
+        for (int q = i + 1; q < d; ++q) s = fma(-a[i][q], inv[q][col], s);
+        inv[i][col] = s / a[i][i];
+      }
+    }
+  }
+  return det;
+}
+
+template <int D>
+__global__ __launch_bounds__(128) void local_cov_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t N,
+    int d, const int32_t* __restrict__ nbr, int k, double scaling,
+    double* __restrict__ covs, double* __restrict__ invs,
+    double* __restrict__ dets) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double xn[D];
+  for (int q = 0; q < d; ++q) xn[q] = X[n * d + q];
+  // local weights lw = w[nbr] / sum
+  double sw = 0.0;
+  for (int t = 0; t < k; ++t) sw += w[nbr[n * k + t]];
+  double v1 = 0.0, v2 = 0.0, mu[D];
+  for (int q = 0; q < d; ++q) mu[q] = 0.0;
+  for (int t = 0; t < k; ++t) {
+    const int64_t j = nbr[n * k + t];
+    const double lw = w[j] / sw;
+    v1 += lw;
+    v2 += lw * lw;
+    for (int q = 0; q < d; ++q) mu[q] = fma(lw, X[j * d + q] - xn[q], mu[q]);
+  }
+  for (int q = 0; q < d; ++q) mu[q] /= v1;
+  double C[D][D];
+  for (int a = 0; a < d; ++a)
+    for (int b = 0; b < d; ++b) C[a][b] = 0.0;
+  for (int t = 0; t < k; ++t) {
+    const int64_t j = nbr[n * k + t];
+    const double lw = w[j] / sw;
+    double dl[D];
+    for (int q = 0; q < d; ++q) dl[q] = (X[j * d + q] - xn[q]) - mu[q];
+    for (int a = 0; a < d; ++a)
+      for (int b = a; b < d; ++b) C[a][b] = fma(lw * dl[a], dl[b], C[a][b]);
+  }
+  double fact = v1 - v2 / v1;
+  if (fact <= 0.0) fact = 0.0;
+  double csum = 0.0;
+  for (int a = 0; a < d; ++a)
+    for (int b = a; b < d; ++b) {
+      C[a][b] = C[a][b] * (1.0 / fact);
+      C[b][a] = C[a][b];
+    }
+  if (k == 1) {  // smart_cov of ONE delta row: diag(|delta_0|) (util.py:8-11)
+    const int64_t j = nbr[n * k];
+    for (int a = 0; a < d; ++a)
+      for (int b = 0; b < d; ++b)
+        C[a][b] = a == b ? fabs(X[j * d + a] - xn[a]) : 0.0;
+  }
+  for (int a = 0; a < d; ++a)
+    for (int b = 0; b < d; ++b) csum += C[a][b];
+  if (fabs(csum) == 0.0)
+    for (int q = 0; q < d; ++q) C[q][q] = fabs(X[q]);
+  for (int a = 0; a < d; ++a)
+    for (int b = 0; b < d; ++b) C[a][b] *= scaling;
+  double work[D][D], inv[D][D];
+  double det;
+  for (int it = 0; it < 100000; ++it) {
+    for (int a = 0; a < d; ++a)
+      for (int b = 0; b < d; ++b) work[a][b] = C[a][b];
+    det = lu_det_inv<D>(work, inv, d, false);
+    if (!(det <= 0.0)) break;  // reference: while det <= 0 (NaN exits)
+    for (int q = 0; q < d; ++q) C[q][q] += 1e-3;
+  }
+  for (int a = 0; a < d; ++a)
+    for (int b = 0; b < d; ++b) work[a][b] = C[a][b];
+  lu_det_inv<D>(work, inv, d, true);
+  for (int a = 0; a < d; ++a)
+    for (int b = 0; b < d; ++b) {
+      covs[n * d * d + a * d + b] = C[a][b];
+      invs[n * d * d + a * d + b] = inv[a][b];
+    }
+  dets[n] = det;
+}
+
+// per-previous-particle constant: lc_n = log(w_n) - 0.5 (d log 2pi + log det_n)
+__global__ __launch_bounds__(256) void local_const_kernel(const double* __restrict__ w,
+                                                          const double* __restrict__ dets,
+                                                          int64_t N, int d,
+                                                          double* __restrict__ lc) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (n >= N) return;
+  const double norm = sqrt(pow(2.0 * 3.141592653589793, d) * dets[n]);
+  lc[n] = w[n] > 0.0 ? log(w[n] / norm) : -INFINITY;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void local_pdf_kernel(
+    const double* __restrict__ pts, int64_t M, const double* __restrict__ X,
+    const double* __restrict__ invs, const double* __restrict__ lc, int64_t N,
+    int split, int64_t nchunk, double* __restrict__ part_m,
+    double* __restrict__ part_s) {
+  const int s = blockIdx.x % split;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
+  const int64_t i = i0 < M ? i0 : M - 1;
+  double th[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
+  double m = -INFINITY, acc = 0.0;
+  const int64_t n0 = static_cast<int64_t>(s) * nchunk;
+  int64_t n1 = n0 + nchunk;
+  if (n1 > N) n1 = N;
+  for (int64_t n = n0; n < n1; ++n) {
+    double dl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
+    double qf = 0.0;
+    const double* A = invs + n * D * D;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      double r = 0.0;
+#pragma unroll
+      for (int b = 0; b < D; ++b) r = fma(A[a * D + b], dl[b], r);
+      qf = fma(dl[a], r, qf);
+    }
+    const double e = lc[n] - 0.5 * qf;
+    if (e > m) {
+      acc = acc * exp(m - e) + 1.0;
+      m = e;
+    } else {
+      acc += exp(e - m);
+    }
+  }
+  if (i0 < M) {
+    part_m[static_cast<int64_t>(s) * M + i0] = m;
+    part_s[static_cast<int64_t>(s) * M + i0] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void local_pdf_final_kernel(
+    const double* __restrict__ part_m, const double* __restrict__ part_s,
+    int64_t M, int split, const double* __restrict__ logsumw,
+    double* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= M) return;
+  double m = -INFINITY;
+  for (int s = 0; s < split; ++s) m = fmax(m, part_m[s * M + i]);
+  double acc = 0.0;
+  if (m > -INFINITY)
+    for (int s = 0; s < split; ++s) {
+      const double ms = part_m[s * M + i];
+      if (ms > -INFINITY) acc += part_s[s * M + i] * exp(ms - m);
+    }
+  out[i] = (m > -INFINITY ? m + log(acc) : -INFINITY) - *logsumw;
+}
+
+__global__ void log_kernel(double* x) { *x = log(*x); }
+
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+size_t abc_knn_workspace_bytes(int64_t N, int k) {
+  (void)N;
+  (void)k;
+  return 0;
+}
+
+int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
+                double* nbr_d2, void* ws, size_t ws_bytes, hipStream_t st) {
+  (void)ws;
+  (void)ws_bytes;
+  ABC_REQUIRE(N > 1 && k >= 1 && k <= N - 1, "knn: need 1 <= k <= N-1");
+  ABC_REQUIRE(k <= kMaxK, "knn: k=%d exceeds the one-pass limit %d", k, kMaxK);
+  const unsigned grid = static_cast<unsigned>(ceil_div(N, kKnnRows * kKnnWaves));
+  const int rows = kKnnWaves * kKnnRows;
+#define L(DD)                                                                  \
+  {                                                                            \
+    const size_t lds = kKnnTile * DD * 8 + rows * kKnnCap * 12 + rows * 4;     \
+    hipLaunchKernelGGL((knn_kernel<DD>), dim3(grid), dim3(256), lds, st, X, N, \
+                       k, nbr, nbr_d2);                                        \
+  }
+  switch (d) {
+    case 1: L(1) break;
+    case 2: L(2) break;
+    case 3: L(3) break;
+    case 4: L(4) break;
+    case 5: L(5) break;
+    case 6: L(6) break;
+    case 7: L(7) break;
+    case 8: L(8) break;
+    default:
+      set_error("knn: unsupported d=%d (d <= 8)", d);
+      return kUnsupported;
+  }
+#undef L
+  ABC_LAUNCH_CHECK("knn_kernel");
+  return kOk;
+}
+
+int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
+                      const int32_t* nbr, int k, double scaling, double* covs,
+                      double* inv_covs, double* dets, hipStream_t st) {
+  ABC_REQUIRE(N >= 1 && k >= 1, "local_cov: bad sizes");
+  const unsigned g = static_cast<unsigned>(ceil_div(N, 128));
+#define L(DD)                                                                   \
+  hipLaunchKernelGGL((local_cov_kernel<DD>), dim3(g), dim3(128), 0, st, X, w, N, \
+                     d, nbr, k, scaling, covs, inv_covs, dets);
+  if (d <= 4) {
+    L(4)
+  } else if (d <= 8) {
+    L(8)
+  } else if (d <= 16) {
+    L(16)
+  } else {
+    set_error("local_cov: unsupported d=%d (d <= 16)", d);
+    return kUnsupported;
+  }
+#undef L
+  ABC_LAUNCH_CHECK("local_cov_kernel");
+  return kOk;
+}
+
+static void local_plan(int64_t M, int64_t N, int& split, int64_t& nchunk) {
+  const int64_t row_blocks = ceil_div(M, 256);
+  int64_t sp = ceil_div(4096, row_blocks);
+  if (sp > 64) sp = 64;
+  if (sp > N) sp = N;
+  if (sp < 1) sp = 1;
+  split = static_cast<int>(sp);
+  nchunk = ceil_div(N, sp);
+}
+
+size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N) {
+  int split;
+  int64_t nchunk;
+  local_plan(M > 0 ? M : 1, N > 0 ? N : 1, split, nchunk);
+  return static_cast<size_t>(N) * 8 + static_cast<size_t>(split) * M * 16 + 512;
+}
+
+__global__ __launch_bounds__(256) void local_sumw_kernel(const double* __restrict__ w,
+                                                         int64_t N,
+                                                         double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += 256) s += w[i];
+  s = block_sum<double, 256>(s, red);
+  if (threadIdx.x == 0) *out = log(s);
+}
+
+int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
+                         const double* w, const double* inv_covs,
+                         const double* dets, int64_t N, int d,
+                         double* out_logpdf, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  ABC_REQUIRE(M >= 0 && N >= 1, "local_logpdf: bad sizes");
+  if (M == 0) return kOk;
+  ABC_REQUIRE(ws_bytes >= abc_local_logpdf_workspace_bytes(M, N),
+              "local_logpdf: workspace too small");
+  int split;
+  int64_t nchunk;
+  local_plan(M, N, split, nchunk);
+  char* base = static_cast<char*>(ws);
+  double* logsumw = reinterpret_cast<double*>(base);
+  double* lc = logsumw + 8;
+  double* part_m = lc + N;
+  double* part_s = part_m + static_cast<int64_t>(split) * M;
+  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
+  hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
+                     st, w, dets, N, d, lc);
+  const unsigned grid = static_cast<unsigned>(ceil_div(M, 256) * split);
+#define L(DD)                                                                  \
+  hipLaunchKernelGGL((local_pdf_kernel<DD>), dim3(grid), dim3(256), 0, st, pts, \
+                     M, X, inv_covs, lc, N, split, nchunk, part_m, part_s);
+  switch (d) {
+    case 1: L(1) break;
+    case 2: L(2) break;
+    case 3: L(3) break;
+    case 4: L(4) break;
+    case 5: L(5) break;
+    case 6: L(6) break;
+    case 7: L(7) break;
+    case 8: L(8) break;
+    default:
+      set_error("local_logpdf: unsupported d=%d (d <= 8)", d);
+      return kUnsupported;
+  }
+#undef L
+  hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),
+                     0, st, part_m, part_s, M, split, logsumw, out_logpdf);
+  ABC_LAUNCH_CHECK("local_logpdf kernels");
+  return kOk;
+}
+
+}  // extern "C"

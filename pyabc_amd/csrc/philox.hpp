@@ -1,0 +1,63 @@
+// Philox4x32-10 counter-based RNG (Salmon, Moraes, Dror, Shaw, SC'11).
+//
+// Stream layout shared with oracle/ref_cpu.py (philox_block/philox_uniform/
+// philox_normal): block i of stream s under seed k is
+//   counter = (i_lo, i_hi, s_lo, s_hi), key = (k_lo, k_hi).
+// Uniform u[i] takes words (0,1) of block i/2 for even i and (2,3) for odd i,
+// as a 53-bit value (hi << 21 | lo >> 11) * 2^-53 in [0,1).
+// Normal z[i] is Box-Muller on block i/2: u1 = 1 - U(w0,w1) in (0,1],
+// u2 = U(w2,w3); even i -> r cos(2 pi u2), odd i -> r sin(2 pi u2).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace abc {
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0,
+                                                uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = static_cast<uint64_t>(M0) * c.x;
+    const uint64_t p1 = static_cast<uint64_t>(M1) * c.z;
+    const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32);
+    const uint32_t lo0 = static_cast<uint32_t>(p0);
+    const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32);
+    const uint32_t lo1 = static_cast<uint32_t>(p1);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+__host__ __device__ inline u32x4 philox_block(uint64_t seed, uint64_t stream,
+                                               uint64_t i) {
+  u32x4 c{static_cast<uint32_t>(i), static_cast<uint32_t>(i >> 32),
+          static_cast<uint32_t>(stream), static_cast<uint32_t>(stream >> 32)};
+  return philox4x32_10(c, static_cast<uint32_t>(seed),
+                       static_cast<uint32_t>(seed >> 32));
+}
+
+__host__ __device__ inline double u53(uint32_t hi, uint32_t lo) {
+  const uint64_t v = (static_cast<uint64_t>(hi) << 21) | (lo >> 11);
+  return static_cast<double>(v) * (1.0 / 9007199254740992.0);
+}
+
+// pair of normals (cos branch, sin branch) from one Philox block
+__device__ inline void box_muller(u32x4 b, double& z0, double& z1) {
+  const double u1 = 1.0 - u53(b.x, b.y);
+  const double u2 = u53(b.z, b.w);
+  const double r = sqrt(-2.0 * log(u1));
+  double s, c;
+  sincospi(2.0 * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+}  // namespace abc

@@ -1,0 +1,428 @@
+// Proposal generation: MultivariateNormalTransition.rvs + prior support.
+//
+// Reference semantics (pyabc/transition/multivariatenormal.py:87-95 and
+// pyabc/smc.py:602-645, numpy legacy RandomState):
+//   cdf = cumsum(w); cdf /= cdf[-1]            (sequential fp64)
+//   idx = cdf.searchsorted(u, side='right')    (u = random_sample())
+//   theta = X[idx] + z @ A,  A = sqrt(s)[:,None] * V  from svd(cov)
+//   valid iff prior.pdf(theta) > 0; for RV('uniform', lo, scale) scipy tests
+//   0 <= (theta - lo) / scale <= 1 in fp64 (random_variables.py:425-452).
+// The CDF is built by ONE lane in sequential order so that it is bit-identical
+// to numpy's; the resampled indices are then bit-exact for injected u.
+// Production proposals draw u and z from Philox4x32-10 inside the kernel
+// (no u/z round trip through HBM); the parity entry point takes them as
+// inputs.  Out-of-support draws are not evaluations: an order-preserving
+// compaction assigns proposal ids to in-support draws only.
+#include "common.hpp"
+#include "philox.hpp"
+
+namespace abc {
+
+// one wave; lane 0 carries the dependent fp64 chain, the other lanes stage
+// the next 64*8 weights into LDS so that the chain never waits on memory.
+__global__ __launch_bounds__(64) void cdf_scan_kernel(const double* __restrict__ w,
+                                                      int64_t n,
+                                                      double* __restrict__ cdf) {
+  __shared__ double buf[2][512];
+  double acc = 0.0;
+  const int lane = threadIdx.x;
+  const int64_t nchunk = ceil_div(n, 512);
+  double pre[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = k * 64 + lane;
+    buf[0][k * 64 + lane] = i < n ? w[i] : 0.0;
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < nchunk; ++c) {
+    const int cur = c & 1;
+    // issue the next chunk's loads into registers; they land while lane 0
+    // runs the dependent chain below
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = (c + 1) * 512 + k * 64 + lane;
+      pre[k] = i < n ? w[i] : 0.0;
+    }
+    if (lane == 0) {
+      const int64_t base = c * 512;
+      const int m = static_cast<int>(n - base < 512 ? n - base : 512);
+      for (int k = 0; k < m; ++k) {
+        acc += buf[cur][k];
+        buf[cur][k] = acc;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t i = c * 512 + k * 64 + lane;
+      if (i < n) cdf[i] = buf[cur][k * 64 + lane];
+      buf[cur ^ 1][k * 64 + lane] = pre[k];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void cdf_normalize_kernel(double* __restrict__ cdf,
+                                                            int64_t n) {
+  const double last = cdf[n - 1];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    cdf[i] = cdf[i] / last;
+}
+
+// first index i with cdf[i] > u (numpy searchsorted side='right')
+__device__ inline int64_t search_right(const double* __restrict__ cdf, int64_t n,
+                                       double u) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] <= u)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+template <int D>
+__device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
+                                   int d, const double* __restrict__ cdf,
+                                   double u, const double (&z)[D],
+                                   const double* __restrict__ A,
+                                   const double* __restrict__ lo,
+                                   const double* __restrict__ scale,
+                                   double* __restrict__ theta_row,
+                                   int64_t* idx_out, uint8_t* sup_out) {
+  int64_t idx = search_right(cdf, N, u);
+  const int64_t idx_c = idx < N ? idx : N - 1;  // numpy would raise; u<1 always
+  bool ok = true;
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+    if (l < d) {
+      double p = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        if (k < d) p = fma(z[k], A[k * d + l], p);
+      const double th = X[idx_c * d + l] + p;
+      theta_row[l] = th;
+      if (lo) {
+        const double x = (th - lo[l]) / scale[l];
+        ok = ok && (x >= 0.0) && (x <= 1.0);
+      }
+    }
+  }
+  *idx_out = idx;
+  *sup_out = ok ? 1 : 0;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void resample_perturb_kernel(
+    const double* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ cdf, const double* __restrict__ u,
+    const double* __restrict__ z, const double* __restrict__ A,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    int64_t B, double* __restrict__ theta, int64_t* __restrict__ idx,
+    uint8_t* __restrict__ sup) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double zz[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) zz[k] = k < d ? z[b * d + k] : 0.0;
+  perturb_one<D>(X, N, d, cdf, u[b], zz, A, lo, scale, theta + b * d, idx + b,
+                 sup + b);
+}
+
+// Production proposals: u from stream (2*sid), z from stream (2*sid+1).
+//   u[b]   = philox_uniform(seed, 2*sid,   offset + b)
+//   z[b,k] = philox_normal (seed, 2*sid+1, (offset + b) * d + k)
+template <int D>
+__global__ __launch_bounds__(256) void propose_philox_kernel(
+    const double* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ cdf, const double* __restrict__ A,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
+    double* __restrict__ theta, int64_t* __restrict__ idx,
+    uint8_t* __restrict__ sup) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t ui = offset + static_cast<uint64_t>(b);
+  const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
+  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
+  double zz[D];
+  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    if (k < d) {
+      const uint64_t zi = zi0 + k;
+      double c0, c1;
+      box_muller(philox_block(seed, 2 * sid + 1, zi >> 1), c0, c1);
+      zz[k] = (zi & 1) ? c1 : c0;
+    } else {
+      zz[k] = 0.0;
+    }
+  }
+  perturb_one<D>(X, N, d, cdf, u, zz, A, lo, scale, theta + b * d, idx + b,
+                 sup + b);
+}
+
+// prior sampling at t=0: theta = lo + scale * U  (scipy uniform.rvs)
+__global__ __launch_bounds__(256) void prior_uniform_kernel(
+    const double* __restrict__ lo, const double* __restrict__ scale, int d,
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
+    double* __restrict__ theta) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= B * d) return;
+  const int k = static_cast<int>(i % d);
+  const uint64_t ui = offset * d + static_cast<uint64_t>(i);
+  const u32x4 ub = philox_block(seed, sid, ui >> 1);
+  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
+  theta[i] = lo[k] + scale[k] * u;
+}
+
+// ---------------------------------------------------------------------------
+// RNG fills (for tests and for callers that need raw streams)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void philox_uniform_kernel(uint64_t seed,
+                                                             uint64_t sid,
+                                                             uint64_t offset,
+                                                             int64_t n,
+                                                             double* __restrict__ u) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ui = offset + static_cast<uint64_t>(i);
+  const u32x4 b = philox_block(seed, sid, ui >> 1);
+  u[i] = (ui & 1) ? u53(b.z, b.w) : u53(b.x, b.y);
+}
+
+__global__ __launch_bounds__(256) void philox_normal_kernel(uint64_t seed,
+                                                            uint64_t sid,
+                                                            uint64_t offset,
+                                                            int64_t n,
+                                                            double* __restrict__ z) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t zi = offset + static_cast<uint64_t>(i);
+  double c0, c1;
+  box_muller(philox_block(seed, sid, zi >> 1), c0, c1);
+  z[i] = (zi & 1) ? c1 : c0;
+}
+
+// ---------------------------------------------------------------------------
+// order-preserving stream compaction of u8 flags -> int64 positions
+// ---------------------------------------------------------------------------
+constexpr int kCompactBlock = 256;
+constexpr int kCompactItems = 16;  // per thread
+constexpr int kCompactTile = kCompactBlock * kCompactItems;
+
+__global__ __launch_bounds__(kCompactBlock) void compact_count_kernel(
+    const uint8_t* __restrict__ flags, int64_t n, int64_t* __restrict__ counts) {
+  __shared__ int64_t red[4];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kCompactTile;
+  int64_t c = 0;
+  for (int k = 0; k < kCompactItems; ++k) {
+    const int64_t i = base + k * kCompactBlock + threadIdx.x;
+    if (i < n) c += flags[i] != 0;
+  }
+  c = block_sum<int64_t, kCompactBlock>(c, red);
+  if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+
+// exclusive scan of the per-tile counts by one block; writes the total
+__global__ __launch_bounds__(1024) void compact_scan_kernel(int64_t* __restrict__ counts,
+                                                            int64_t ntiles,
+                                                            int64_t* __restrict__ total) {
+  __shared__ int64_t s[1024];
+  int64_t carry = 0;
+  for (int64_t base = 0; base < ntiles; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < ntiles ? counts[i] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < ntiles) counts[i] = carry + s[threadIdx.x] - v;
+    const int64_t tot = s[1023];
+    __syncthreads();
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(kCompactBlock) void compact_scatter_kernel(
+    const uint8_t* __restrict__ flags, int64_t n,
+    const int64_t* __restrict__ offsets, int64_t* __restrict__ out) {
+  __shared__ int wsum[4];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kCompactTile;
+  int64_t run = offsets[blockIdx.x];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int k = 0; k < kCompactItems; ++k) {
+    const int64_t i = base + k * kCompactBlock + threadIdx.x;
+    const bool f = i < n && flags[i] != 0;
+    const uint64_t m = __ballot(f);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wid] = __popcll(m);
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wid; ++w) woff += wsum[w];
+    if (f) out[run + woff + before] = i;
+    run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+}
+
+// gather rows: out[i, :] = src[idx[i], :]   (int64 idx, fp64 rows of width w)
+__global__ __launch_bounds__(256) void gather_rows_kernel(
+    const double* __restrict__ src, int64_t width, const int64_t* __restrict__ idx,
+    int64_t n, double* __restrict__ out) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n * width) return;
+  const int64_t i = t / width, k = t % width;
+  out[t] = src[idx[i] * width + k];
+}
+
+// ---------------------------------------------------------------------------
+static int check_dim(int d) {
+  return d >= 1 && d <= 32;
+}
+
+#define DISPATCH_D(d, MACRO) \
+  if ((d) <= 1) { MACRO(1) } \
+  else if ((d) <= 2) { MACRO(2) } \
+  else if ((d) <= 4) { MACRO(4) } \
+  else if ((d) <= 8) { MACRO(8) } \
+  else if ((d) <= 16) { MACRO(16) } \
+  else if ((d) <= 24) { MACRO(24) } \
+  else { MACRO(32) }
+
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf,
+                         hipStream_t st) {
+  ABC_REQUIRE(n > 0 && w && cdf, "resample_cdf: need n > 0 and buffers");
+  hipLaunchKernelGGL(cdf_scan_kernel, dim3(1), dim3(64), 0, st, w, n, cdf);
+  ABC_LAUNCH_CHECK("cdf_scan_kernel");
+  hipLaunchKernelGGL(cdf_normalize_kernel, dim3(stream_grid(n, 256, 1024)),
+                     dim3(256), 0, st, cdf, n);
+  ABC_LAUNCH_CHECK("cdf_normalize_kernel");
+  return kOk;
+}
+
+int abc_resample_perturb_f64(const double* X, int64_t N, int d,
+                             const double* cdf, const double* u,
+                             const double* z, const double* A,
+                             const double* lo, const double* scale, int64_t B,
+                             double* theta, int64_t* idx, uint8_t* in_support,
+                             hipStream_t st) {
+  ABC_REQUIRE(check_dim(d), "resample_perturb: unsupported d=%d", d);
+  ABC_REQUIRE(N > 0 && B >= 0, "resample_perturb: bad sizes");
+  if (B == 0) return kOk;
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+#define L(DD)                                                                \
+  hipLaunchKernelGGL((resample_perturb_kernel<DD>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, u, z, A, lo, scale, B, theta, idx,         \
+                     in_support);
+  DISPATCH_D(d, L)
+#undef L
+  ABC_LAUNCH_CHECK("resample_perturb_kernel");
+  return kOk;
+}
+
+int abc_propose_philox_f64(const double* X, int64_t N, int d,
+                           const double* cdf, const double* A,
+                           const double* lo, const double* scale,
+                           uint64_t seed, uint64_t sid, uint64_t offset,
+                           int64_t B, double* theta, int64_t* idx,
+                           uint8_t* in_support, hipStream_t st) {
+  ABC_REQUIRE(check_dim(d), "propose: unsupported d=%d", d);
+  ABC_REQUIRE(N > 0 && B >= 0, "propose: bad sizes");
+  if (B == 0) return kOk;
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+#define L(DD)                                                              \
+  hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta, \
+                     idx, in_support);
+  DISPATCH_D(d, L)
+#undef L
+  ABC_LAUNCH_CHECK("propose_philox_kernel");
+  return kOk;
+}
+
+int abc_prior_uniform_f64(const double* lo, const double* scale, int d,
+                          uint64_t seed, uint64_t sid, uint64_t offset,
+                          int64_t B, double* theta, hipStream_t st) {
+  ABC_REQUIRE(d >= 1 && B >= 0, "prior_uniform: bad sizes");
+  if (B == 0) return kOk;
+  hipLaunchKernelGGL(prior_uniform_kernel, dim3(ceil_div(B * d, 256)),
+                     dim3(256), 0, st, lo, scale, d, seed, sid, offset, B,
+                     theta);
+  ABC_LAUNCH_CHECK("prior_uniform_kernel");
+  return kOk;
+}
+
+int abc_philox_uniform_f64(uint64_t seed, uint64_t sid, uint64_t offset,
+                           int64_t n, double* u, hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "philox_uniform: n < 0");
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(philox_uniform_kernel, dim3(ceil_div(n, 256)), dim3(256),
+                     0, st, seed, sid, offset, n, u);
+  ABC_LAUNCH_CHECK("philox_uniform_kernel");
+  return kOk;
+}
+
+int abc_philox_normal_f64(uint64_t seed, uint64_t sid, uint64_t offset,
+                          int64_t n, double* z, hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "philox_normal: n < 0");
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(philox_normal_kernel, dim3(ceil_div(n, 256)), dim3(256),
+                     0, st, seed, sid, offset, n, z);
+  ABC_LAUNCH_CHECK("philox_normal_kernel");
+  return kOk;
+}
+
+size_t abc_compact_workspace_bytes(int64_t n) {
+  return static_cast<size_t>(ceil_div(n > 0 ? n : 1, kCompactTile)) * 8 + 64;
+}
+
+int abc_compact_flags(const uint8_t* flags, int64_t n, int64_t* out_idx,
+                      int64_t* out_count, void* ws, size_t ws_bytes,
+                      hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "compact: n < 0");
+  if (n == 0) {
+    ABC_HIP(hipMemsetAsync(out_count, 0, 8, st));
+    return kOk;
+  }
+  const int64_t tiles = ceil_div(n, kCompactTile);
+  ABC_REQUIRE(ws_bytes >= static_cast<size_t>(tiles) * 8,
+              "compact: workspace too small");
+  int64_t* counts = static_cast<int64_t*>(ws);
+  hipLaunchKernelGGL(compact_count_kernel, dim3(tiles), dim3(kCompactBlock), 0,
+                     st, flags, n, counts);
+  ABC_LAUNCH_CHECK("compact_count_kernel");
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, counts,
+                     tiles, out_count);
+  ABC_LAUNCH_CHECK("compact_scan_kernel");
+  hipLaunchKernelGGL(compact_scatter_kernel, dim3(tiles), dim3(kCompactBlock),
+                     0, st, flags, n, counts, out_idx);
+  ABC_LAUNCH_CHECK("compact_scatter_kernel");
+  return kOk;
+}
+
+int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
+                        int64_t n, double* out, hipStream_t st) {
+  ABC_REQUIRE(width > 0 && n >= 0, "gather_rows: bad sizes");
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(n * width, 256)),
+                     dim3(256), 0, st, src, width, idx, n, out);
+  ABC_LAUNCH_CHECK("gather_rows_kernel");
+  return kOk;
+}
+
+}  // extern "C"

@@ -1,0 +1,685 @@
+// Order statistics and reductions on the per-generation hot path.
+//
+// * weighted quantile epsilon (pyabc/weighted_statistics.py:26-43 used by
+//   QuantileEpsilon._update, pyabc/epsilon/epsilon.py:202-228):
+//     eps = interp(alpha, cumsum(w[argsort d]) - w/2, sort(d))
+//   computed WITHOUT a sort: a weighted radix select (8 passes of 8-bit
+//   digits on order-preserving 64-bit keys) finds the element k whose
+//   cumulative weight interval contains alpha, one more pass finds its sorted
+//   neighbours, and the interpolation formula of np.interp is applied to the
+//   bracketing knots.  Weights are summed in 2^62 fixed point, so every sum is
+//   exact and independent of thread / block / GPU order.
+// * column median / MAD (pyabc/distance/scale.py:38-47, np.median semantics:
+//   mean of the two middle values for even n) by a segmented count radix
+//   select per statistic column, bit-exact (order statistics + one fp64 add
+//   and halving), and column std (scale.py:59-65, ddof 0).
+// * weighted moments for MultivariateNormalTransition.fit (smart_cov,
+//   pyabc/transition/util.py:4-15), deterministic block partials.
+// * deterministic sums and the importance weight prior / transition
+//   (pyabc/smc.py:776-792).
+#include "common.hpp"
+
+namespace abc {
+
+constexpr int kBins = 256;
+constexpr double kFix = 4611686018427387904.0;  // 2^62
+
+// ---------------------------------------------------------------------------
+// deterministic sums (fixed grid + ordered final reduce)
+// ---------------------------------------------------------------------------
+constexpr int kRedGrid = 256;
+
+__global__ __launch_bounds__(256) void partial_sum_kernel(const double* __restrict__ x,
+                                                          int64_t n, int mode,
+                                                          double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const double v = x[i];
+    s += mode == 1 ? v * v : v;
+  }
+  s = block_sum<double, 256>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void final_sum_kernel(const double* __restrict__ part,
+                                                        int np, double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = threadIdx.x < np ? part[threadIdx.x] : 0.0;
+  s = block_sum<double, 256>(s, red);
+  if (threadIdx.x == 0) *out = s;
+}
+
+// ---------------------------------------------------------------------------
+// weighted quantile
+// ---------------------------------------------------------------------------
+struct WQState {
+  unsigned long long prefix;    // selected high digits
+  unsigned long long remaining; // target minus selected lower mass
+  unsigned long long w_less;    // fixed-point mass of keys < selected prefix
+  unsigned long long w_eq;      // mass of the final key
+  unsigned long long w_tot;     // total mass
+  unsigned long long kprev, knext, wprev, wnext;
+  int none;                     // alpha beyond the last knot
+  int pad;
+  double scale;                 // 2^62 / sum(w)
+  double sumw;
+};
+
+__device__ inline unsigned long long fixw(double w, double scale) {
+  return static_cast<unsigned long long>(__double2ull_rn(w * scale));
+}
+
+__global__ void wq_init_kernel(WQState* st, const double* __restrict__ sumw) {
+  st->prefix = 0;
+  st->w_less = 0;
+  st->w_eq = 0;
+  st->w_tot = 0;
+  st->kprev = 0;
+  st->knext = ~0ull;
+  st->wprev = 0;
+  st->wnext = 0;
+  st->none = 0;
+  st->sumw = *sumw;
+  st->scale = kFix / *sumw;
+}
+
+__global__ __launch_bounds__(256) void wq_total_kernel(const double* __restrict__ w,
+                                                       int64_t n, WQState* st) {
+  const double scale = st->scale;
+  unsigned long long s = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    s += w ? fixw(w[i], scale) : fixw(1.0, scale);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&st->w_tot, s);
+}
+
+__global__ void wq_target_kernel(WQState* st, double alpha) {
+  const double t = alpha * static_cast<double>(st->w_tot);
+  unsigned long long T = t >= 18446744073709551615.0 ? ~0ull : static_cast<unsigned long long>(t);
+  st->remaining = T;
+}
+
+__global__ __launch_bounds__(256) void wq_hist_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    const WQState* __restrict__ st, int shift, unsigned long long mask,
+    unsigned long long* __restrict__ hist_w, unsigned* __restrict__ hist_c) {
+  __shared__ unsigned long long hw[kBins];
+  __shared__ unsigned hc[kBins];
+  hw[threadIdx.x] = 0;
+  hc[threadIdx.x] = 0;
+  __syncthreads();
+  const unsigned long long prefix = st->prefix;
+  const double scale = st->scale;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint64_t k = f64_key(d[i]);
+    if (((k ^ prefix) & mask) == 0) {
+      const int bin = static_cast<int>((k >> shift) & 0xff);
+      atomicAdd(&hw[bin], w ? fixw(w[i], scale) : fixw(1.0, scale));
+      atomicAdd(&hc[bin], 1u);
+    }
+  }
+  __syncthreads();
+  if (hc[threadIdx.x]) {
+    atomicAdd(&hist_w[threadIdx.x], hw[threadIdx.x]);
+    atomicAdd(&hist_c[threadIdx.x], hc[threadIdx.x]);
+  }
+}
+
+__global__ __launch_bounds__(256) void wq_select_kernel(
+    WQState* st, int shift, unsigned long long* __restrict__ hist_w,
+    unsigned* __restrict__ hist_c, int last) {
+  __shared__ unsigned long long s[kBins];
+  __shared__ int found;
+  const int t = threadIdx.x;
+  const unsigned long long v = hist_w[t];
+  const unsigned c = hist_c[t];
+  s[t] = v;
+  if (t == 0) found = -1;
+  __syncthreads();
+  for (int o = 1; o < kBins; o <<= 1) {
+    const unsigned long long a = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  const unsigned long long incl = s[t], excl = incl - v;
+  const unsigned long long rem = st->remaining;
+  if (st->none == 0 && c > 0 && excl <= rem && incl > rem) found = t;
+  __syncthreads();
+  if (t == found) {
+    st->prefix |= static_cast<unsigned long long>(t) << shift;
+    st->remaining = rem - excl;
+    st->w_less += excl;
+    if (last) st->w_eq = v;
+  }
+  if (t == 0 && found < 0 && st->none == 0) st->none = 1;
+  hist_w[t] = 0;
+  hist_c[t] = 0;
+}
+
+__global__ __launch_bounds__(256) void wq_neighbors_kernel(const double* __restrict__ d,
+                                                           int64_t n, WQState* st) {
+  const unsigned long long key = st->none ? ~0ull : st->prefix;
+  unsigned long long kp = 0, kn = ~0ull;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint64_t k = f64_key(d[i]);
+    if (k < key && k > kp) kp = k;
+    if (k > key && k < kn) kn = k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(kp, o, 64);
+    const unsigned long long b = __shfl_xor(kn, o, 64);
+    kp = a > kp ? a : kp;
+    kn = b < kn ? b : kn;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&st->kprev, kp);
+    atomicMin(&st->knext, kn);
+  }
+}
+
+__global__ __launch_bounds__(256) void wq_neighbor_mass_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    WQState* st) {
+  const unsigned long long kp = st->kprev, kn = st->knext;
+  const double scale = st->scale;
+  unsigned long long sp = 0, sn = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint64_t k = f64_key(d[i]);
+    const unsigned long long wi = w ? fixw(w[i], scale) : fixw(1.0, scale);
+    if (k == kp) sp += wi;
+    if (k == kn) sn += wi;
+  }
+  sp = wave_sum(sp);
+  sn = wave_sum(sn);
+  if ((threadIdx.x & 63) == 0) {
+    if (sp) atomicAdd(&st->wprev, sp);
+    if (sn) atomicAdd(&st->wnext, sn);
+  }
+}
+
+// np.interp(alpha, xp, fp) restricted to the bracketing knots
+__global__ void wq_finalize_kernel(const WQState* st, int64_t n, double alpha,
+                                   double* __restrict__ out) {
+  const double W = static_cast<double>(st->w_tot);
+  double eps;
+  if (st->none) {
+    eps = key_f64(st->kprev);  // alpha past the last knot: largest point
+  } else {
+    const double pk = key_f64(st->prefix);
+    const double wk = static_cast<double>(st->w_eq) / W;
+    const double csk = static_cast<double>(st->w_less + st->w_eq) / W;
+    const double xk = csk - 0.5 * wk;
+    // a sorted neighbour exists (zero-mass neighbours are knots too)
+    const bool prev_ok = st->kprev != 0;
+    const bool next_ok = st->knext != ~0ull;
+    if (alpha >= xk) {
+      if (!next_ok || alpha == xk) {
+        eps = pk;
+      } else {
+        const double pn = key_f64(st->knext);
+        const double wn = static_cast<double>(st->wnext) / W;
+        const double xn = csk + wn - 0.5 * wn;
+        const double slope = (pn - pk) / (xn - xk);
+        eps = slope * (alpha - xk) + pk;
+      }
+    } else {
+      if (!prev_ok) {
+        eps = pk;
+      } else {
+        const double pp = key_f64(st->kprev);
+        const double wp = static_cast<double>(st->wprev) / W;
+        const double csp = static_cast<double>(st->w_less) / W;
+        const double xp = csp - 0.5 * wp;
+        if (alpha == xp) {
+          eps = pp;
+        } else {
+          const double slope = (pk - pp) / (xk - xp);
+          eps = slope * (alpha - xp) + pp;
+        }
+      }
+    }
+  }
+  out[0] = eps;
+  out[1] = key_f64(st->prefix);
+  out[2] = static_cast<double>(st->w_less) / W;
+  out[3] = static_cast<double>(st->w_eq) / W;
+}
+
+// ---------------------------------------------------------------------------
+// segmented count select: column median / MAD
+// ---------------------------------------------------------------------------
+struct SegState {
+  unsigned long long prefix;
+  long long rank;       // remaining rank within candidates
+  long long less;       // count of keys < prefix
+  long long eq;         // count == final key
+  unsigned long long knext;
+};
+
+template <int MODE>  // 0: key(x), 1: key(|x - center|)
+__device__ inline uint64_t seg_key(double x, double c) {
+  return MODE == 0 ? f64_key(x) : f64_key(fabs(x - c));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void seg_hist_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t n, int S, int bps,
+    const double* __restrict__ center, const SegState* __restrict__ st,
+    int shift, unsigned long long mask, unsigned* __restrict__ hist) {
+  __shared__ unsigned hc[kBins];
+  const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  hc[threadIdx.x] = 0;
+  __syncthreads();
+  const unsigned long long prefix = st[s].prefix;
+  const double c = MODE == 1 ? center[s] : 0.0;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  for (int64_t i = static_cast<int64_t>(part) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(bps) * 256) {
+    const uint64_t k = seg_key<MODE>(col[i], c);
+    if (((k ^ prefix) & mask) == 0) atomicAdd(&hc[(k >> shift) & 0xff], 1u);
+  }
+  __syncthreads();
+  if (hc[threadIdx.x]) atomicAdd(&hist[s * kBins + threadIdx.x], hc[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void seg_select_kernel(SegState* st, int shift,
+                                                         unsigned* __restrict__ hist,
+                                                         int last) {
+  __shared__ long long sc[kBins];
+  const int s = blockIdx.x, t = threadIdx.x;
+  const long long v = hist[s * kBins + t];
+  sc[t] = v;
+  __syncthreads();
+  for (int o = 1; o < kBins; o <<= 1) {
+    const long long a = t >= o ? sc[t - o] : 0;
+    __syncthreads();
+    sc[t] += a;
+    __syncthreads();
+  }
+  const long long incl = sc[t], excl = incl - v;
+  const long long rank = st[s].rank;
+  __syncthreads();
+  if (v > 0 && excl <= rank && rank < incl) {
+    st[s].prefix |= static_cast<unsigned long long>(t) << shift;
+    st[s].rank = rank - excl;
+    st[s].less += excl;
+    if (last) st[s].eq = v;
+  }
+  hist[s * kBins + t] = 0;
+}
+
+__global__ void seg_init_kernel(SegState* st, int S, long long rank) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  st[s].prefix = 0;
+  st[s].rank = rank;
+  st[s].less = 0;
+  st[s].eq = 0;
+  st[s].knext = ~0ull;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void seg_next_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t n, int bps,
+    const double* __restrict__ center, SegState* st) {
+  const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  const unsigned long long key = st[s].prefix;
+  const double c = MODE == 1 ? center[s] : 0.0;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  unsigned long long kn = ~0ull;
+  for (int64_t i = static_cast<int64_t>(part) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(bps) * 256) {
+    const uint64_t k = seg_key<MODE>(col[i], c);
+    if (k > key && k < kn) kn = k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(kn, o, 64);
+    kn = b < kn ? b : kn;
+  }
+  if ((threadIdx.x & 63) == 0 && kn != ~0ull) atomicMin(&st[s].knext, kn);
+}
+
+// median = a (odd n) or (a + b) / 2 (even n), np.median semantics
+__global__ void seg_median_kernel(const SegState* st, int S, int64_t n,
+                                  double* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const double a = key_f64(st[s].prefix);
+  if (n & 1) {
+    out[s] = a;
+    return;
+  }
+  const long long k = (n - 1) / 2;
+  const bool same = st[s].less + st[s].eq > k + 1;
+  const double b = same ? a : key_f64(st[s].knext);
+  out[s] = (a + b) / 2.0;
+}
+
+// ---------------------------------------------------------------------------
+// column mean / std (np.std, ddof 0), one block per column
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col_std_kernel(const double* __restrict__ data,
+                                                      int64_t ld, int64_t n,
+                                                      double* __restrict__ mean_out,
+                                                      double* __restrict__ std_out) {
+  __shared__ double red[4];
+  const double* col = data + static_cast<int64_t>(blockIdx.x) * ld;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += col[i];
+  s = block_sum<double, 256>(s, red);
+  const double mean = s / static_cast<double>(n);
+  double q = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const double x = col[i] - mean;
+    q += x * x;
+  }
+  q = block_sum<double, 256>(q, red);
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[blockIdx.x] = mean;
+    std_out[blockIdx.x] = sqrt(q / static_cast<double>(n));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weighted moments (fit_cov): out = [sw, sw2, mu[d], C[d*d]] with
+// C = sum_i w_i (x_i - mu)(x_i - mu)^T (unnormalised; host divides by
+// sw - sw2/sw as np.cov(aweights) does)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void moments1_kernel(const double* __restrict__ X,
+                                                       const double* __restrict__ w,
+                                                       int64_t n, int d,
+                                                       double* __restrict__ part) {
+  __shared__ double red[4];
+  const int nv = 2 + d;
+  for (int v = 0; v < nv; ++v) {
+    double s = 0.0;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * 256) {
+      const double wi = w[i];
+      s += v == 0 ? wi : (v == 1 ? wi * wi : wi * X[i * d + (v - 2)]);
+    }
+    s = block_sum<double, 256>(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x * nv + v] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void moments1_final_kernel(const double* __restrict__ part,
+                                                             int np, int d,
+                                                             double* __restrict__ out) {
+  __shared__ double red[4];
+  const int nv = 2 + d;
+  for (int v = 0; v < nv; ++v) {
+    double s = threadIdx.x < np ? part[threadIdx.x * nv + v] : 0.0;
+    s = block_sum<double, 256>(s, red);
+    if (threadIdx.x == 0) out[v] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < d) out[2 + threadIdx.x] = out[2 + threadIdx.x] / out[0];
+}
+
+__global__ __launch_bounds__(256) void moments2_kernel(const double* __restrict__ X,
+                                                       const double* __restrict__ w,
+                                                       int64_t n, int d,
+                                                       const double* __restrict__ mom,
+                                                       double* __restrict__ part) {
+  __shared__ double tile[64 * 33];
+  __shared__ double tw[64];
+  const int np = d * (d + 1) / 2;
+  double acc[3] = {0.0, 0.0, 0.0};
+  int pk[3], pl[3];
+  for (int q = 0; q < 3; ++q) {
+    int p = threadIdx.x + q * 256;
+    int k = 0;
+    while (p >= d - k && k < d) {
+      p -= d - k;
+      ++k;
+    }
+    pk[q] = k;
+    pl[q] = k + p;
+  }
+  const double* mu = mom + 2;
+  const int64_t rows_per_block = ceil_div(n, gridDim.x);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > n) r1 = n;
+  for (int64_t base = r0; base < r1; base += 64) {
+    const int rows = static_cast<int>(r1 - base < 64 ? r1 - base : 64);
+    __syncthreads();
+    for (int t = threadIdx.x; t < rows * d; t += 256) {
+      const int r = t / d, k = t % d;
+      tile[r * 33 + k] = X[(base + r) * d + k] - mu[k];
+    }
+    if (threadIdx.x < rows) tw[threadIdx.x] = w[base + threadIdx.x];
+    __syncthreads();
+    for (int q = 0; q < 3; ++q) {
+      if (threadIdx.x + q * 256 < np) {
+        const int k = pk[q], l = pl[q];
+        double a = acc[q];
+        for (int r = 0; r < rows; ++r) a = fma(tw[r] * tile[r * 33 + k], tile[r * 33 + l], a);
+        acc[q] = a;
+      }
+    }
+  }
+  for (int q = 0; q < 3; ++q)
+    if (threadIdx.x + q * 256 < np) part[blockIdx.x * np + threadIdx.x + q * 256] = acc[q];
+}
+
+__global__ __launch_bounds__(256) void moments2_final_kernel(const double* __restrict__ part,
+                                                             int nb, int d,
+                                                             double* __restrict__ out) {
+  const int np = d * (d + 1) / 2;
+  for (int p = threadIdx.x; p < np; p += 256) {
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[b * np + p];
+    int k = 0, q = p;
+    while (q >= d - k) {
+      q -= d - k;
+      ++k;
+    }
+    const int l = k + q;
+    out[2 + d + k * d + l] = s;
+    out[2 + d + l * d + k] = s;
+  }
+}
+
+// w_i = prior_i / exp(logpd_i)   (smc.py:776-792; prior may be a constant)
+__global__ __launch_bounds__(256) void importance_kernel(const double* __restrict__ logpd,
+                                                         const double* __restrict__ prior,
+                                                         double prior_const, int64_t M,
+                                                         double* __restrict__ w) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= M) return;
+  const double pr = prior ? prior[i] : prior_const;
+  w[i] = pr / exp(logpd[i]);
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(double* __restrict__ x, int64_t n,
+                                                    const double* __restrict__ div) {
+  const double dv = *div;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    x[i] = x[i] / dv;
+}
+
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+size_t abc_reduce_workspace_bytes(void) { return kRedGrid * 8 * 34 + 1024; }
+
+int abc_sum_f64(const double* x, int64_t n, int squares, double* out, void* ws,
+                hipStream_t st) {
+  ABC_REQUIRE(n >= 0 && x && out && ws, "sum: bad args");
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(kRedGrid), dim3(256), 0, st, x,
+                     n, squares ? 1 : 0, part);
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part,
+                     kRedGrid, out);
+  ABC_LAUNCH_CHECK("sum kernels");
+  return kOk;
+}
+
+int abc_scale_inplace_f64(double* x, int64_t n, const double* divisor,
+                          hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "scale: bad size");
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(scale_kernel, dim3(stream_grid(n, 256, 2048)), dim3(256), 0,
+                     st, x, n, divisor);
+  ABC_LAUNCH_CHECK("scale_kernel");
+  return kOk;
+}
+
+int abc_importance_weights_f64(const double* logpd, const double* prior,
+                               double prior_const, int64_t M, double* w,
+                               hipStream_t st) {
+  ABC_REQUIRE(M >= 0, "importance: bad size");
+  if (M == 0) return kOk;
+  hipLaunchKernelGGL(importance_kernel, dim3(ceil_div(M, 256)), dim3(256), 0,
+                     st, logpd, prior, prior_const, M, w);
+  ABC_LAUNCH_CHECK("importance_kernel");
+  return kOk;
+}
+
+size_t abc_wquantile_workspace_bytes(void) {
+  return sizeof(WQState) + kBins * 12 + 8 + kRedGrid * 8 + 256;
+}
+
+int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
+                      double* out4, void* ws, size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && d && out4 && ws, "wquantile: bad args");
+  ABC_REQUIRE(ws_bytes >= abc_wquantile_workspace_bytes(),
+              "wquantile: workspace too small");
+  char* base = static_cast<char*>(ws);
+  WQState* s = reinterpret_cast<WQState*>(base);
+  unsigned long long* hw = reinterpret_cast<unsigned long long*>(base + 256);
+  unsigned* hc = reinterpret_cast<unsigned*>(base + 256 + kBins * 8);
+  double* sumw = reinterpret_cast<double*>(base + 256 + kBins * 12);
+  double* part = sumw + 1;
+  if (w) {
+    hipLaunchKernelGGL(partial_sum_kernel, dim3(kRedGrid), dim3(256), 0, st, w,
+                       n, 0, part);
+    hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part,
+                       kRedGrid, sumw);
+  } else {
+    const double nn = static_cast<double>(n);
+    ABC_HIP(hipMemcpyAsync(sumw, &nn, 8, hipMemcpyHostToDevice, st));
+  }
+  ABC_HIP(hipMemsetAsync(hw, 0, kBins * 12, st));
+  hipLaunchKernelGGL(wq_init_kernel, dim3(1), dim3(1), 0, st, s, sumw);
+  const unsigned g = stream_grid(n, 256, 1024);
+  hipLaunchKernelGGL(wq_total_kernel, dim3(g), dim3(256), 0, st, w, n, s);
+  hipLaunchKernelGGL(wq_target_kernel, dim3(1), dim3(1), 0, st, s, alpha);
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    const unsigned long long mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
+    hipLaunchKernelGGL(wq_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,
+                       shift, mask, hw, hc);
+    hipLaunchKernelGGL(wq_select_kernel, dim3(1), dim3(256), 0, st, s, shift,
+                       hw, hc, pass == 7 ? 1 : 0);
+  }
+  hipLaunchKernelGGL(wq_neighbors_kernel, dim3(g), dim3(256), 0, st, d, n, s);
+  hipLaunchKernelGGL(wq_neighbor_mass_kernel, dim3(g), dim3(256), 0, st, d, w,
+                     n, s);
+  hipLaunchKernelGGL(wq_finalize_kernel, dim3(1), dim3(1), 0, st, s, n, alpha,
+                     out4);
+  ABC_LAUNCH_CHECK("wquantile kernels");
+  return kOk;
+}
+
+size_t abc_column_select_workspace_bytes(int S) {
+  return static_cast<size_t>(S) * (sizeof(SegState) + kBins * 4) + 256;
+}
+
+// median (and MAD when mad_out != NULL) of every column of data_T[S][ld]
+int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
+                              int S, double* median_out, double* mad_out,
+                              void* ws, size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && S > 0 && ld >= n, "median: bad sizes");
+  ABC_REQUIRE(ws_bytes >= abc_column_select_workspace_bytes(S),
+              "median: workspace too small");
+  SegState* sst = static_cast<SegState*>(ws);
+  unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
+                                               static_cast<size_t>(S) * sizeof(SegState));
+  ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * kBins * 4, st));
+  int bps = static_cast<int>(ceil_div(2048, S));
+  const int64_t maxb = ceil_div(n, 256);
+  if (bps > maxb) bps = static_cast<int>(maxb);
+  if (bps < 1) bps = 1;
+  const long long k = (n - 1) / 2;
+  for (int round = 0; round < (mad_out ? 2 : 1); ++round) {
+    const double* center = round == 0 ? nullptr : median_out;
+    double* out = round == 0 ? median_out : mad_out;
+    hipLaunchKernelGGL(seg_init_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, st,
+                       sst, S, k);
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = 56 - 8 * pass;
+      const unsigned long long mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
+      if (round == 0)
+        hipLaunchKernelGGL(seg_hist_kernel<0>, dim3(S * bps), dim3(256), 0, st,
+                           data_T, ld, n, S, bps, center, sst, shift, mask, hist);
+      else
+        hipLaunchKernelGGL(seg_hist_kernel<1>, dim3(S * bps), dim3(256), 0, st,
+                           data_T, ld, n, S, bps, center, sst, shift, mask, hist);
+      hipLaunchKernelGGL(seg_select_kernel, dim3(S), dim3(256), 0, st, sst, shift,
+                         hist, pass == 7 ? 1 : 0);
+    }
+    if ((n & 1) == 0) {
+      if (round == 0)
+        hipLaunchKernelGGL(seg_next_kernel<0>, dim3(S * bps), dim3(256), 0, st,
+                           data_T, ld, n, bps, center, sst);
+      else
+        hipLaunchKernelGGL(seg_next_kernel<1>, dim3(S * bps), dim3(256), 0, st,
+                           data_T, ld, n, bps, center, sst);
+    }
+    hipLaunchKernelGGL(seg_median_kernel, dim3(ceil_div(S, 256)), dim3(256), 0,
+                       st, sst, S, n, out);
+  }
+  ABC_LAUNCH_CHECK("column median/mad kernels");
+  return kOk;
+}
+
+int abc_column_std_f64(const double* data_T, int64_t ld, int64_t n, int S,
+                       double* mean_out, double* std_out, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && S > 0 && ld >= n, "std: bad sizes");
+  hipLaunchKernelGGL(col_std_kernel, dim3(S), dim3(256), 0, st, data_T, ld, n,
+                     mean_out, std_out);
+  ABC_LAUNCH_CHECK("col_std_kernel");
+  return kOk;
+}
+
+size_t abc_moments_workspace_bytes(int d) {
+  const int np = d * (d + 1) / 2;
+  return static_cast<size_t>(kRedGrid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
+}
+
+int abc_weighted_moments_f64(const double* X, const double* w, int64_t n, int d,
+                             double* out, void* ws, size_t ws_bytes,
+                             hipStream_t st) {
+  ABC_REQUIRE(n > 0 && d >= 1 && d <= 32, "moments: bad sizes (d <= 32)");
+  ABC_REQUIRE(ws_bytes >= abc_moments_workspace_bytes(d),
+              "moments: workspace too small");
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(moments1_kernel, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
+                     d, part);
+  hipLaunchKernelGGL(moments1_final_kernel, dim3(1), dim3(256), 0, st, part,
+                     kRedGrid, d, out);
+  hipLaunchKernelGGL(moments2_kernel, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
+                     d, out, part);
+  hipLaunchKernelGGL(moments2_final_kernel, dim3(1), dim3(256), 0, st, part,
+                     kRedGrid, d, out);
+  ABC_LAUNCH_CHECK("moments kernels");
+  return kOk;
+}
+
+}  // extern "C"

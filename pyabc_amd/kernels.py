@@ -1,0 +1,366 @@
+"""Typed torch-tensor wrappers over the libabc_hip C-ABI.
+
+Every function here enqueues HIP kernels on torch's current stream through
+``_native`` and returns device tensors.  Inputs must already be device
+tensors of the stated dtype and layout; there is no host/CPU path.  Small
+d x d linear algebra (eigh/svd of the KDE covariance) is done by the callers on
+the host, exactly where the reference calls numpy/scipy on d x d matrices.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from ._native import ptr, call
+
+F64 = torch.float64
+F32 = torch.float32
+
+
+def _dev():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class Workspace:
+    """Grow-only scratch buffer per device (no allocation in steady state)."""
+
+    def __init__(self):
+        self._buf = {}
+
+    def get(self, nbytes, tag="default"):
+        nbytes = max(int(nbytes), 256)
+        key = (torch.cuda.current_device(), tag)
+        b = self._buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes + (nbytes >> 3), dtype=torch.uint8,
+                            device=_dev())
+            self._buf[key] = b
+        return b
+
+
+WS = Workspace()
+
+
+def _contig(t, dtype):
+    if t.dtype != dtype:
+        raise TypeError(f"expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# RNG / proposals (a2)
+# ---------------------------------------------------------------------------
+def philox_uniform(seed, sid, offset, n):
+    out = torch.empty(n, dtype=F64, device=_dev())
+    call("abc_philox_uniform_f64", seed, sid, offset, n, ptr(out), nat.stream())
+    return out
+
+
+def philox_normal(seed, sid, offset, n):
+    out = torch.empty(n, dtype=F64, device=_dev())
+    call("abc_philox_normal_f64", seed, sid, offset, n, ptr(out), nat.stream())
+    return out
+
+
+def resample_cdf(w):
+    w = _contig(w, F64)
+    cdf = torch.empty_like(w)
+    call("abc_resample_cdf_f64", ptr(w), w.numel(), ptr(cdf), nat.stream())
+    return cdf
+
+
+def resample_perturb(X, cdf, u, z, A, lo=None, scale=None):
+    X = _contig(X, F64)
+    N, d = X.shape
+    B = u.numel()
+    theta = torch.empty((B, d), dtype=F64, device=_dev())
+    idx = torch.empty(B, dtype=torch.int64, device=_dev())
+    sup = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_resample_perturb_f64", ptr(X), N, d, ptr(_contig(cdf, F64)),
+         ptr(_contig(u, F64)), ptr(_contig(z, F64)), ptr(_contig(A, F64)),
+         ptr(lo), ptr(scale), B, ptr(theta), ptr(idx), ptr(sup), nat.stream())
+    return theta, idx, sup
+
+
+def propose_philox(X, cdf, A, lo, scale, seed, sid, offset, B, out=None):
+    X = _contig(X, F64)
+    N, d = X.shape
+    if out is None:
+        theta = torch.empty((B, d), dtype=F64, device=_dev())
+        idx = torch.empty(B, dtype=torch.int64, device=_dev())
+        sup = torch.empty(B, dtype=torch.uint8, device=_dev())
+    else:
+        theta, idx, sup = out
+    call("abc_propose_philox_f64", ptr(X), N, d, ptr(cdf), ptr(A), ptr(lo),
+         ptr(scale), seed, sid, offset, B, ptr(theta), ptr(idx), ptr(sup),
+         nat.stream())
+    return theta, idx, sup
+
+
+def prior_uniform(lo, scale, seed, sid, offset, B):
+    d = lo.numel()
+    theta = torch.empty((B, d), dtype=F64, device=_dev())
+    call("abc_prior_uniform_f64", ptr(lo), ptr(scale), d, seed, sid, offset,
+         B, ptr(theta), nat.stream())
+    return theta
+
+
+def compact(flags, out_idx=None):
+    """Order-preserving positions of nonzero u8 flags; returns (idx, count_dev)."""
+    n = flags.numel()
+    if out_idx is None:
+        out_idx = torch.empty(max(n, 1), dtype=torch.int64, device=_dev())
+    count = torch.empty(1, dtype=torch.int64, device=_dev())
+    wsb = nat.lib().abc_compact_workspace_bytes(n)
+    ws = WS.get(wsb, "compact")
+    call("abc_compact_flags", ptr(flags), n, ptr(out_idx), ptr(count), ptr(ws),
+         wsb, nat.stream())
+    return out_idx, count
+
+
+def gather_rows(src, idx, n=None):
+    src = _contig(src, F64)
+    width = src.shape[1] if src.dim() == 2 else 1
+    n = idx.numel() if n is None else n
+    out = torch.empty((n, width), dtype=F64, device=_dev())
+    call("abc_gather_rows_f64", ptr(src), width, ptr(idx), n, ptr(out),
+         nat.stream())
+    return out if src.dim() == 2 else out.view(-1)
+
+
+# ---------------------------------------------------------------------------
+# fit (a1)
+# ---------------------------------------------------------------------------
+def weighted_moments(X, w):
+    """Device [sw, sw2, mu(d), C(d*d)] (C un-normalised centred products)."""
+    X = _contig(X, F64)
+    n, d = X.shape
+    out = torch.empty(2 + d + d * d, dtype=F64, device=_dev())
+    wsb = nat.lib().abc_moments_workspace_bytes(d)
+    ws = WS.get(wsb, "moments")
+    call("abc_weighted_moments_f64", ptr(X), ptr(_contig(w, F64)), n, d,
+         ptr(out), ptr(ws), wsb, nat.stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# KDE (a3)
+# ---------------------------------------------------------------------------
+LOG2E = 1.4426950408889634
+LOG_2PI = math.log(2 * math.pi)
+
+
+def padded_dim(d):
+    D = nat.lib().abc_kde_padded_dim(d)
+    if D < 0:
+        raise nat.NativeLibraryError(f"KDE: unsupported dimension d={d}")
+    return D
+
+
+def row_pad():
+    return nat.lib().abc_kde_row_pad()
+
+
+def psd_whitening(cov):
+    """scipy _PSD semantics on the host (d x d): U, rank, log_pdet."""
+    cov = np.asarray(cov, dtype=np.float64)
+    s, u = np.linalg.eigh(cov)
+    eps = 1e6 * np.finfo(np.float64).eps * np.max(np.abs(s))
+    keep = s > eps
+    s_pinv = np.where(keep, 1.0 / np.where(keep, s, 1.0), 0.0)
+    U = u * np.sqrt(s_pinv)
+    return U, int(keep.sum()), float(np.sum(np.log(s[keep])))
+
+
+class PackedPopulation:
+    """The previous population packed for the KDE pass (built once per fit)."""
+
+    def __init__(self, X, w, mu, Us, rank, log_pdet, precision="f32"):
+        X = _contig(X, F64)
+        n, d = X.shape
+        self.n, self.d = n, d
+        self.D = padded_dim(d)
+        rp = row_pad()
+        self.npad = ((n + rp - 1) // rp) * rp
+        self.precision = precision
+        dt = F32 if precision == "f32" else F64
+        self.P = torch.empty((self.npad, self.D + 1), dtype=dt, device=_dev())
+        self.lw2max = torch.empty(1, dtype=F64, device=_dev())
+        self.mu = mu
+        self.Us = Us
+        self.log_const = -0.5 * (rank * LOG_2PI + log_pdet)
+        ws = WS.get(256, "pack")
+        fn = "abc_kde_pack_prev_f32" if precision == "f32" else \
+            "abc_kde_pack_prev_f64"
+        call(fn, ptr(X), ptr(_contig(w, F64)), n, d, ptr(mu), ptr(Us),
+             ptr(self.P), self.npad, ptr(self.lw2max), ptr(ws), nat.stream())
+
+    def whiten(self, theta):
+        theta = _contig(theta, F64)
+        M = theta.shape[0]
+        dt = F32 if self.precision == "f32" else F64
+        Y = torch.zeros((M, self.D), dtype=dt, device=_dev())
+        fn = "abc_whiten_f32" if self.precision == "f32" else "abc_whiten_f64"
+        call(fn, ptr(theta), M, self.d, ptr(self.mu), ptr(self.Us), ptr(Y),
+             nat.stream())
+        return Y
+
+    def logpdf_whitened(self, Y, out=None):
+        M = Y.shape[0]
+        if out is None:
+            out = torch.empty(M, dtype=F64, device=_dev())
+        if M == 0:
+            return out
+        wsb = nat.lib().abc_kde_workspace_bytes(M, self.npad, self.d)
+        ws = WS.get(wsb, "kde")
+        fn = "abc_kde_logpdf_f32" if self.precision == "f32" else \
+            "abc_kde_logpdf_f64"
+        call(fn, ptr(Y), M, ptr(self.P), self.npad, self.d, ptr(self.lw2max),
+             self.log_const, ptr(out), ptr(ws), wsb, nat.stream())
+        return out
+
+    def logpdf(self, theta):
+        return self.logpdf_whitened(self.whiten(theta))
+
+
+def importance_weights(logpd, prior=None, prior_const=1.0):
+    M = logpd.numel()
+    w = torch.empty(M, dtype=F64, device=_dev())
+    call("abc_importance_weights_f64", ptr(logpd), ptr(prior), prior_const, M,
+         ptr(w), nat.stream())
+    return w
+
+
+# ---------------------------------------------------------------------------
+# reductions (a4)
+# ---------------------------------------------------------------------------
+def dsum(x, squares=False):
+    out = torch.empty(1, dtype=F64, device=_dev())
+    ws = WS.get(nat.lib().abc_reduce_workspace_bytes(), "reduce")
+    call("abc_sum_f64", ptr(_contig(x, F64)), x.numel(), 1 if squares else 0,
+         ptr(out), ptr(ws), nat.stream())
+    return out
+
+
+def scale_inplace(x, divisor_dev):
+    call("abc_scale_inplace_f64", ptr(x), x.numel(), ptr(divisor_dev),
+         nat.stream())
+    return x
+
+
+# ---------------------------------------------------------------------------
+# distances (a5), scales (a6), quantile (a7)
+# ---------------------------------------------------------------------------
+def pnorm_distance(stats_T, x0, fw, p, eps=math.inf, B=None, with_accept=True,
+                   d_out=None, acc_out=None, guard_out=None):
+    S, ld = stats_T.shape
+    B = ld if B is None else B
+    d = torch.empty(B, dtype=F64, device=_dev()) if d_out is None else d_out
+    acc = guard = None
+    if with_accept:
+        acc = torch.empty(B, dtype=torch.uint8, device=_dev()) \
+            if acc_out is None else acc_out
+        guard = torch.empty(B, dtype=torch.uint8, device=_dev()) \
+            if guard_out is None else guard_out
+    call("abc_pnorm_distance_f64", ptr(stats_T), ld, ptr(x0), ptr(fw), B, S,
+         float(p), float(eps), ptr(d), ptr(acc), ptr(guard), nat.stream())
+    return d, acc, guard
+
+
+def column_median_mad(data_T, n=None, mad=True):
+    S, ld = data_T.shape
+    n = ld if n is None else n
+    med = torch.empty(S, dtype=F64, device=_dev())
+    madv = torch.empty(S, dtype=F64, device=_dev()) if mad else None
+    wsb = nat.lib().abc_column_select_workspace_bytes(S)
+    ws = WS.get(wsb, "colsel")
+    call("abc_column_median_mad_f64", ptr(data_T), ld, n, S, ptr(med),
+         ptr(madv), ptr(ws), wsb, nat.stream())
+    return med, madv
+
+
+def column_std(data_T, n=None):
+    S, ld = data_T.shape
+    n = ld if n is None else n
+    mean = torch.empty(S, dtype=F64, device=_dev())
+    std = torch.empty(S, dtype=F64, device=_dev())
+    call("abc_column_std_f64", ptr(data_T), ld, n, S, ptr(mean), ptr(std),
+         nat.stream())
+    return mean, std
+
+
+def weighted_quantile(d, w, alpha):
+    """Device [eps, p_k, cs_{k-1}, w_k] for interp(alpha, cs - w/2, sort d)."""
+    n = d.numel()
+    out = torch.empty(4, dtype=F64, device=_dev())
+    wsb = nat.lib().abc_wquantile_workspace_bytes()
+    ws = WS.get(wsb, "wq")
+    call("abc_wquantile_f64", ptr(_contig(d, F64)),
+         ptr(None if w is None else _contig(w, F64)), n, float(alpha),
+         ptr(out), ptr(ws), wsb, nat.stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# LocalTransition (a8)
+# ---------------------------------------------------------------------------
+def knn(X, k):
+    X = _contig(X, F64)
+    N, d = X.shape
+    nbr = torch.empty((N, k), dtype=torch.int32, device=_dev())
+    d2 = torch.empty((N, k), dtype=F64, device=_dev())
+    call("abc_knn_f64", ptr(X), N, d, k, ptr(nbr), ptr(d2), None, 0,
+         nat.stream())
+    return nbr, d2
+
+
+def local_cov(X, w, nbr, scaling=1.0):
+    X = _contig(X, F64)
+    N, d = X.shape
+    k = nbr.shape[1]
+    covs = torch.empty((N, d, d), dtype=F64, device=_dev())
+    invs = torch.empty((N, d, d), dtype=F64, device=_dev())
+    dets = torch.empty(N, dtype=F64, device=_dev())
+    call("abc_local_cov_f64", ptr(X), ptr(_contig(w, F64)), N, d,
+         ptr(nbr.contiguous()), k, float(scaling), ptr(covs), ptr(invs),
+         ptr(dets), nat.stream())
+    return covs, invs, dets
+
+
+def local_logpdf(pts, X, w, invs, dets):
+    pts = _contig(pts, F64)
+    M, d = pts.shape
+    N = X.shape[0]
+    out = torch.empty(M, dtype=F64, device=_dev())
+    wsb = nat.lib().abc_local_logpdf_workspace_bytes(M, N)
+    ws = WS.get(wsb, "localpdf")
+    call("abc_local_logpdf_f64", ptr(pts), M, ptr(_contig(X, F64)),
+         ptr(_contig(w, F64)), ptr(invs), ptr(dets), N, d, ptr(out), ptr(ws),
+         wsb, nat.stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# synthetic simulators
+# ---------------------------------------------------------------------------
+def sim_linear_gaussian(theta, A, c, sigma, seed, sid, offset, out_T=None,
+                        B=None):
+    theta = _contig(theta, F64)
+    B = theta.shape[0] if B is None else B
+    S, d = A.shape
+    if out_T is None:
+        out_T = torch.empty((S, max(B, 1)), dtype=F64, device=_dev())
+    call("abc_sim_linear_gaussian_f64", ptr(theta), B, d, ptr(A), ptr(c), S,
+         float(sigma), seed, sid, offset, ptr(out_T), out_T.shape[1],
+         nat.stream())
+    return out_T
+
+
+def sim_gaussian_mean(theta, sigma, seed, sid, offset, out=None, B=None):
+    B = theta.shape[0] if B is None else B
+    if out is None:
+        out = torch.empty(B, dtype=F64, device=_dev())
+    call("abc_sim_gaussian_mean_f64", ptr(_contig(theta, F64)), B,
+         float(sigma), seed, sid, offset, ptr(out), nat.stream())
+    return out

@@ -1,0 +1,283 @@
+"""HIP kernels through the C-ABI vs the oracle and the reference's golden vectors.
+
+Tolerances (BASELINE north star): resampled indices, support masks, accept
+masks and order statistics bit-exact; weights / densities / distances /
+covariances / epsilon within 1e-5 relative for the fp32 KDE kernel and
+1e-12 for fp64.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as ref
+from tests.conftest import load_golden, golden_names
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pyabc_amd import kernels
+    return kernels
+
+
+def dev(a, dtype=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device="cuda")
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------- (a3) KDE
+def _packed(K, X, w, cov, precision):
+    U, rank, log_pdet = K.psd_whitening(cov)
+    Us = U * math.sqrt(0.5 * K.LOG2E)
+    mu = (X * w[:, None]).sum(0) / w.sum()
+    return K.PackedPopulation(dev(X), dev(w), dev(mu), dev(Us), rank,
+                              log_pdet, precision)
+
+
+@pytest.mark.parametrize("precision,rtol", [("f32", 1e-5), ("f64", 1e-12)])
+@pytest.mark.parametrize("name", golden_names("kde_"))
+def test_kde_density_vs_reference(K, name, precision, rtol):
+    g = load_golden(name)
+    w = ref.fit_normalize_weights(g["w"])
+    pp = _packed(K, g["X"], w, g["cov"], precision)
+    logpd = pp.logpdf(dev(g["theta"]))
+    dens = np.exp(host(logpd))
+    k = len(g["transition_pd_series"])
+    np.testing.assert_allclose(dens[:k], g["transition_pd_series"], rtol=rtol)
+    if g["X"].shape[0] > 1:
+        np.testing.assert_allclose(dens, g["transition_pd"], rtol=rtol)
+        prior = dev(ref.uniform_box_pdf(g["theta"], g["prior_lo"],
+                                        g["prior_scale"]))
+        wt = K.importance_weights(logpd, prior)
+        np.testing.assert_allclose(host(wt), g["weight"], rtol=rtol)
+        s = K.dsum(wt)
+        K.scale_inplace(wt, s)
+        np.testing.assert_allclose(host(wt), g["weight_norm"], rtol=rtol)
+
+
+def test_kde_underflow_rows_fixup(K):
+    """Rows far from every previous particle underflow the fixed offset;
+    the fixup pass must still return the exact log density."""
+    rng = np.random.default_rng(7)
+    X = rng.normal(size=(3000, 4))
+    w = rng.uniform(0.5, 1.5, 3000)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = np.concatenate([X[:50] + 0.01, X[:20] + 6.0])   # far rows
+    pp = _packed(K, X, w, cov, "f32")
+    lp = host(pp.logpdf(dev(theta)))
+    U, rank, log_pdet = ref.psd_whitening(cov)
+    ls = ref.kde_logsum(theta @ U, X @ U, np.log(w))
+    expect = ls - 0.5 * (rank * ref.LOG_2PI + log_pdet)
+    np.testing.assert_allclose(lp, expect, rtol=2e-6, atol=1e-5)
+
+
+def test_kde_large_random_vs_oracle(K):
+    rng = np.random.default_rng(11)
+    N, M, d = 20000, 777, 8
+    X = rng.normal(size=(N, d)) * 2 + 5
+    w = rng.uniform(0.2, 2, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = X[rng.integers(0, N, M)] + rng.normal(size=(M, d)) * 0.3
+    expect = ref.kde_transition_pd(theta, X, w, cov)
+    for prec, rtol in [("f32", 1e-5), ("f64", 1e-12)]:
+        pp = _packed(K, X, w, cov, prec)
+        got = np.exp(host(pp.logpdf(dev(theta))))
+        np.testing.assert_allclose(got, expect, rtol=rtol)
+
+
+# ------------------------------------------------------------ (a1) fit
+@pytest.mark.parametrize("name", golden_names("kde_"))
+def test_weighted_moments_cov(K, name):
+    g = load_golden(name)
+    if g["X"].shape[0] < 2:
+        pytest.skip("single particle: diag(|x|) handled on the host")
+    w = ref.fit_normalize_weights(g["w"])
+    mom = host(K.weighted_moments(dev(g["X"]), dev(w)))
+    d = g["X"].shape[1]
+    sw, sw2 = mom[0], mom[1]
+    C = mom[2 + d:].reshape(d, d) / (sw - sw2 / sw)
+    bw = ref.silverman_rule_of_thumb(1 / sw2, d)
+    np.testing.assert_allclose(C * bw ** 2, g["cov"], rtol=1e-12, atol=1e-15)
+
+
+# -------------------------------------------------------- (a2) proposals
+@pytest.mark.parametrize("name", golden_names("resample_"))
+def test_resample_perturb_bit_exact(K, name):
+    g = load_golden(name)
+    cdf_ref = ref.resample_cdf(g["w"])
+    cdf = K.resample_cdf(dev(g["w"]))
+    np.testing.assert_array_equal(host(cdf), cdf_ref)
+    A = ref.svd_factor(g["cov"])
+    theta, idx, sup = K.resample_perturb(dev(g["X"]), cdf, dev(g["u"]),
+                                         dev(g["z"]), dev(A),
+                                         dev(g["prior_lo"]),
+                                         dev(g["prior_scale"]))
+    np.testing.assert_array_equal(host(idx), g["idx"])
+    np.testing.assert_allclose(host(theta), g["theta"], rtol=1e-13,
+                               atol=1e-13)
+    B = len(g["u"])
+    np.testing.assert_array_equal(host(sup), g["in_support"][:B])
+
+
+@pytest.mark.parametrize("name", golden_names("resample_"))
+def test_support_boundary_probes(K, name):
+    """theta exactly on / one ulp outside the box: scipy's inclusive test."""
+    g = load_golden(name)
+    P = g["probes"]
+    n, d = P.shape
+    cdf = K.resample_cdf(dev(np.ones(n)))
+    u = (np.arange(n) + 0.5) / n
+    theta, idx, sup = K.resample_perturb(dev(P), cdf, dev(u),
+                                         dev(np.zeros((n, d))),
+                                         dev(np.eye(d)), dev(g["prior_lo"]),
+                                         dev(g["prior_scale"]))
+    np.testing.assert_array_equal(host(idx), np.arange(n))
+    np.testing.assert_array_equal(host(theta), P)
+    B = len(g["u"])
+    np.testing.assert_array_equal(host(sup), g["in_support"][B:])
+
+
+def test_philox_streams_match_oracle(K):
+    u = host(K.philox_uniform(1234, 7, 3, 100001))
+    np.testing.assert_array_equal(u, ref.philox_uniform(1234, 7, 100004)[3:])
+    z = host(K.philox_normal(99, 2, 0, 50001))
+    np.testing.assert_allclose(z, ref.philox_normal(99, 2, 50001),
+                               rtol=1e-13, atol=1e-13)
+
+
+def test_propose_philox_consistent_with_injected(K):
+    rng = np.random.default_rng(5)
+    N, d, B = 5000, 6, 40000
+    X = rng.normal(size=(N, d))
+    w = rng.uniform(size=N)
+    w /= w.sum()
+    A = ref.svd_factor(ref.mvn_fit_cov(X, w))
+    lo, sc = np.full(d, -2.0), np.full(d, 4.0)
+    cdf = K.resample_cdf(dev(w))
+    seed, sid, off = 42, 3, 1000
+    th, idx, sup = K.propose_philox(dev(X), cdf, dev(A), dev(lo), dev(sc),
+                                    seed, sid, off, B)
+    u = ref.philox_uniform(seed, 2 * sid, off + B)[off:]
+    z = ref.philox_normal(seed, 2 * sid + 1, (off + B) * d)[off * d:]
+    idx_ref, th_ref = ref.resample_perturb(X, w, None if False else
+                                           ref.mvn_fit_cov(X, w), u,
+                                           z.reshape(B, d))
+    np.testing.assert_array_equal(host(idx), idx_ref)
+    np.testing.assert_allclose(host(th), th_ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(
+        host(sup).astype(bool), ref.uniform_box_support(th_ref, lo, sc))
+
+
+def test_compaction(K):
+    rng = np.random.default_rng(3)
+    for n in [1, 100, 4096, 4097, 1_000_003]:
+        f = (rng.uniform(size=n) < 0.37).astype(np.uint8)
+        idx, cnt = K.compact(dev(f, torch.uint8))
+        c = int(host(cnt)[0])
+        np.testing.assert_array_equal(host(idx)[:c], np.nonzero(f)[0])
+
+
+# ------------------------------------------------------ (a5) distances
+def test_pnorm_distances_and_accept(K):
+    g = load_golden("pnorm_B1500_S100")
+    stats_T = dev(g["stats"].T)
+    for tag, p in [("1", 1), ("2", 2), ("3", 3), ("inf", math.inf)]:
+        eps = float(g["eps_p2"]) if tag == "2" else math.inf
+        d, acc, guard = K.pnorm_distance(stats_T, dev(g["x0"]), dev(g["fw"]),
+                                         p, eps)
+        np.testing.assert_allclose(host(d), g["d_p" + tag], rtol=1e-12)
+        if tag == "2":
+            np.testing.assert_array_equal(host(acc), g["accept_p2"])
+            assert host(guard).sum() == 0
+
+
+# ---------------------------------------------- (a6) adaptive scales
+@pytest.mark.parametrize("name", golden_names("adaptive_"))
+def test_column_mad_and_std(K, name):
+    g = load_golden(name)
+    data = g["data"]
+    med, mad = K.column_median_mad(dev(data.T))
+    np.testing.assert_array_equal(host(med), np.median(data, axis=0))
+    mad_ref = np.array([ref.median_absolute_deviation(data[:, k])
+                        for k in range(data.shape[1])])
+    np.testing.assert_array_equal(host(mad), mad_ref)
+    _, std = K.column_std(dev(data.T))
+    np.testing.assert_allclose(host(std), np.std(data, axis=0), rtol=1e-12)
+
+    def weights(scale):
+        w = np.array([0 if np.isclose(s, 0) else 1 / s for s in scale])
+        return w / np.mean(w)
+    np.testing.assert_array_equal(weights(host(mad)), g["w_mad"])
+    np.testing.assert_allclose(weights(host(std)), g["w_std"], rtol=1e-12)
+
+
+# ------------------------------------------------------ (a7) quantile
+def test_weighted_quantile_golden(K):
+    g = load_golden("quantile")
+    for N in [3, 4, 1000, 100000]:
+        d, w = g[f"d_{N}"], g[f"w_{N}"]
+        for j, a in enumerate(g["alphas"]):
+            q = float(host(K.weighted_quantile(dev(d), dev(w), a))[0])
+            qu = float(host(K.weighted_quantile(dev(d), None, a))[0])
+            # reference cumsum rounding enters through the interpolation
+            # slope: |dq| <= 1e-12 q + slope * N * 2^-52
+            srt = np.sort(d)
+            slope = np.max(np.diff(srt)) / np.min(w) * 2 if N > 1 else 0
+            tol = 1e-12 * abs(g[f"q_{N}"][j]) + slope * N * 2.0 ** -52
+            assert abs(q - g[f"q_{N}"][j]) <= tol, (N, a, q, g[f"q_{N}"][j])
+            tolu = 1e-12 * abs(g[f"qu_{N}"][j]) + np.max(np.diff(srt)) * N * \
+                N * 2.0 ** -51 if N > 1 else 0
+            assert abs(qu - g[f"qu_{N}"][j]) <= tolu
+
+
+def test_weighted_quantile_kat(K):
+    """test/test_weighted_statistics.py:6-20 on the device path."""
+    pts = dev([1, 5, 2.5])
+    w = dev([0.5, 0.2, 0.3])
+
+    def q(a):
+        return float(host(K.weighted_quantile(pts, w, a))[0])
+    assert 1 < q(0.5) < 2.5
+    assert q(0.2) == 1
+    assert 2.5 < q(0.8) < 5
+    assert q(0.9) == 5
+    assert q(1.0) == 5
+
+
+# ------------------------------------------------ (a8) LocalTransition
+@pytest.mark.parametrize("name", golden_names("local_"))
+def test_local_transition(K, name):
+    g = load_golden(name)
+    X, w, k = g["X"], g["w"], int(g["k"])
+    nbr, d2 = K.knn(dev(X), k)
+    np.testing.assert_array_equal(np.sort(host(nbr), axis=1), g["nbr"])
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    np.testing.assert_allclose(host(covs), g["covs"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(host(dets), g["dets"], rtol=1e-11)
+    np.testing.assert_allclose(host(invs), g["inv_covs"], rtol=1e-9,
+                               atol=1e-12)
+    lp = K.local_logpdf(dev(g["pts"]), dev(X), dev(w), invs, dets)
+    np.testing.assert_allclose(np.exp(host(lp)), g["pdf"], rtol=1e-11)
+
+
+# ------------------------------------------------------ simulators
+def test_sim_linear_gaussian(K):
+    rng = np.random.default_rng(1)
+    B, d, S = 3000, 4, 100
+    th = rng.normal(size=(B, d))
+    A = rng.normal(size=(S, d))
+    c = rng.normal(size=S)
+    out = host(K.sim_linear_gaussian(dev(th), dev(A), dev(c), 0.5, 17, 4, 10))
+    z = ref.philox_normal(17, 4, (10 + B) * S)[10 * S:].reshape(B, S)
+    expect = (th @ A.T + c + 0.5 * z).T
+    np.testing.assert_allclose(out, expect, rtol=1e-12, atol=1e-12)

@@ -1,0 +1,51 @@
+"""KDE kernel micro-benchmark on the GPU: pairs/s and FP32 roofline fraction."""
+import math
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from pyabc_amd import kernels as K  # noqa: E402
+
+
+def run(N, M, d, prec="f32", reps=3):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
+    w = torch.rand(N, dtype=torch.float64, device="cuda", generator=g) + 0.5
+    w /= w.sum()
+    Xh = X.cpu().numpy()
+    wh = w.cpu().numpy()
+    from oracle import ref_cpu as ref
+    cov = ref.mvn_fit_cov(Xh, wh)
+    U, rank, lpd = K.psd_whitening(cov)
+    Us = torch.as_tensor(U * math.sqrt(0.5 * K.LOG2E), device="cuda")
+    mu = torch.zeros(d, dtype=torch.float64, device="cuda")
+    pp = K.PackedPopulation(X, w, mu, Us, rank, lpd, prec)
+    theta = X[:M] + 0.1
+    Y = pp.whiten(theta)
+    pp.logpdf_whitened(Y)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        pp.logpdf_whitened(Y)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    t = min(ts)
+    pairs = M * pp.npad
+    fl = (3 * d + 4) * pairs / t
+    print(f"N={N} M={M} d={d} {prec}: {t*1e3:.2f} ms  {pairs/t:.3e} pairs/s "
+          f"{fl/1e12:.1f} TFLOP/s  frac={fl/157.3e12:.3f}  split="
+          f"{K.nat.lib().abc_kde_split(M, pp.npad, d)}", flush=True)
+
+
+if __name__ == "__main__":
+    for (N, M, d, p) in [(262144, 262144, 8, "f32"), (1000000, 1000000, 8, "f32"),
+                         (262144, 262144, 4, "f32"), (262144, 262144, 20, "f32"),
+                         (65536, 65536, 8, "f64")]:
+        run(N, M, d, p)

@@ -1,0 +1,104 @@
+"""Batch simulators for the GPU sampler.
+
+The reference evaluates one Python model call per proposal
+(pyabc/model.py:92-123, 176-239).  The batch sampler instead asks a
+:class:`BatchModel` for the statistics of B proposals at once, stat-major
+``[S, B]`` on the device.  The two synthetic models below are the benchmark
+models of BASELINE.json; each is one HIP kernel with
+Philox4x32-10 noise.
+"""
+import numpy as np
+import torch
+
+from . import kernels as K
+
+
+class BatchModel:
+    """Interface: ``simulate(theta[B, d], seed, sid, offset) -> stats_T[S, B]``.
+
+    ``keys`` are the summary-statistic names in x_0 order; ``name`` as in
+    pyabc.Model.  ``offset`` is the global index of the first row, so that
+    the noise of proposal i is the same however the batch is cut.
+    """
+    name = "batch_model"
+    keys = ()
+
+    @property
+    def n_stats(self):
+        return len(self.keys)
+
+    def simulate(self, theta, seed, sid, offset):  # pragma: no cover
+        raise NotImplementedError
+
+    def observed(self):
+        """x_0 as a dict in key order (optional)."""
+        raise NotImplementedError
+
+
+class LinearGaussianModel(BatchModel):
+    """y = A theta + c + sigma * eps, eps ~ N(0, I_S)  (SURVEY C2/C5)."""
+
+    def __init__(self, A, c=None, sigma=0.5, keys=None, name="linear_gaussian",
+                 x0=None):
+        A = np.asarray(A, dtype=np.float64)
+        self.S, self.d = A.shape
+        self.A_host = A
+        self.c_host = None if c is None else np.asarray(c, dtype=np.float64)
+        self.sigma = float(sigma)
+        self.keys = tuple(keys) if keys is not None else tuple(
+            f"y{k:03d}" for k in range(self.S))
+        self.name = name
+        self._x0 = x0
+        self._dev = {}
+
+    def _tensors(self):
+        dev = torch.cuda.current_device()
+        if dev not in self._dev:
+            A = torch.as_tensor(self.A_host, device="cuda")
+            c = None if self.c_host is None else torch.as_tensor(
+                self.c_host, device="cuda")
+            self._dev[dev] = (A, c)
+        return self._dev[dev]
+
+    def simulate(self, theta, seed, sid, offset):
+        A, c = self._tensors()
+        return K.sim_linear_gaussian(theta, A, c, self.sigma, seed, sid,
+                                     offset)
+
+    def simulate_host(self, theta, rng):
+        """numpy reference of the same model (for CPU baselines)."""
+        theta = np.atleast_2d(theta)
+        y = theta @ self.A_host.T + self.sigma * rng.normal(
+            size=(theta.shape[0], self.S))
+        if self.c_host is not None:
+            y = y + self.c_host
+        return y
+
+    def observed(self):
+        return dict(zip(self.keys, self._x0))
+
+    @staticmethod
+    def benchmark(d, S=100, seed_A=42, seed_x0=7, sigma=0.5):
+        """The synthetic inference problem of SURVEY 8(d): A =
+        RandomState(42).randn(S,d)/sqrt(d), theta_true = linspace(-1,1,d),
+        x_0 = A theta_true + sigma * RandomState(7).randn(S)."""
+        A = np.random.RandomState(seed_A).randn(S, d) / np.sqrt(d)
+        theta_true = np.linspace(-1, 1, d)
+        x0 = A @ theta_true + sigma * np.random.RandomState(seed_x0).randn(S)
+        m = LinearGaussianModel(A, None, sigma, x0=x0)
+        m.theta_true = theta_true
+        return m
+
+
+class GaussianMeanModel(BatchModel):
+    """Quickstart model: y = mean + 0.5 N(0,1)  (doc/examples/
+    parameter_inference.ipynb, model cell)."""
+
+    def __init__(self, sigma=0.5, key="data", name="model"):
+        self.sigma = float(sigma)
+        self.keys = (key,)
+        self.name = name
+
+    def simulate(self, theta, seed, sid, offset):
+        out = K.sim_gaussian_mean(theta, self.sigma, seed, sid, offset)
+        return out.view(1, -1)

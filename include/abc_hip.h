@@ -176,6 +176,14 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
                          double* out_logpdf, void* ws, size_t ws_bytes,
                          hipStream_t stream);
 size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N);
+/* LocalTransition.rvs_single                        local_transition.py:141-145
+ * (CDF index as abc_propose_philox_f64; Cholesky factor of C[idx]) */
+int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
+                                 const double* cdf, const double* covs,
+                                 const double* lo, const double* scale,
+                                 uint64_t seed, uint64_t sid, uint64_t offset,
+                                 int64_t B, double* theta, int64_t* idx,
+                                 uint8_t* in_support, hipStream_t stream);
 
 /* ---------------- synthetic batch simulators (benchmark models) ----------
  * linear-Gaussian y = A theta + c + sigma eps (SURVEY configs C2/C5) and the

@@ -104,6 +104,10 @@ _SIGS = {
     "abc_local_logpdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
                                      c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                      c_size, c_ptr]),
+    "abc_propose_local_philox_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr,
+                                             c_ptr, c_ptr, c_ptr, c_u64,
+                                             c_u64, c_u64, c_i64, c_ptr,
+                                             c_ptr, c_ptr, c_ptr]),
     # simulators
     "abc_sim_linear_gaussian_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                             c_int, c_dbl, c_u64, c_u64, c_u64,

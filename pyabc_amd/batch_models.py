@@ -102,3 +102,32 @@ class GaussianMeanModel(BatchModel):
     def simulate(self, theta, seed, sid, offset):
         out = K.sim_gaussian_mean(theta, self.sigma, seed, sid, offset)
         return out.view(1, -1)
+
+
+def _per_particle_accept(model, t, pars, sum_stats_calculator,
+                         distance_calculator, eps_calculator, acceptor, x_0):
+    """One proposal through a batch model (closure sampling path): B = 1 on
+    the device, then the acceptor, as Model.accept does (model.py:176-239)."""
+    from .model import ModelResult
+    res = model.summary_statistics(t, pars, sum_stats_calculator)
+    acc = acceptor(distance_function=distance_calculator, eps=eps_calculator,
+                   x=res.sum_stats, x_0=x_0, t=t, par=pars)
+    res.distance = acc.distance
+    res.accepted = acc.accept
+    res.weight = acc.weight
+    return res
+
+
+def _per_particle_stats(model, t, pars, sum_stats_calculator):
+    from .model import ModelResult
+    names = sorted(pars.keys())
+    theta = torch.as_tensor(np.array([[float(pars[k]) for k in names]]),
+                            device="cuda")
+    seed = int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+    stats = model.simulate(theta, seed, 0, 0)[:, 0].cpu().numpy()
+    return ModelResult(sum_stats=sum_stats_calculator(
+        dict(zip(model.keys, stats))))
+
+
+BatchModel.summary_statistics = _per_particle_stats
+BatchModel.accept = _per_particle_accept

@@ -20,6 +20,7 @@
 // uniform), d^2 FMAs per pair for the quadratic form, online log-sum-exp
 // in fp64.
 #include "common.hpp"
+#include "philox.hpp"
 
 namespace abc {
 
@@ -355,13 +356,95 @@ __global__ __launch_bounds__(256) void local_pdf_final_kernel(
   out[i] = (m > -INFINITY ? m + log(acc) : -INFINITY) - *logsumw;
 }
 
-__global__ void log_kernel(double* x) { *x = log(*x); }
+
+// LocalTransition.rvs_single (local_transition.py:141-145):
+//   idx ~ choice(N, p=w); theta ~ N(X[idx], C[idx]).
+// The index is the same CDF search as the global kernel (bit-exact for the
+// same u); the Gaussian draw uses the Cholesky factor of C[idx] (numpy uses
+// an SVD factor: same distribution, different map from z to theta).
+template <int D>
+__global__ __launch_bounds__(256) void propose_local_kernel(
+    const double* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ cdf, const double* __restrict__ covs,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
+    double* __restrict__ theta, int64_t* __restrict__ idx_out,
+    uint8_t* __restrict__ sup) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t ui = offset + static_cast<uint64_t>(b);
+  const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
+  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
+  int64_t lo_i = 0, hi_i = N;
+  while (lo_i < hi_i) {
+    const int64_t mid = (lo_i + hi_i) >> 1;
+    if (cdf[mid] <= u) lo_i = mid + 1; else hi_i = mid;
+  }
+  const int64_t idx = lo_i < N ? lo_i : N - 1;
+  double L[D][D];
+  const double* C = covs + idx * d * d;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = C[i * d + j];
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      if (i == j)
+        L[i][i] = sqrt(s > 0.0 ? s : 0.0);
+      else
+        L[i][j] = L[j][j] > 0.0 ? s / L[j][j] : 0.0;
+    }
+  double z[D];
+  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
+  for (int k = 0; k < d; ++k) {
+    const uint64_t zi = zi0 + k;
+    double c0, c1;
+    box_muller(philox_block(seed, 2 * sid + 1, zi >> 1), c0, c1);
+    z[k] = (zi & 1) ? c1 : c0;
+  }
+  bool ok = true;
+  for (int i = 0; i < d; ++i) {
+    double s = 0.0;
+    for (int k = 0; k <= i; ++k) s = fma(L[i][k], z[k], s);
+    const double th = X[idx * d + i] + s;
+    theta[b * d + i] = th;
+    if (lo) {
+      const double x = (th - lo[i]) / scale[i];
+      ok = ok && x >= 0.0 && x <= 1.0;
+    }
+  }
+  idx_out[b] = lo_i;
+  sup[b] = ok ? 1 : 0;
+}
 
 }  // namespace abc
 
 using namespace abc;
 
 extern "C" {
+
+int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
+                                 const double* cdf, const double* covs,
+                                 const double* lo, const double* scale,
+                                 uint64_t seed, uint64_t sid, uint64_t offset,
+                                 int64_t B, double* theta, int64_t* idx,
+                                 uint8_t* in_support, hipStream_t st) {
+  ABC_REQUIRE(N > 0 && B >= 0 && d >= 1 && d <= 16, "propose_local: bad sizes");
+  if (B == 0) return kOk;
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+  if (d <= 4)
+    hipLaunchKernelGGL((propose_local_kernel<4>), dim3(g), dim3(256), 0, st, X,
+                       N, d, cdf, covs, lo, scale, seed, sid, offset, B, theta,
+                       idx, in_support);
+  else if (d <= 8)
+    hipLaunchKernelGGL((propose_local_kernel<8>), dim3(g), dim3(256), 0, st, X,
+                       N, d, cdf, covs, lo, scale, seed, sid, offset, B, theta,
+                       idx, in_support);
+  else
+    hipLaunchKernelGGL((propose_local_kernel<16>), dim3(g), dim3(256), 0, st,
+                       X, N, d, cdf, covs, lo, scale, seed, sid, offset, B,
+                       theta, idx, in_support);
+  ABC_LAUNCH_CHECK("propose_local_kernel");
+  return kOk;
+}
 
 size_t abc_knn_workspace_bytes(int64_t N, int k) {
   (void)N;

@@ -129,6 +129,7 @@ class GenerationEngine:
         self.valid_rate_est = 1.0
         self.timers = {}
         self.kde_events = None   # list -> (start, end, M, N) per KDE launch
+        self.max_rounds = None
 
     # ------------------------------------------------------------------
     def _sid(self, t, kind):
@@ -151,13 +152,19 @@ class GenerationEngine:
         return GenerationResult(theta=theta, stats_T=stats, n_eval=nq,
                                 rec_stats_T=stats, n_rec=nq)
 
-    def sample_generation(self, t, n, fit, x0, fw, eps):
+    def sample_generation(self, t, n, fit, x0, fw, eps, keep_stats=None,
+                          record=None):
         """Proposals until this rank's quota of n is accepted, then KDE
-        weights.  Returns the rank-local accepted rows."""
+        weights.  ``fit=None`` proposes from the prior (generation 0,
+        weight 1).  Returns the rank-local accepted rows; with ``record``
+        also the statistics of every evaluated proposal up to the last
+        acceptance (record_rejected, sampler/base.py:119-141)."""
+        keep_stats = self.record_stats if keep_stats is None else keep_stats
+        record = self.record_stats if record is None else record
         nq = self.quota(n)
         tm = {}
         t0 = time.perf_counter()
-        cdf = fit.cdf
+        cdf = fit.cdf if fit is not None else None
         rounds = []
         n_acc = 0
         prop_off = 0
@@ -168,16 +175,21 @@ class GenerationEngine:
                 self.min_batch,
                 math.ceil(1.2 * need / max(self.acc_rate_est, 1e-3)
                           / max(self.valid_rate_est, 1e-3)))))
-            theta_all, idx, sup = K.propose_philox(
-                fit.X, cdf, fit.A, self.lo, self.scale, self.seed,
-                self._sid(t, 0), prop_off, B)
+            if fit is None:
+                theta = K.prior_uniform(self.lo, self.scale, self.seed,
+                                        self._sid(t, 0), prop_off, B)
+                nv = B
+            else:
+                theta_all, idx, sup = K.propose_philox(
+                    fit.X, cdf, fit.A, self.lo, self.scale, self.seed,
+                    self._sid(t, 0), prop_off, B)
+                vpos, vcount = K.compact(sup)
+                nv = int(vcount.item())                             # sync 1
+                self.valid_rate_est = max(nv / B, 1e-3)
+                theta = K.gather_rows(theta_all, vpos, nv) if nv else None
             prop_off += B
-            vpos, vcount = K.compact(sup)
-            nv = int(vcount.item())                                 # sync 1
-            self.valid_rate_est = max(nv / B, 1e-3)
             if nv == 0:
                 continue
-            theta = K.gather_rows(theta_all, vpos, nv)
             stats = self.model.simulate(theta, self.seed, self._sid(t, 1),
                                         sim_off)
             sim_off += nv
@@ -187,6 +199,11 @@ class GenerationEngine:
             self.acc_rate_est = max(na / nv, 1e-4)
             rounds.append((theta, stats, d, apos, na, nv, guard))
             n_acc += na
+            if self.max_rounds is not None and len(rounds) >= self.max_rounds \
+                    and n_acc < nq:
+                raise RuntimeError("acceptance rate too low: "
+                                   f"{n_acc}/{sim_off} after {len(rounds)} "
+                                   "rounds")
         tm["propose_sim_dist"] = time.perf_counter() - t0
         # first nq accepted in proposal order; evaluations up to the nq-th
         thetas, ds, stats_acc, recs = [], [], [], []
@@ -202,29 +219,36 @@ class GenerationEngine:
             n_eval += last
             thetas.append(theta.index_select(0, sel))
             ds.append(d.index_select(0, sel))
-            if self.record_stats:
+            if keep_stats:
                 stats_acc.append(stats.index_select(1, sel))
+            if record:
                 recs.append(stats[:, :last])
-            n_guard += int(guard[:nv].sum().item())
+            n_guard += int(guard[:last].sum().item())
             left -= take
             if left == 0:
                 break
-        theta_acc = torch.cat(thetas)
-        d_acc = torch.cat(ds)
+        theta_acc = torch.cat(thetas) if thetas else torch.empty(
+            (0, self.d), dtype=F64, device=self.dev)
+        d_acc = torch.cat(ds) if ds else torch.empty(0, dtype=F64,
+                                                     device=self.dev)
         torch.cuda.synchronize()
         tm["select"] = time.perf_counter() - t0 - tm["propose_sim_dist"]
         t1 = time.perf_counter()
-        if self.kde_events is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            Y = fit.packed.whiten(theta_acc)
-            e0.record()
-            logpd = fit.packed.logpdf_whitened(Y)
-            e1.record()
-            self.kde_events.append((e0, e1, theta_acc.shape[0], fit.n))
+        if fit is None:
+            logpd = None
+            w = torch.ones(theta_acc.shape[0], dtype=F64, device=self.dev)
         else:
-            logpd = fit.logpdf(theta_acc)
-        w = K.importance_weights(logpd, None, self.prior_pd)
+            if self.kde_events is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                Y = fit.packed.whiten(theta_acc)
+                e0.record()
+                logpd = fit.packed.logpdf_whitened(Y)
+                e1.record()
+                self.kde_events.append((e0, e1, theta_acc.shape[0], fit.n))
+            else:
+                logpd = fit.logpdf(theta_acc)
+            w = K.importance_weights(logpd, None, self.prior_pd)
         torch.cuda.synchronize()
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm

@@ -341,6 +341,18 @@ def local_logpdf(pts, X, w, invs, dets):
     return out
 
 
+def propose_local(X, cdf, covs, seed, sid, offset, B, lo=None, scale=None):
+    X = _contig(X, F64)
+    N, d = X.shape
+    theta = torch.empty((B, d), dtype=F64, device=_dev())
+    idx = torch.empty(B, dtype=torch.int64, device=_dev())
+    sup = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_propose_local_philox_f64", ptr(X), N, d, ptr(cdf),
+         ptr(covs.contiguous()), ptr(lo), ptr(scale), seed, sid, offset, B,
+         ptr(theta), ptr(idx), ptr(sup), nat.stream())
+    return theta, idx, sup
+
+
 # ---------------------------------------------------------------------------
 # synthetic simulators
 # ---------------------------------------------------------------------------

@@ -1,0 +1,196 @@
+"""Particles and populations (API of pyabc/population.py:1-286), plus the
+columnar device population the GPU sampler produces."""
+import numpy as np
+import pandas as pd
+import torch
+
+from . import kernels as K
+from .frames import DeviceFrame
+from .distance import DeviceStats
+
+
+class Particle:
+    def __init__(self, m, parameter, weight, accepted_sum_stats,
+                 accepted_distances, rejected_sum_stats=None,
+                 rejected_distances=None, accepted=True):
+        self.m = m
+        self.parameter = parameter
+        self.weight = weight
+        self.accepted_sum_stats = accepted_sum_stats
+        self.accepted_distances = accepted_distances
+        self.rejected_sum_stats = rejected_sum_stats or []
+        self.rejected_distances = rejected_distances or []
+        self.accepted = accepted
+
+
+class Population:
+    """List of particles; weights normalised per model on construction
+    (population.py:120-142)."""
+
+    def __init__(self, particles):
+        self._list = list(particles)
+        self._model_probabilities = None
+        self._normalize_weights()
+
+    def __len__(self):
+        return len(self._list)
+
+    def get_list(self):
+        return self._list.copy()
+
+    def to_dict(self):
+        store = {}
+        for p in self._list:
+            store.setdefault(p.m, []).append(p)
+        return store
+
+    def _normalize_weights(self):
+        store = self.to_dict()
+        totals = {m: sum(p.weight for p in pl) for m, pl in store.items()}
+        tot = sum(totals.values())
+        self._model_probabilities = {m: w / tot for m, w in totals.items()}
+        for m, pl in store.items():
+            for p in pl:
+                p.weight /= totals[m]
+
+    def update_distances(self, distance_to_ground_truth):
+        for p in self._list:
+            for i in range(len(p.accepted_distances)):
+                p.accepted_distances[i] = distance_to_ground_truth(
+                    p.accepted_sum_stats[i], p.parameter)
+
+    def get_model_probabilities(self):
+        return self._model_probabilities
+
+    def get_alive_models(self):
+        return list(self._model_probabilities.keys())
+
+    def nr_of_models_alive(self):
+        return len(self.get_alive_models())
+
+    def get_weighted_distances(self):
+        rows = []
+        for p in self._list:
+            mp = self._model_probabilities[p.m]
+            for d in p.accepted_distances:
+                rows.append({"distance": d, "w": p.weight * mp})
+        return pd.DataFrame(rows)
+
+    def get_weighted_sum_stats(self):
+        weights, sum_stats = [], []
+        for p in self._list:
+            mp = self._model_probabilities[p.m]
+            n = len(p.accepted_sum_stats)
+            for s in p.accepted_sum_stats:
+                weights.append(p.weight * mp / n)
+                sum_stats.append(s)
+        return weights, sum_stats
+
+    def get_accepted_sum_stats(self):
+        return sum((p.accepted_sum_stats for p in self._list), [])
+
+    def get_for_keys(self, keys):
+        return {k: [getattr(p, k) for p in self._list] for k in keys}
+
+    def get_distribution(self, m=0):
+        pl = [p for p in self._list if p.m == m]
+        df = pd.DataFrame([dict(p.parameter) for p in pl])
+        if len(df.columns):
+            df = df[sorted(df.columns)]
+        w = np.array([p.weight for p in pl], dtype=np.float64)
+        return df, w
+
+
+class WeightedDistances:
+    """``get_weighted_distances`` of a device population: columns
+    ``distance`` and ``w`` as device tensors (host copies on demand)."""
+
+    def __init__(self, d, w):
+        self.distance_tensor = d
+        self.w_tensor = w
+
+    @property
+    def distance(self):
+        return pd.Series(self.distance_tensor.cpu().numpy(), name="distance")
+
+    @property
+    def w(self):
+        return pd.Series(self.w_tensor.cpu().numpy(), name="w")
+
+    def __len__(self):
+        return self.distance_tensor.numel()
+
+    def to_pandas(self):
+        return pd.DataFrame({"distance": self.distance.values,
+                             "w": self.w.values})
+
+
+class ColumnarPopulation:
+    """Single-model population as device columns: theta [n, d], normalised
+    weights [n], distances [n], accepted statistics [S, n] (optional).
+    Same methods as :class:`Population`; ``get_list`` materialises particles
+    on the host only when asked."""
+
+    def __init__(self, theta, w, d, names, stats_T=None, stat_keys=None,
+                 m=0, normalize=True):
+        self.theta = theta
+        self.d = d
+        self.names = list(names)
+        self.stats_T = stats_T
+        self.stat_keys = list(stat_keys) if stat_keys is not None else None
+        self.m = m
+        if normalize:
+            s = K.dsum(w)
+            w = w.clone()
+            K.scale_inplace(w, s)
+        self.w = w
+        self._model_probabilities = {m: 1.0}
+
+    def __len__(self):
+        return self.theta.shape[0]
+
+    def get_model_probabilities(self):
+        return self._model_probabilities
+
+    def get_alive_models(self):
+        return [self.m]
+
+    def nr_of_models_alive(self):
+        return 1
+
+    def get_weighted_distances(self):
+        return WeightedDistances(self.d, self.w)
+
+    def get_accepted_sum_stats(self):
+        if self.stats_T is None:
+            raise ValueError("statistics of this population were not kept")
+        return DeviceStats(self.stats_T, self.stat_keys)
+
+    def update_distances_device(self, distance, t, x_0):
+        """Recompute distances under an updated distance (smc.py:978-984)
+        with the batch kernel."""
+        if self.stats_T is None:
+            raise ValueError("statistics of this population were not kept")
+        self.d, _, _ = distance.batch(self.stats_T, t, x_0, np.inf)
+        return self.d
+
+    def update_distances(self, distance_to_ground_truth):
+        raise NotImplementedError(
+            "ColumnarPopulation: use update_distances_device (batch kernel)")
+
+    def get_distribution(self, m=0):
+        return DeviceFrame(self.theta, self.names), self.w
+
+    def get_list(self):
+        th = self.theta.cpu().numpy()
+        w = self.w.cpu().numpy()
+        d = self.d.cpu().numpy()
+        st = self.stats_T.cpu().numpy() if self.stats_T is not None else None
+        out = []
+        from .parameters import Parameter
+        for i in range(th.shape[0]):
+            ss = [dict(zip(self.stat_keys, st[:, i]))] if st is not None \
+                else [{}]
+            out.append(Particle(self.m, Parameter(dict(zip(self.names, th[i]))),
+                                float(w[i]), ss, [float(d[i])]))
+        return out

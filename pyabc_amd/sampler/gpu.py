@@ -1,0 +1,215 @@
+"""GPUBatchSampler: the drop-in sampler that runs a whole generation on the
+MI355X (reference boundary: ``Sampler.sample_until_n_accepted``,
+pyabc/sampler/base.py:196-234, called at pyabc/smc.py:888 and 524).
+
+The reference hands the sampler an opaque per-proposal closure
+(``_create_simulate_function``, smc.py:536-600).  :class:`pyabc_amd.ABCSMC`
+attaches a :class:`BatchSpec` to that closure; when the spec describes a
+configuration the device engine covers (one :class:`BatchModel`, uniform-box
+prior, :class:`MultivariateNormalTransition`, p-norm distance, uniform
+acceptance, one simulation per parameter), the generation runs through
+:mod:`pyabc_amd.engine`.  Otherwise the closure is called proposal by
+proposal with SingleCoreSampler semantics (user Python models), its
+transition / distance / epsilon calls still computing on the device.
+"""
+import numpy as np
+import torch
+
+from .base import Sampler, Sample
+from ..distance import DeviceStats, PNormDistance
+from ..distributed import Comm
+from ..engine import GenerationEngine
+from ..population import ColumnarPopulation
+from ..batch_models import BatchModel
+
+
+class BatchSpec:
+    """Everything ``simulate_one`` closes over, for batch evaluation."""
+
+    def __init__(self, t, kind, models, priors, transitions, distance, eps,
+                 acceptor, x_0, nr_samples_per_parameter, summary_statistics,
+                 model_probabilities=None):
+        self.t = t
+        self.kind = kind           # "calibration" (all accepted) or "smc"
+        self.models = models
+        self.priors = priors
+        self.transitions = transitions
+        self.distance = distance
+        self.eps = eps
+        self.acceptor = acceptor
+        self.x_0 = x_0
+        self.nr_samples_per_parameter = nr_samples_per_parameter
+        self.summary_statistics = summary_statistics
+        self.model_probabilities = model_probabilities
+
+    def unsupported_reason(self):
+        from ..acceptor import UniformAcceptor
+        from ..transition import MultivariateNormalTransition
+        if len(self.models) != 1:
+            return "model selection (several models)"
+        if not isinstance(self.models[0], BatchModel):
+            return "model is not a BatchModel"
+        if self.priors[0].uniform_box() is None:
+            return "prior is not a product of uniform marginals"
+        if self.nr_samples_per_parameter != 1:
+            return "nr_samples_per_parameter != 1"
+        if getattr(self.summary_statistics, "__name__", "") != "identity":
+            return "custom summary_statistics"
+        if self.kind == "smc":
+            if not isinstance(self.distance, PNormDistance):
+                return "distance is not a (Adaptive)PNormDistance"
+            if not isinstance(self.acceptor, UniformAcceptor) or \
+                    self.acceptor.use_complete_history:
+                return "acceptor is not UniformAcceptor(current time)"
+            if self.t > 0 and not isinstance(
+                    self.transitions[0], MultivariateNormalTransition):
+                return "transition is not MultivariateNormalTransition"
+        return None
+
+
+class BatchSample(Sample):
+    """Columnar sample: the accepted population on the device plus the
+    recorded statistics (accepted and rejected, evaluation order)."""
+
+    def __init__(self, population, recorded, record_rejected, ok=True):
+        super().__init__(record_rejected=record_rejected, ok=ok)
+        self.population = population
+        self.recorded = recorded
+
+    @property
+    def n_accepted(self):
+        return len(self.population)
+
+    def get_accepted_population(self):
+        return self.population
+
+    @property
+    def all_sum_stats(self):
+        return self.recorded
+
+    def first_m_sum_stats(self, m):
+        if self.recorded is None:
+            return self.population.get_accepted_sum_stats()
+        n = len(self.recorded)
+        if m >= n:
+            return self.recorded
+        return DeviceStats(self.recorded.stats_T[:, :int(m)],
+                           self.recorded.keys)
+
+    def first_m_particles(self, m):
+        return self.population.get_list()[:int(min(m, len(self.population)))]
+
+
+class GPUBatchSampler(Sampler):
+    """Runs each generation as batched HIP kernels on the current device.
+
+    Parameters: ``seed`` (Philox seed; default drawn from numpy's global
+    state), ``min_batch`` / ``max_batch`` proposals per round,
+    ``kde_precision`` ("f32" or "f64" KDE kernel), ``comm`` (multi-GPU
+    sharding, default from the torchrun environment).
+    """
+
+    def __init__(self, seed=None, min_batch=1 << 14, max_batch=1 << 22,
+                 kde_precision="f32", comm=None):
+        super().__init__()
+        self.seed = seed
+        self.min_batch = min_batch
+        self.max_batch = max_batch
+        self.kde_precision = kde_precision
+        self.comm = comm
+        self._engines = {}
+        self.last_timers = {}
+        self.fallback_reason = None
+
+    def _engine(self, spec):
+        model = spec.models[0]
+        names, lo, sc = spec.priors[0].uniform_box()
+        key = (id(model), tuple(lo), tuple(sc))
+        eng = self._engines.get(key)
+        if eng is None:
+            seed = self.seed if self.seed is not None else int(
+                np.random.randint(0, 2 ** 62, dtype=np.int64))
+            eng = GenerationEngine(
+                model, lo, sc, comm=self.comm or Comm.from_env(),
+                seed=seed, min_batch=self.min_batch,
+                max_batch=self.max_batch, kde_precision=self.kde_precision)
+            eng.max_rounds = 100000
+            self._engines[key] = eng
+        return eng, names
+
+    def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
+                                all_accepted=False):
+        spec = getattr(simulate_one, "batch_spec", None)
+        reason = "no batch spec" if spec is None else spec.unsupported_reason()
+        self.fallback_reason = reason
+        if reason is not None:
+            return self._closure_path(n, simulate_one, max_eval)
+        eng, names = self._engine(spec)
+        model = spec.models[0]
+        keys = list(model.keys)
+        record = self.sample_factory.record_rejected
+        if spec.kind == "calibration":
+            res = eng.sample_generation(spec.t, n, None, None, None, np.inf,
+                                        keep_stats=True, record=False)
+            # calibration distances are computed later (smc.py:516-534)
+            res.d = torch.full_like(res.w, np.inf)
+        else:
+            keys_d, x0d, fwd = spec.distance.device_params(spec.t, spec.x_0)
+            if keys_d != keys:
+                perm = [keys.index(k) for k in keys_d]
+                model = _PermutedModel(model, perm)
+                eng.model = model
+            eps = spec.eps(spec.t)
+            fit = spec.transitions[0].device_fit if spec.t > 0 and \
+                spec.transitions[0].device_fit is not None else None
+            res = eng.sample_generation(spec.t, n, fit, x0d, fwd, eps,
+                                        keep_stats=True, record=record)
+            eng.model = spec.models[0]
+            keys = keys_d
+        comm = eng.comm
+        theta = comm.all_gather_rows(res.theta)
+        d = comm.all_gather_rows(res.d)
+        w = comm.all_gather_rows(res.w)
+        stats = comm.all_gather_rows(res.stats_T.t().contiguous()).t() \
+            if res.stats_T is not None else None
+        rec = None
+        if res.rec_stats_T is not None:
+            rec = DeviceStats(comm.all_gather_rows(
+                res.rec_stats_T.t().contiguous()).t().contiguous(), keys)
+        self.nr_evaluations_ = comm.all_reduce_int(res.n_eval)
+        self.last_timers = dict(eng.timers)
+        pop = ColumnarPopulation(theta, w, d, names,
+                                 stats.contiguous() if stats is not None
+                                 else None, keys)
+        return BatchSample(pop, rec, record)
+
+    def _closure_path(self, n, simulate_one, max_eval):
+        nr = 0
+        sample = self._create_empty_sample()
+        for _ in range(n):
+            while True:
+                if nr >= max_eval:
+                    break
+                p = simulate_one()
+                sample.append(p)
+                nr += 1
+                if p.accepted:
+                    break
+        self.nr_evaluations_ = nr
+        if sample.n_accepted < n:
+            sample.ok = False
+        return sample
+
+
+class _PermutedModel(BatchModel):
+    """Presents a model's statistics in the distance's key order."""
+
+    def __init__(self, model, perm):
+        self.model = model
+        self.perm = torch.as_tensor(perm, device="cuda")
+        self.keys = tuple(model.keys[i] for i in perm)
+        self.name = model.name
+
+    def simulate(self, theta, seed, sid, offset):
+        return self.model.simulate(theta, seed, sid, offset).index_select(
+            0, self.perm).contiguous()

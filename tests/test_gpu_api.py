@@ -1,0 +1,219 @@
+"""The drop-in API on the GPU: ABCSMC end to end against the reference's
+own runs (Monte-Carlo pins from tools/gen_golden.py gen_e2e), transition
+contracts (test/test_transition.py), adaptive distance and epsilon KATs."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pa():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pyabc_amd
+    return pyabc_amd
+
+
+def _post_stats(h, names):
+    out = []
+    for t in range(h.max_t + 1):
+        df, w = h.distribution_numpy(0, t)
+        X = df[names].values
+        w = w / w.sum()
+        m = (X * w[:, None]).sum(0)
+        s = np.sqrt(((X - m) ** 2 * w[:, None]).sum(0))
+        out.append((m, s))
+    return out
+
+
+def _check_against_reference(g, prefix, R, eps, stats, names_dim):
+    ref_eps = np.array([g[f"{prefix}_eps_{r}"] for r in range(R)])
+    ref_mean = np.array([g[f"{prefix}_mean_{r}"][-1] for r in range(R)])
+    ref_std = np.array([g[f"{prefix}_std_{r}"][-1] for r in range(R)])
+    T = ref_eps.shape[1]
+    assert len(eps) >= T
+    for t in range(T):
+        lo, hi = ref_eps[:, t].min(), ref_eps[:, t].max()
+        span = hi - lo
+        assert lo - 2 * span - 0.05 * lo <= eps[t] <= hi + 2 * span + \
+            0.05 * hi, (t, eps[t], ref_eps[:, t])
+    m, s = stats[T - 1]
+    spread = ref_mean.std(0) + ref_std.mean(0) / np.sqrt(200)
+    np.testing.assert_array_less(np.abs(m - ref_mean.mean(0)),
+                                 5 * spread + 1e-3)
+    np.testing.assert_allclose(s, ref_std.mean(0), rtol=0.25)
+
+
+def test_config1_quickstart_batch_path(pa):
+    """C1: quickstart Gaussian mean, N=1000, MedianEpsilon, PNorm p=2."""
+    g = load_golden("e2e_stats")
+    np.random.seed(0)
+    prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
+    sampler = pa.GPUBatchSampler(seed=11)
+    abc = pa.ABCSMC(pa.GaussianMeanModel(), prior, pa.PNormDistance(p=2),
+                    population_size=1000, eps=pa.MedianEpsilon(),
+                    sampler=sampler)
+    abc.new("mem://c1", {"data": 2.5})
+    h = abc.run(minimum_epsilon=0.1, max_nr_populations=4)
+    assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
+    eps = h.get_all_populations().epsilon.values
+    _check_against_reference(g, "c1", 5, eps, _post_stats(h, ["mean"]), 1)
+
+
+def test_config2_adaptive_mad_batch_path(pa):
+    """C2 (N reduced to 1000): 4-param linear Gaussian, S=100,
+    AdaptivePNormDistance(MAD), QuantileEpsilon(0.5)."""
+    g = load_golden("e2e_stats")
+    A, x0v = g["A2"], g["x0_2"]
+    S, d = A.shape
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k}" for k in range(d)]
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    sampler = pa.GPUBatchSampler(seed=5)
+    abc = pa.ABCSMC(model, prior,
+                    pa.AdaptivePNormDistance(
+                        p=2, scale_function=pa.median_absolute_deviation),
+                    population_size=1000, eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=sampler)
+    abc.new("mem://c2", dict(zip(keys, x0v)))
+    h = abc.run(max_nr_populations=4)
+    assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
+    eps = h.get_all_populations().epsilon.values
+    _check_against_reference(g, "c2", 3, eps, _post_stats(h, names), d)
+
+
+def test_closure_path_python_model(pa):
+    """A plain Python model cannot be batched: the sampler calls the closure
+    per proposal; transitions / distances still compute on the device."""
+    np.random.seed(3)
+
+    def model(par):
+        return {"data": par["mean"] + 0.5 * np.random.randn()}
+    prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
+    sampler = pa.GPUBatchSampler()
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2), population_size=100,
+                    sampler=sampler)
+    abc.new("mem://closure", {"data": 2.5})
+    h = abc.run(max_nr_populations=3)
+    assert sampler.fallback_reason == "model is not a BatchModel"
+    df, w = h.distribution_numpy(0, h.max_t)
+    m = np.sum(df["mean"].values * w) / w.sum()
+    assert abs(m - 2.5) < 0.35
+
+
+def _data(n, k=2):
+    cols = ["a", "b"][:k]
+    df = pd.DataFrame({c: np.random.rand(n) for c in cols})
+    return df, np.ones(n) / n
+
+
+@pytest.mark.parametrize("kind", ["mvn", "local"])
+def test_transition_contracts(pa, kind):
+    """test/test_transition.py:26-39, 101-152 on the GPU transitions."""
+    make = (lambda: pa.MultivariateNormalTransition()) if kind == "mvn" \
+        else (lambda: pa.LocalTransition())
+    np.random.seed(0)
+    tr = make()
+    df, w = _data(20)
+    tr.fit(df, w)
+    s = tr.rvs()
+    assert (s.index == pd.Index(["a", "b"])).all()
+    single = tr.pdf(df.iloc[0])
+    multiple = tr.pdf(df)
+    assert isinstance(single, float)
+    assert multiple.shape == (20,)
+    test = df.iloc[0]
+    assert tr.pdf(test) == tr.pdf(test[::-1])
+    assert np.isfinite(tr.score(df, w))
+    many = tr.rvs(size=7)
+    assert many.shape == (7, 2)
+    with pytest.raises(pa.NotEnoughParticles):
+        make().fit(*_data(0))
+    for n in [1, 2]:
+        t2 = make()
+        t2.fit(*_data(n))
+        assert np.isfinite(t2.pdf(df.iloc[0]))
+
+
+def test_mvn_transition_api_vs_golden(pa):
+    g = load_golden("kde_N4096_M1024_d8")
+    cols = [f"p{k:02d}" for k in range(8)]
+    tr = pa.MultivariateNormalTransition()
+    tr.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
+    np.testing.assert_allclose(tr.cov, g["cov"], rtol=1e-12)
+    got = tr.pdf(pd.DataFrame(g["theta"], columns=cols))
+    np.testing.assert_allclose(got, g["transition_pd"], rtol=1e-5)
+    tr64 = pa.MultivariateNormalTransition(kde_precision="f64")
+    tr64.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
+    got = tr64.pdf(pd.DataFrame(g["theta"], columns=cols))
+    np.testing.assert_allclose(got, g["transition_pd"], rtol=1e-12)
+
+
+def test_local_transition_api_vs_golden(pa):
+    g = load_golden("local_N2000_d6_k50")
+    cols = [f"p{k:02d}" for k in range(6)]
+    tr = pa.LocalTransition(k=50, k_fraction=None)
+    tr.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
+    assert tr.k == int(g["k"])
+    np.testing.assert_allclose(tr.covs, g["covs"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(tr.determinants, g["dets"], rtol=1e-11)
+    got = tr.pdf(pd.DataFrame(g["pts"], columns=cols))
+    np.testing.assert_allclose(got, g["pdf"], rtol=1e-11)
+
+
+@pytest.mark.parametrize("tag", ["even_n1000", "odd_n999"])
+def test_adaptive_distance_api_vs_golden(pa, tag):
+    g = load_golden(f"adaptive_{tag}_S100")
+    rng = np.random.default_rng(300)
+    S = 100
+    keys = [f"s{k:03d}" for k in range(S)]
+    keys = [keys[k] for k in rng.permutation(S)]
+    x0 = dict(zip(keys, g["x0"]))
+    recs = [dict(zip(keys, row)) for row in g["data"]]
+    for name, sf in [("mad", pa.median_absolute_deviation), ("std", None)]:
+        dist = pa.AdaptivePNormDistance(p=2, scale_function=sf)
+        dist.initialize(0, lambda: recs, x0)
+        w = np.array([dist.weights[0][k] for k in keys])
+        if name == "mad":
+            np.testing.assert_array_equal(w, g["w_mad"])
+        else:
+            np.testing.assert_allclose(w, g["w_std"], rtol=1e-12)
+
+
+def test_distance_and_epsilon_kats(pa):
+    """test/test_distance_function.py:75-91,132-150; test/test_epsilon.py:25-47;
+    test/test_weighted_statistics.py:6-20 through the device path."""
+    x0 = {"s1": 0, "s2": 0, "s3": 1}
+    smp = [{"s1": -1, "s2": -1, "s3": -1}, {"s1": -1, "s2": 0, "s3": 1}]
+    dist = pa.PNormDistance()
+    dist.initialize(0, lambda: smp, x_0=x0)
+    assert dist(smp[0], smp[1], t=0) == pow(1 ** 2 + 2 ** 2, 1 / 2)
+    ad = pa.AdaptivePNormDistance(initial_weights={"s1": 1, "s2": 2, "s3": 3})
+    ad.initialize(0, lambda: smp, x_0=x0)
+    assert ad(smp[0], smp[1], t=0) == pow(sum([(2 * 1) ** 2, (3 * 2) ** 2]),
+                                          1 / 2)
+    ad.update(1, lambda: smp)
+    assert ad.weights[1] != ad.weights[0]
+    df = pd.DataFrame({"distance": [1, 2, 3, 4], "w": [2, 1, 1, 1]})
+    eps = pa.QuantileEpsilon(initial_epsilon=5.1, alpha=0.5,
+                             quantile_multiplier=1.1, weighted=False)
+    eps.initialize(0, lambda: df, lambda: None, None, None)
+    assert np.isclose(eps(0), 5.1)
+    eps.update(1, lambda: df, lambda: None, None, None)
+    assert np.isclose(eps(1), 1.1 * 2.5)
+    eps = pa.QuantileEpsilon(alpha=0.9, weighted=True)
+    eps.initialize(0, lambda: df, lambda: None, None, None)
+    assert 3 <= eps(0) <= 4
+    ws = pa.weighted_statistics
+    pts, w = np.array([1, 5, 2.5]), np.array([0.5, 0.2, 0.3])
+    assert 1 < ws.weighted_quantile(pts, w) < 2.5
+    assert ws.weighted_quantile(pts, w, alpha=0.2) == 1
+    assert ws.weighted_quantile(pts, w, alpha=0.9) == 5
+    assert ws.weighted_quantile(pts, w, alpha=1.0) == 5
+    assert ws.weighted_mean(pts, w) == 2.25

@@ -1,0 +1,171 @@
+"""Host-side logic of the drop-in API (no GPU): configuration objects,
+contracts and the multi-process plumbing (gloo, world_size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import pyabc_amd as pa
+from pyabc_amd.distributed import Comm
+from pyabc_amd.sampler.gpu import BatchSpec
+
+
+def test_uniform_box_and_rv_bounds():
+    prior = pa.Distribution(b=pa.RV("uniform", -1, 2),
+                            a=pa.RV("uniform", loc=0.5, scale=3))
+    names, lo, sc = prior.uniform_box()
+    assert names == ["a", "b"]
+    np.testing.assert_array_equal(lo, [0.5, -1])
+    np.testing.assert_array_equal(sc, [3, 2])
+    assert pa.Distribution(x=pa.RV("norm", 0, 1)).uniform_box() is None
+    # scipy support semantics at the boundary
+    assert prior.pdf(pa.Parameter(a=3.5, b=1.0)) > 0
+    assert prior.pdf(pa.Parameter(a=np.nextafter(3.5, 4), b=0.0)) == 0
+
+
+def test_population_normalisation_matches_reference_fixture(golden):
+    g = golden("kde_N4096_M1024_d8")
+    parts = [pa.Particle(0, pa.Parameter(x=float(i)), float(w), [{}], [0.0])
+             for i, w in enumerate(g["weight"])]
+    pop = pa.Population(parts)
+    w = np.array([p.weight for p in pop.get_list()])
+    np.testing.assert_array_equal(w, g["weight_norm"])
+    assert pop.get_model_probabilities() == {0: 1.0}
+
+
+class _WrongOutputSampler(pa.SingleCoreSampler):
+    def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
+                                all_accepted=False):
+        return super().sample_until_n_accepted(n + 1, simulate_one, max_eval,
+                                               all_accepted)
+
+
+def test_sampler_meta_contract():
+    """test/test_samplers.py:66-70, 206-214: wrong n raises."""
+    def sim():
+        return pa.Particle(0, {}, 1.0, [{}], [0.0], accepted=True)
+    s = _WrongOutputSampler()
+    with pytest.raises(AssertionError):
+        s.sample_until_n_accepted(10, sim)
+    ok = pa.SingleCoreSampler().sample_until_n_accepted(10, sim)
+    assert ok.n_accepted == 10
+
+
+def test_singlecore_counts_evaluations():
+    rng = np.random.default_rng(0)
+
+    def sim():
+        acc = bool(rng.uniform() < 0.3)
+        return pa.Particle(0, {}, 1.0, [{"a": 1}], [0.0], [{"a": 2}], [1.0],
+                           accepted=acc)
+    smp = pa.SingleCoreSampler()
+    smp.sample_factory.record_rejected = True
+    sample = smp.sample_until_n_accepted(50, sim)
+    assert sample.n_accepted == 50
+    assert len(sample.first_m_particles(10 ** 9)) == smp.nr_evaluations_
+
+
+def test_pnorm_weight_formatting():
+    w = pa.PNormDistance.format_dict(None, 3, ["a", "b"])
+    assert w == {3: {"a": 1., "b": 1.}}
+    assert pa.PNormDistance.format_dict({"a": 2}, 1, ["a"]) == {1: {"a": 2}}
+    assert pa.PNormDistance.get_for_t_or_latest({0: 1, 5: 2}, 7) == 2
+    with pytest.raises(ValueError):
+        pa.PNormDistance(p=0.5)
+
+
+def test_epsilon_api():
+    with pytest.raises(ValueError):
+        pa.QuantileEpsilon(alpha=0)
+    assert np.isclose(pa.ConstantEpsilon(42)(100), 42)
+    with pytest.raises(Exception):
+        pa.ListEpsilon([3.5, 2.3, 1, 0.3])(4)
+    assert not np.isfinite(pa.NoEpsilon()(42))
+    assert np.isclose(pa.MedianEpsilon().alpha, 0.5)
+
+
+def test_batch_spec_support_rules():
+    prior = pa.Distribution(a=pa.RV("uniform", 0, 1))
+    model = pa.GaussianMeanModel()
+    ident = pa.smc.identity
+    base = dict(priors=[prior], transitions=[pa.MultivariateNormalTransition()],
+                distance=pa.PNormDistance(), eps=pa.MedianEpsilon(),
+                acceptor=pa.UniformAcceptor(), x_0={"data": 1.0},
+                nr_samples_per_parameter=1, summary_statistics=ident)
+    assert BatchSpec(1, "smc", [model], **base).unsupported_reason() is None
+    assert "BatchModel" in BatchSpec(1, "smc", [lambda p: p],
+                                     **base).unsupported_reason()
+    assert "several" in BatchSpec(1, "smc", [model, model],
+                                  **base).unsupported_reason()
+    b2 = dict(base, priors=[pa.Distribution(a=pa.RV("norm", 0, 1))])
+    assert "uniform" in BatchSpec(1, "smc", [model], **b2).unsupported_reason()
+    b3 = dict(base, transitions=[pa.LocalTransition()])
+    assert "Multivariate" in BatchSpec(1, "smc", [model],
+                                       **b3).unsupported_reason()
+
+
+def test_fast_random_choice():
+    np.random.seed(0)
+    c = [pa.smc.fast_random_choice([0.2, 0.5, 0.3]) for _ in range(20000)]
+    f = np.bincount(c, minlength=3) / len(c)
+    np.testing.assert_allclose(f, [0.2, 0.5, 0.3], atol=0.02)
+
+
+def test_quota_split():
+    from pyabc_amd.engine import GenerationEngine
+    for R in [1, 2, 3, 8]:
+        for n in [1, 7, 1000, 10 ** 6 + 3]:
+            q = []
+            for r in range(R):
+                e = GenerationEngine.__new__(GenerationEngine)
+                e.comm = Comm(r, R)
+                q.append(e.quota(n))
+            assert sum(q) == n and max(q) - min(q) <= 1
+
+
+def test_transition_weight_normalisation_and_empty():
+    tr = pa.MultivariateNormalTransition()
+    import pandas as pd
+    with pytest.raises(pa.NotEnoughParticles):
+        tr.fit(pd.DataFrame({"a": []}), np.array([]))
+    tr.fit(pd.DataFrame(index=[0, 1]), np.array([0.5, 0.5]))
+    assert tr.no_parameters and tr.pdf(pd.Series(dtype=float)) == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    comm = Comm.from_env("gloo")
+    # uneven per-rank row counts, as the per-rank quotas give
+    rows = torch.arange((rank + 2) * 3, dtype=torch.float64).view(-1, 3) \
+        + 100 * rank
+    g = comm.all_gather_rows(rows)
+    n = comm.all_reduce_int(rank + 1)
+    mx = comm.all_reduce_max_float(float(rank) * 1.5)
+    out[rank] = (g.numpy().tolist(), n, mx)
+    torch.distributed.destroy_process_group()
+
+
+def test_comm_gloo_world2():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_gloo_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    exp = np.concatenate([np.arange(6).reshape(-1, 3),
+                          np.arange(9).reshape(-1, 3) + 100])
+    for r in range(2):
+        np.testing.assert_array_equal(np.array(res[r][0]), exp)
+        assert res[r][1] == 3
+        assert res[r][2] == 1.5

@@ -261,7 +261,7 @@ def gen_local():
 GENS = {"kde": gen_kde, "resample": gen_resample, "distance": gen_distance,
         "quantile": gen_quantile, "local": gen_local}
 
-if __name__ == "__main__":
+def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*", default=None)
     args = ap.parse_args()
@@ -270,3 +270,90 @@ if __name__ == "__main__":
             continue
         print(f"[{name}]")
         fn()
+
+
+# --------------------------------------------------------------------------
+# end-to-end statistics (Monte-Carlo pins): reference runs over seeds
+# --------------------------------------------------------------------------
+def _run_stats(history, names):
+    out = []
+    for t in range(history.max_t + 1):
+        df, w = history.get_distribution(m=0, t=t)
+        X = df[names].values
+        w = w / w.sum()
+        mean = (X * w[:, None]).sum(0)
+        std = np.sqrt(((X - mean) ** 2 * w[:, None]).sum(0))
+        ess = 1.0 / np.sum(w ** 2)
+        out.append((mean, std, ess))
+    pops = history.get_all_populations()
+    eps = pops[pops.t >= 0].epsilon.values
+    nsim = pops[pops.t >= 0].samples.values
+    return out, eps, nsim
+
+
+def gen_e2e():
+    from pyabc.sampler import SingleCoreSampler
+    # C1: quickstart Gaussian mean (doc/examples/parameter_inference.ipynb)
+    res = {}
+    R, T = 5, 4
+    for r in range(R):
+        np.random.seed(100 + r)
+
+        def model(parameter):
+            return {"data": parameter["mean"] + 0.5 * np.random.randn()}
+        prior = pyabc.Distribution(mean=pyabc.RV("uniform", 0, 5))
+        abc = pyabc.ABCSMC(model, prior, PNormDistance(p=2),
+                           population_size=1000,
+                           eps=pyabc.MedianEpsilon(),
+                           sampler=SingleCoreSampler())
+        abc.new("sqlite://", {"data": 2.5})
+        h = abc.run(minimum_epsilon=0.1, max_nr_populations=T)
+        st, eps, nsim = _run_stats(h, ["mean"])
+        res[f"c1_mean_{r}"] = np.array([s[0] for s in st])
+        res[f"c1_std_{r}"] = np.array([s[1] for s in st])
+        res[f"c1_ess_{r}"] = np.array([s[2] for s in st])
+        res[f"c1_eps_{r}"] = eps
+        res[f"c1_nsim_{r}"] = nsim
+        print(f"    c1 seed {r}: eps {eps} mean {st[-1][0]}")
+    # C2 (reduced N): 4-param linear Gaussian, S=100, AdaptivePNorm(MAD)
+    d, S = 4, 100
+    A = np.random.RandomState(42).randn(S, d) / 2
+    th_true = np.array([0.5, -1.0, 1.5, 0.0])
+    x0v = A @ th_true + 0.5 * np.random.RandomState(7).randn(S)
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k}" for k in range(d)]
+    x0 = dict(zip(keys, x0v))
+    for r in range(3):
+        np.random.seed(200 + r)
+
+        def model2(par):
+            th = np.array([par[n] for n in names])
+            y = A @ th + 0.5 * np.random.randn(S)
+            return dict(zip(keys, y))
+        prior = pyabc.Distribution(**{n: pyabc.RV("uniform", -5, 10)
+                                      for n in names})
+        abc = pyabc.ABCSMC(
+            model2, prior,
+            AdaptivePNormDistance(p=2,
+                                  scale_function=median_absolute_deviation),
+            population_size=1000, eps=pyabc.QuantileEpsilon(alpha=0.5),
+            sampler=SingleCoreSampler())
+        abc.new("sqlite://", x0)
+        h = abc.run(max_nr_populations=4)
+        st, eps, nsim = _run_stats(h, names)
+        res[f"c2_mean_{r}"] = np.array([s[0] for s in st])
+        res[f"c2_std_{r}"] = np.array([s[1] for s in st])
+        res[f"c2_eps_{r}"] = eps
+        res[f"c2_nsim_{r}"] = nsim
+        print(f"    c2 seed {r}: eps {eps} mean {st[-1][0]}")
+    save("e2e_stats", A2=A, x0_2=x0v, theta_true_2=th_true, **res,
+         _ref=np.array("pyabc/smc.py:796-1022 (ABCSMC.run) with "
+                       "SingleCoreSampler; C1 doc/examples/"
+                       "parameter_inference.ipynb; C2 SURVEY 8(d)"))
+
+
+GENS["e2e"] = gen_e2e
+
+
+if __name__ == "__main__":
+    _main()

@@ -111,6 +111,7 @@ int abc_pnorm_distance_f64(const double* stats_T, int64_t ld, const double* x0,
   ABC_REQUIRE(B >= 0 && S >= 0 && ld >= B, "pnorm: bad sizes");
   ABC_REQUIRE(p >= 1.0, "pnorm: It must be p >= 1");
   if (B == 0) return kOk;
+  ABC_REQUIRE(stats_T && x0 && fw && d_out, "pnorm: null pointer");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
   if (std::isinf(p))
     hipLaunchKernelGGL(pnorm_kernel<3>, dim3(g), dim3(256), 0, st, stats_T, ld,
@@ -136,6 +137,7 @@ int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
   ABC_REQUIRE(d >= 1 && d <= 32 && S >= 1 && B >= 0 && ld >= B,
               "sim_linear_gaussian: bad sizes (d <= 32)");
   if (B == 0) return kOk;
+  ABC_REQUIRE(theta && A && out_T, "sim_linear_gaussian: null pointer");
   hipLaunchKernelGGL(sim_linear_gaussian_kernel, dim3(ceil_div(B, 256)),
                      dim3(256), 0, st, theta, B, d, A, c, S, sigma, seed, sid,
                      offset, out_T, ld);

@@ -324,6 +324,10 @@ int abc_resample_perturb_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE(check_dim(d), "resample_perturb: unsupported d=%d", d);
   ABC_REQUIRE(N > 0 && B >= 0, "resample_perturb: bad sizes");
   if (B == 0) return kOk;
+  ABC_REQUIRE(X && cdf && u && z && A && theta && idx && in_support,
+              "resample_perturb: null pointer");
+  ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
+              "resample_perturb: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
 #define L(DD)                                                                \
   hipLaunchKernelGGL((resample_perturb_kernel<DD>), dim3(g), dim3(256), 0, st, \
@@ -344,6 +348,10 @@ int abc_propose_philox_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE(check_dim(d), "propose: unsupported d=%d", d);
   ABC_REQUIRE(N > 0 && B >= 0, "propose: bad sizes");
   if (B == 0) return kOk;
+  ABC_REQUIRE(X && cdf && A && theta && idx && in_support,
+              "propose: null pointer");
+  ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
+              "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
 #define L(DD)                                                              \
   hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \

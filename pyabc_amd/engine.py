@@ -153,7 +153,7 @@ class GenerationEngine:
                                 rec_stats_T=stats, n_rec=nq)
 
     def sample_generation(self, t, n, fit, x0, fw, eps, keep_stats=None,
-                          record=None):
+                          record=None, stream_base=0):
         """Proposals until this rank's quota of n is accepted, then KDE
         weights.  ``fit=None`` proposes from the prior (generation 0,
         weight 1).  Returns the rank-local accepted rows; with ``record``
@@ -177,12 +177,12 @@ class GenerationEngine:
                           / max(self.valid_rate_est, 1e-3)))))
             if fit is None:
                 theta = K.prior_uniform(self.lo, self.scale, self.seed,
-                                        self._sid(t, 0), prop_off, B)
+                                        self._sid(t, stream_base), prop_off, B)
                 nv = B
             else:
                 theta_all, idx, sup = K.propose_philox(
                     fit.X, cdf, fit.A, self.lo, self.scale, self.seed,
-                    self._sid(t, 0), prop_off, B)
+                    self._sid(t, stream_base), prop_off, B)
                 vpos, vcount = K.compact(sup)
                 nv = int(vcount.item())                             # sync 1
                 self.valid_rate_est = max(nv / B, 1e-3)
@@ -190,12 +190,21 @@ class GenerationEngine:
             prop_off += B
             if nv == 0:
                 continue
-            stats = self.model.simulate(theta, self.seed, self._sid(t, 1),
-                                        sim_off)
+            stats = self.model.simulate(theta, self.seed,
+                                        self._sid(t, stream_base + 1), sim_off)
             sim_off += nv
-            d, acc, guard = K.pnorm_distance(stats, x0, fw, self.p, eps, B=nv)
-            apos, acount = K.compact(acc)
-            na = int(acount.item())                                 # sync 2
+            if x0 is None:
+                # calibration sample: everything accepted, distances later
+                # (smc.py:486-514: accepted_distances = [inf])
+                d = torch.full((nv,), math.inf, dtype=F64, device=self.dev)
+                guard = torch.zeros(nv, dtype=torch.uint8, device=self.dev)
+                apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
+                na = nv
+            else:
+                d, acc, guard = K.pnorm_distance(stats, x0, fw, self.p, eps,
+                                                 B=nv)
+                apos, acount = K.compact(acc)
+                na = int(acount.item())                             # sync 2
             self.acc_rate_est = max(na / nv, 1e-4)
             rounds.append((theta, stats, d, apos, na, nv, guard))
             n_acc += na

@@ -150,7 +150,8 @@ class GPUBatchSampler(Sampler):
         record = self.sample_factory.record_rejected
         if spec.kind == "calibration":
             res = eng.sample_generation(spec.t, n, None, None, None, np.inf,
-                                        keep_stats=True, record=False)
+                                        keep_stats=True, record=False,
+                                        stream_base=2)
             # calibration distances are computed later (smc.py:516-534)
             res.d = torch.full_like(res.w, np.inf)
         else:

@@ -18,47 +18,145 @@
 
 namespace abc {
 
-// one wave; lane 0 carries the dependent fp64 chain, the other lanes stage
-// the next 64*8 weights into LDS so that the chain never waits on memory.
-__global__ __launch_bounds__(64) void cdf_scan_kernel(const double* __restrict__ w,
-                                                      int64_t n,
-                                                      double* __restrict__ cdf) {
-  __shared__ double buf[2][512];
-  double acc = 0.0;
-  const int lane = threadIdx.x;
-  const int64_t nchunk = ceil_div(n, 512);
-  double pre[8];
+// ---------------------------------------------------------------------------
+// Exact sequential fp64 cumsum, evaluated in parallel.
+//
+// numpy's cumsum is the chain c_k = fl(c_{k-1} + w_k).  While c stays in one
+// binade [2^e, 2^(e+1)) every double there is an integer multiple of
+// u = 2^(e-52), so with C = c/u (an integer < 2^53) and v = w * 2^(52-e)
+// (exact scaling) the rounded sum is fl(c + w) = u * (C + floor(v) +
+// [frac(v) > 1/2]) -- except when frac(v) == 1/2 (a tie, resolved by the
+// parity of the result) or when the sum leaves the binade.  So a block turns
+// each 8192-element tile into INTEGER increments, prefix-sums them exactly
+// (int64), and writes every c_k up to the first element that ties or leaves
+// the binade; that element is evaluated with the real fp64 add, the grid is
+// re-derived from the new c, and the tile continues.  Breaks happen about
+// once per binade crossing (~60 for any N), so the result is bit-identical to
+// the sequential chain at tile-scan cost.
+constexpr int kScanThreads = 1024;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__global__ __launch_bounds__(kScanThreads) void cdf_scan_kernel(
+    const double* __restrict__ w, int64_t n, double* __restrict__ cdf) {
+  __shared__ long long wsum[kScanThreads / 64];
+  __shared__ int first_bad;
+  __shared__ double sh_c;
+  __shared__ int sh_s;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double c = 0.0;  // running value (uniform)
+  for (int64_t base = 0; base < n; base += kScanTile) {
+    double wv[kScanItems];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int64_t i = k * 64 + lane;
-    buf[0][k * 64 + lane] = i < n ? w[i] : 0.0;
-  }
-  __syncthreads();
-  for (int64_t c = 0; c < nchunk; ++c) {
-    const int cur = c & 1;
-    // issue the next chunk's loads into registers; they land while lane 0
-    // runs the dependent chain below
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t i = (c + 1) * 512 + k * 64 + lane;
-      pre[k] = i < n ? w[i] : 0.0;
+    for (int q = 0; q < kScanItems; ++q) {
+      const int64_t i = base + static_cast<int64_t>(tid) * kScanItems + q;
+      wv[q] = i < n ? w[i] : 0.0;
     }
-    if (lane == 0) {
-      const int64_t base = c * 512;
-      const int m = static_cast<int>(n - base < 512 ? n - base : 512);
-      for (int k = 0; k < m; ++k) {
-        acc += buf[cur][k];
-        buf[cur][k] = acc;
+    const int tile_n = static_cast<int>(n - base < kScanTile ? n - base : kScanTile);
+    int s = 0;  // first unprocessed element of the tile (uniform)
+    while (s < tile_n) {
+      // grid of the current binade
+      int ex;
+      const double mant = frexp(c, &ex);  // c = mant * 2^ex, mant in [0.5,1)
+      (void)mant;
+      const bool exact_mode = c >= 0x1p-1000;
+      const int e = ex - 1;
+      const long long C = exact_mode ? static_cast<long long>(ldexp(c, 52 - e)) : 0;
+      long long dl[kScanItems];
+      bool bad[kScanItems];
+      long long tsum = 0;
+#pragma unroll
+      for (int q = 0; q < kScanItems; ++q) {
+        const int k = tid * kScanItems + q;
+        long long dq = 0;
+        bool b = false;
+        if (k >= s && k < tile_n) {
+          if (!exact_mode || wv[q] < 0.0) {
+            b = (c != 0.0) || (wv[q] != 0.0);
+          } else {
+            const double v = ldexp(wv[q], 52 - e);
+            if (!(v < 0x1p62)) {
+              b = true;
+            } else {
+              const double fl = floor(v);
+              const double fr = v - fl;
+              dq = static_cast<long long>(fl) + (fr > 0.5 ? 1 : 0);
+              b = (fr == 0.5);
+            }
+          }
+        }
+        tsum += dq;
+        dl[q] = tsum;  // inclusive within the thread
+        bad[q] = b;
       }
-    }
-    __syncthreads();
+      // block exclusive scan of the thread totals
+      long long incl = tsum;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t i = c * 512 + k * 64 + lane;
-      if (i < n) cdf[i] = buf[cur][k * 64 + lane];
-      buf[cur ^ 1][k * 64 + lane] = pre[k];
+      for (int o = 1; o < 64; o <<= 1) {
+        const long long t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) wsum[wid] = incl;
+      if (tid == 0) first_bad = 1 << 30;
+      __syncthreads();
+      long long woff = 0;
+      for (int q = 0; q < wid; ++q) woff += wsum[q];
+      const long long excl = woff + incl - tsum;
+      // binade exit: C + prefix must stay below 2^53 (with one unit margin)
+      int my_bad = 1 << 30;
+#pragma unroll
+      for (int q = 0; q < kScanItems; ++q) {
+        const int k = tid * kScanItems + q;
+        if (k >= s && k < tile_n) {
+          const long long Ck = C + excl + dl[q];
+          if (bad[q] || (exact_mode && Ck + 1 >= (1ll << 53))) {
+            my_bad = k;
+            break;
+          }
+        }
+      }
+      if (my_bad < (1 << 30)) atomicMin(&first_bad, my_bad);
+      __syncthreads();
+      const int b = first_bad;
+      // write every element before the first break
+#pragma unroll
+      for (int q = 0; q < kScanItems; ++q) {
+        const int k = tid * kScanItems + q;
+        if (k >= s && k < tile_n && k < b) {
+          const long long Ck = C + excl + dl[q];
+          cdf[base + k] = ldexp(static_cast<double>(Ck), e - 52);
+        }
+      }
+      // the breaking element: the real fp64 add, by its owner
+      if (b < tile_n && b / kScanItems == tid) {
+        const int q0 = b - tid * kScanItems;
+        double prev = c;
+        double wb = 0.0;
+        long long dprev = 0;
+#pragma unroll
+        for (int q = 0; q < kScanItems; ++q) {
+          if (q == q0) wb = wv[q];
+          if (q == q0 - 1) dprev = dl[q];
+        }
+        if (b > s) prev = ldexp(static_cast<double>(C + excl + dprev), e - 52);
+        const double cb = (base + b == 0) ? wb : prev + wb;
+        cdf[base + b] = cb;
+        sh_c = cb;
+        sh_s = b + 1;
+      }
+      __syncthreads();
+      if (b < tile_n) {
+        c = sh_c;
+        s = sh_s;
+      } else {
+        // value at the end of the tile = C + total
+        long long total = 0;
+        for (int q = 0; q < kScanThreads / 64; ++q) total += wsum[q];
+        if (exact_mode) c = ldexp(static_cast<double>(C + total), e - 52);
+        s = tile_n;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -307,7 +405,8 @@ extern "C" {
 int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf,
                          hipStream_t st) {
   ABC_REQUIRE(n > 0 && w && cdf, "resample_cdf: need n > 0 and buffers");
-  hipLaunchKernelGGL(cdf_scan_kernel, dim3(1), dim3(64), 0, st, w, n, cdf);
+  hipLaunchKernelGGL(cdf_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, w,
+                     n, cdf);
   ABC_LAUNCH_CHECK("cdf_scan_kernel");
   hipLaunchKernelGGL(cdf_normalize_kernel, dim3(stream_grid(n, 256, 1024)),
                      dim3(256), 0, st, cdf, n);

@@ -281,3 +281,34 @@ def test_sim_linear_gaussian(K):
     z = ref.philox_normal(17, 4, (10 + B) * S)[10 * S:].reshape(B, S)
     expect = (th @ A.T + c + 0.5 * z).T
     np.testing.assert_allclose(out, expect, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "lognormal", "zeros", "ties",
+                                  "tiny", "steps"])
+def test_cdf_scan_bit_exact(K, kind):
+    """The parallel binade-grid scan equals numpy's sequential cumsum bit for
+    bit (then /= cdf[-1]) on adversarial weight vectors."""
+    rng = np.random.default_rng({"uniform": 1, "lognormal": 2, "zeros": 3,
+                                 "ties": 4, "tiny": 5, "steps": 6}[kind])
+    n = 1_000_003
+    if kind == "uniform":
+        w = rng.uniform(size=n)
+    elif kind == "lognormal":
+        w = np.exp(rng.normal(size=n) * 6)
+    elif kind == "zeros":
+        w = rng.uniform(size=n) * (rng.uniform(size=n) < 0.3)
+        w[:1000] = 0
+    elif kind == "ties":
+        # dyadic weights: many increments land exactly half-way on the grid
+        w = rng.integers(1, 1 << 12, size=n) * 2.0 ** -40
+    elif kind == "tiny":
+        w = rng.uniform(size=n) * 1e-300
+        w[n // 2:] *= 1e290
+    else:
+        w = np.repeat(rng.uniform(size=n // 1000 + 1) *
+                      10.0 ** rng.integers(-12, 3, size=n // 1000 + 1),
+                      1000)[:n]
+    w = w / w.sum()
+    ref_cdf = ref.resample_cdf(w)
+    got = host(K.resample_cdf(dev(w)))
+    np.testing.assert_array_equal(got, ref_cdf)

@@ -41,38 +41,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(fit, model, x0, eps, n_particles, seed=0):
-    """Reference-style per-particle CPU path, restated by the numpy oracle:
-    per proposal an O(N) CDF rebuild + searchsorted + perturbation (the
-    reference's np.random.choice, multivariatenormal.py:87-95), model,
-    p-norm distance; per accepted particle the O(N d) KDE density
-    (multivariatenormal.py:102-125).  One core."""
-    from oracle import ref_cpu as ref
-    X = fit.X.cpu().numpy()
-    w = fit.w.cpu().numpy()
-    cov = fit.cov
-    A = ref.svd_factor(cov)
-    x0h = x0.cpu().numpy()
-    fw = np.ones_like(x0h)
-    rng = np.random.default_rng(seed)
-    d = X.shape[1]
-    lo, sc = np.full(d, -5.0), np.full(d, 10.0)
-    acc = evals = 0
-    t0 = time.perf_counter()
-    while acc < n_particles:
-        cdf = ref.resample_cdf(w)                    # O(N) per proposal
-        idx = ref.resample_indices(cdf, rng.random())
-        th = X[idx] + rng.standard_normal(d) @ A
-        if not ref.uniform_box_support(th[None], lo, sc)[0]:
-            continue
-        y = model.simulate_host(th, rng)
-        dist = ref.pnorm_distance(y, x0h, fw, 2)[0]
-        evals += 1
-        if dist <= eps:
-            acc += 1
-            ref.kde_transition_pd(th[None], X, w, cov)   # O(N d)
-    t = time.perf_counter() - t0
-    return acc / t, t, evals
+def cpu_baseline(fit, model, x0, eps, seconds):
+    """The reference's per-particle CPU path (restated by the oracle) on the
+    host cores, MulticoreEvalParallelSampler-style (oracle/cpu_baseline.py),
+    over the same previous population, model and epsilon."""
+    from oracle import cpu_baseline as cb
+    d = fit.X.shape[1]
+    return cb.run(fit.X.cpu().numpy(), fit.w.cpu().numpy(), fit.cov,
+                  model.A_host, x0.cpu().numpy(), np.full(d, -5.0),
+                  np.full(d, 10.0), eps, model.sigma, 2.0, seconds=seconds)
+
+
+def kde_traffic():
+    """HBM bytes per launch of the KDE kernel from the committed rocprofv3
+    PMC passes (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE;
+    tools/pmc_traffic.py writes the file)."""
+    path = os.path.join(ROOT, "profiles", "kde_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get("hbm_bytes_per_launch"), t.get("source")
 
 
 def main():
@@ -84,7 +73,7 @@ def main():
     ap.add_argument("--d", type=int, default=8)
     ap.add_argument("--S", type=int, default=100)
     ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--cpu-particles", type=int, default=48)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -146,6 +135,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = N * args.steps / elapsed
     flops_per_pair = 3 * d + 4
+    traffic, traffic_src = kde_traffic()
     # per-launch roofline of the dominant kernel on this rank
     avg_launch_s = kde_t / max(len(kde_ms), 1)
     pairs_per_launch = pairs_local / max(len(kde_ms), 1)
@@ -182,29 +172,33 @@ def main():
         "kde_pairs_per_s": pairs_total / kde_t_max,
         "roofline": {
             "bound": "valu",
-            "kernel": "kde_main_kernel (fp32 VALU: d sub + d fma + "
-                      "v_exp_f32 + add per pair)",
+            "kernel": "kde_main_pk_kernel (fp32 VALU: d sub + d fma + "
+                      "v_exp_f32 + add per pair, packed v_pk_add/v_pk_fma)",
             "achieved": achieved_tf,
             "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tf / FP32_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "flops_per_pair": flops_per_pair,
             "avg_launch_ms": avg_launch_s * 1e3,
             "pairs_per_launch": pairs_per_launch,
         },
     }
     if R == 1 and not args.no_cpu_baseline:
-        v, t_cpu, ev = cpu_baseline(state["fit"], model, x0, state["eps"],
-                                    args.cpu_particles)
+        v, cores, acc, ev, wall = cpu_baseline(state["fit"], model, x0,
+                                               state["eps"], args.cpu_seconds)
         out["cpu_baseline"] = {
-            "value": v, "unit": "accepted particles/s", "cores": 1,
+            "value": v, "unit": "accepted particles/s", "cores": cores,
             "kind": "port",
-            "sample": f"{args.cpu_particles} accepted particles ({ev} "
-                      f"evaluations, {t_cpu:.1f} s) of the same generation "
-                      f"at N_prev={N}, d={d}: reference per-particle "
-                      f"algorithm restated by the numpy oracle (O(N) CDF "
-                      f"per proposal, O(N d) KDE per acceptance)"}
+            "sample": f"{acc} accepted particles ({ev} evaluations) in "
+                      f"{args.cpu_seconds:.0f} s on each of {cores} spawned "
+                      f"workers (1 BLAS thread each), same generation "
+                      f"(N_prev={N}, d={d}, S={S}, same eps): the "
+                      f"reference's per-particle algorithm "
+                      f"(MulticoreEvalParallelSampler layout; O(N) CDF per "
+                      f"proposal, O(N d) KDE per acceptance) restated by "
+                      f"the numpy oracle"}
     print(json.dumps(out), flush=True)
 
 

@@ -16,7 +16,12 @@
 // new rows y_i in VGPRs; the block's j-range streams through the SCALAR path
 // (wave-uniform s_load of P rows, SGPR operands of v_sub/v_fma), so there is
 // no LDS traffic and no barrier in the inner loop.  Per pair: D subs, D FMAs
-// (the first seeded with lw2_j), one v_exp_f32, one add.  fp32 sums are
+// (the first seeded with lw2_j), one v_exp_f32, one add.  The fp32 kernel
+// holds its rows in PAIRS (float2) so the subs and FMAs issue as
+// v_pk_add_f32 / v_pk_fma_f32 with the SGPR operand broadcast to both halves:
+// one wave-instruction does two pairs' work, which keeps a single wave at the
+// SIMD's issue rate (measured +25 % over scalar v_sub/v_fma at d = 8, same
+// bits: each lane still evaluates the identical fp32 expression).  fp32 sums are
 // flushed into fp64 every CH pairs.  The j-range is split over SPLIT blocks
 // (split index = block % SPLIT, so with SPLIT % 8 == 0 every XCD streams its
 // own j-ranges through its own L2), and per-split fp64 partials are summed in
@@ -178,6 +183,82 @@ __global__ __launch_bounds__(256) void kde_main_kernel(
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// fp32 main pass, rows held in pairs: lane t of block rb owns rows
+// rb*256*2*R2 + (2r+h)*256 + t (h = half of the float2), the same row map as
+// kde_main_kernel with R = 2*R2.
+template <int D, int R2, int U, int CH>
+__global__ __launch_bounds__(256) void kde_main_pk_kernel(
+    const float* __restrict__ Ynew, int64_t M, const float* __restrict__ P,
+    int64_t npad, int split, int64_t jchunk, double* __restrict__ partial) {
+  constexpr int R = 2 * R2;
+  constexpr int W = U * (D + 1);
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t rows_per_block = 256 * R;
+  const int64_t j0 = static_cast<int64_t>(s) * jchunk;
+  int64_t j1 = j0 + jchunk;
+  if (j1 > npad) j1 = npad;
+
+  f32x2 yi[R2][D];
+#pragma unroll
+  for (int r = 0; r < R2; ++r) {
+    int64_t ra = rb * rows_per_block + (2 * r) * 256 + threadIdx.x;
+    int64_t rc = ra + 256;
+    if (ra >= M) ra = M - 1;
+    if (rc >= M) rc = M - 1;
+#pragma unroll
+    for (int k = 0; k < D; ++k) yi[r][k] = f32x2{Ynew[ra * D + k], Ynew[rc * D + k]};
+  }
+  double S[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) S[r] = 0.0;
+
+  // int32 trip counts keep the loop control on the scalar unit
+  const int nj = static_cast<int>(j1 - j0);
+  const float* __restrict__ base = P + j0 * (D + 1);
+  for (int jc = 0; jc < nj; jc += CH) {
+    const int je = min(jc + CH, nj);
+    f32x2 sacc[R2];
+#pragma unroll
+    for (int r = 0; r < R2; ++r) sacc[r] = f32x2{0.f, 0.f};
+    for (int j = jc; j < je; j += U) {
+      const float* __restrict__ pj = base + static_cast<int64_t>(j) * (D + 1);
+      float cu[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) cu[q] = pj[q];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float lw = cu[u * (D + 1) + D];
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+          f32x2 acc = f32x2{lw, lw};
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const float pk = cu[u * (D + 1) + k];
+            const f32x2 df = yi[r][k] - f32x2{pk, pk};
+            acc = __builtin_elementwise_fma(-df, df, acc);
+          }
+          sacc[r] += f32x2{fast_exp2(acc.x), fast_exp2(acc.y)};
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R2; ++r) {
+      S[2 * r] += static_cast<double>(sacc[r].x);
+      S[2 * r + 1] += static_cast<double>(sacc[r].y);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R2; ++r) {
+    const int64_t ra = rb * rows_per_block + (2 * r) * 256 + threadIdx.x;
+    const int64_t rc = ra + 256;
+    if (ra < M) partial[static_cast<int64_t>(s) * M + ra] = S[2 * r];
+    if (rc < M) partial[static_cast<int64_t>(s) * M + rc] = S[2 * r + 1];
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void kde_finalize_kernel(
     const double* __restrict__ partial, int64_t M, int split,
@@ -262,9 +343,19 @@ static int padded_dim(int d) {
 constexpr int kRowPad = 64;  // Npad multiple (>= U, == CH)
 constexpr int kCH = 64;
 
+// rows per thread; fp32: R = 2*R2 rows in float2 pairs, R2 and the j-unroll
+// U picked per D from the tools/probes/kde_variants.hip sweep on MI355X
+template <typename T, int D>
+struct RowsPerThread;
 template <int D>
-struct RowsPerThread {
+struct RowsPerThread<double, D> {
   static constexpr int value = D <= 8 ? 4 : 2;
+};
+template <int D>
+struct RowsPerThread<float, D> {
+  static constexpr int pairs = D <= 8 ? 4 : 2;
+  static constexpr int unroll = D <= 8 ? 1 : 2;
+  static constexpr int value = 2 * pairs;
 };
 
 struct Plan {
@@ -273,9 +364,9 @@ struct Plan {
   int64_t row_blocks;
 };
 
-template <int D>
+template <typename T, int D>
 static Plan make_plan(int64_t M, int64_t npad) {
-  constexpr int R = RowsPerThread<D>::value;
+  constexpr int R = RowsPerThread<T, D>::value;
   Plan p;
   p.row_blocks = ceil_div(M, 256 * R);
   const int64_t target_blocks = 8192;  // ~4 waves of 2048 resident blocks
@@ -297,7 +388,7 @@ static size_t ws_bytes_impl(int64_t M, int64_t npad, int d) {
   int64_t split;
   switch (D) {
 #define CASE(DD) \
-  case DD: split = make_plan<DD>(M, npad).split; break;
+  case DD: split = make_plan<T, DD>(M, npad).split; break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
 #undef CASE
@@ -311,8 +402,7 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
                        const double* lw2max, double log_const,
                        double* out_logpd, void* ws, size_t ws_bytes,
                        hipStream_t stream) {
-  constexpr int R = RowsPerThread<D>::value;
-  const Plan p = make_plan<D>(M, npad);
+  const Plan p = make_plan<T, D>(M, npad);
   const size_t need = static_cast<size_t>(p.split * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
   ABC_REQUIRE(ws_bytes >= need, "kde: workspace too small (%zu < %zu)",
@@ -323,9 +413,18 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
   int* fix_rows = n_fix + 4;
   ABC_HIP(hipMemsetAsync(n_fix, 0, 16, stream));
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
-  hipLaunchKernelGGL((kde_main_kernel<T, D, R, 2, kCH>), dim3(grid), dim3(256),
-                     0, stream, Ynew, M, P, npad, p.split, p.jchunk, partial);
-  ABC_LAUNCH_CHECK("kde_main_kernel");
+  if constexpr (sizeof(T) == 4) {
+    using RP = RowsPerThread<float, D>;
+    hipLaunchKernelGGL((kde_main_pk_kernel<D, RP::pairs, RP::unroll, kCH>),
+                       dim3(grid), dim3(256), 0, stream, Ynew, M, P, npad,
+                       p.split, p.jchunk, partial);
+    ABC_LAUNCH_CHECK("kde_main_pk_kernel");
+  } else {
+    constexpr int R = RowsPerThread<T, D>::value;
+    hipLaunchKernelGGL((kde_main_kernel<T, D, R, 2, kCH>), dim3(grid), dim3(256),
+                       0, stream, Ynew, M, P, npad, p.split, p.jchunk, partial);
+    ABC_LAUNCH_CHECK("kde_main_kernel");
+  }
   hipLaunchKernelGGL((kde_finalize_kernel<T>), dim3(ceil_div(M, 256)),
                      dim3(256), 0, stream, partial, M, p.split, lw2max,
                      log_const, out_logpd, n_fix, fix_rows);
@@ -425,13 +524,16 @@ int abc_kde_padded_dim(int d) { return padded_dim(d); }
 int abc_kde_row_pad(void) { return kRowPad; }
 
 size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d) {
-  return ws_bytes_impl<float>(M, npad, d);
+  // one size for both precisions (their plans may split differently)
+  const size_t a = ws_bytes_impl<float>(M, npad, d);
+  const size_t b = ws_bytes_impl<double>(M, npad, d);
+  return a > b ? a : b;
 }
 
 int abc_kde_split(int64_t M, int64_t npad, int d) {
   switch (padded_dim(d)) {
 #define CASE(DD) \
-  case DD: return make_plan<DD>(M, npad).split;
+  case DD: return make_plan<float, DD>(M, npad).split;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
 #undef CASE

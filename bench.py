@@ -69,19 +69,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--d", type=int, default=8)
-    ap.add_argument("--S", type=int, default=100)
+    ap.add_argument("--particles", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=8)
+    ap.add_argument("--n-stats", type=int, default=100)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="multi-rank rehearsal on a one-GPU box: every rank "
+                         "on cuda:0, gloo collectives staged through host")
     args = ap.parse_args()
 
-    comm = Comm.from_env("nccl")
+    if args.rehearse_gloo:
+        comm = Comm.from_env("gloo", device=0)
+    else:
+        comm = Comm.from_env("nccl")
     if comm.world == 1:
         torch.cuda.set_device(0)
     R = comm.world
-    N, d, S = args.n, args.d, args.S
+    N, d, S = args.particles, args.dim, args.n_stats
     model = LinearGaussianModel.benchmark(d, S)
     x0 = torch.as_tensor(model._x0, device="cuda")
     fw = torch.ones(S, dtype=torch.float64, device="cuda")

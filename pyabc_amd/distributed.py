@@ -25,18 +25,28 @@ class Comm:
         return Comm(0, 1, None)
 
     @staticmethod
-    def from_env(backend=None):
-        """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK."""
+    def from_env(backend=None, device=None):
+        """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK.
+
+        ``device`` overrides the GPU of this rank (default LOCAL_RANK); a
+        rehearsal of the multi-rank path on a one-GPU box puts every rank on
+        device 0 with the "gloo" backend."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if world == 1:
             return Comm.single()
         if not dist.is_initialized():
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
-            if backend == "nccl":
-                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            if backend == "nccl" or device is not None:
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0"))
+                                      if device is None else device)
             dist.init_process_group(backend=backend)
         return Comm(dist.get_rank(), dist.get_world_size(), None)
+
+    @property
+    def _host_staged(self):
+        # gloo's all_gather takes host tensors only
+        return dist.get_backend() == "gloo"
 
     @property
     def active(self):
@@ -51,6 +61,8 @@ class Comm:
         order."""
         if not self.active:
             return t
+        if self._host_staged and t.is_cuda:
+            return self.all_gather_rows(t.cpu()).to(t.device)
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(sizes, n)

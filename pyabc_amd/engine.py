@@ -98,6 +98,11 @@ class DeviceMVNFit:
     def logpdf(self, theta):
         return self.packed.logpdf(theta)
 
+    def propose(self, lo, scale, seed, sid, offset, B):
+        """B draws of resample + perturb + support flag (Philox)."""
+        return K.propose_philox(self.X, self.cdf, self.A, lo, scale, seed,
+                                sid, offset, B)
+
 
 class GenerationResult:
     def __init__(self, **kw):
@@ -164,7 +169,6 @@ class GenerationEngine:
         nq = self.quota(n)
         tm = {}
         t0 = time.perf_counter()
-        cdf = fit.cdf if fit is not None else None
         rounds = []
         n_acc = 0
         prop_off = 0
@@ -180,8 +184,8 @@ class GenerationEngine:
                                         self._sid(t, stream_base), prop_off, B)
                 nv = B
             else:
-                theta_all, idx, sup = K.propose_philox(
-                    fit.X, cdf, fit.A, self.lo, self.scale, self.seed,
+                theta_all, idx, sup = fit.propose(
+                    self.lo, self.scale, self.seed,
                     self._sid(t, stream_base), prop_off, B)
                 vpos, vcount = K.compact(sup)
                 nv = int(vcount.item())                             # sync 1
@@ -247,7 +251,7 @@ class GenerationEngine:
             logpd = None
             w = torch.ones(theta_acc.shape[0], dtype=F64, device=self.dev)
         else:
-            if self.kde_events is not None:
+            if self.kde_events is not None and hasattr(fit, "packed"):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 Y = fit.packed.whiten(theta_acc)

@@ -44,7 +44,7 @@ class BatchSpec:
 
     def unsupported_reason(self):
         from ..acceptor import UniformAcceptor
-        from ..transition import MultivariateNormalTransition
+        from ..transition import MultivariateNormalTransition, LocalTransition
         if len(self.models) != 1:
             return "model selection (several models)"
         if not isinstance(self.models[0], BatchModel):
@@ -62,8 +62,9 @@ class BatchSpec:
                     self.acceptor.use_complete_history:
                 return "acceptor is not UniformAcceptor(current time)"
             if self.t > 0 and not isinstance(
-                    self.transitions[0], MultivariateNormalTransition):
-                return "transition is not MultivariateNormalTransition"
+                    self.transitions[0],
+                    (MultivariateNormalTransition, LocalTransition)):
+                return "transition is not MultivariateNormal/LocalTransition"
         return None
 
 

@@ -265,6 +265,13 @@ class LocalTransition(Transition):
         self._covs, self._invs, self._dets = covs, invs, dets
         self._cdf = K.resample_cdf(self._wd)
 
+    # device-level API used by the batch sampler (engine.GenerationEngine)
+    @property
+    def device_fit(self):
+        if getattr(self, "_covs", None) is None:
+            return None
+        return _LocalDeviceFit(self)
+
     @property
     def covs(self):
         return self._covs.cpu().numpy()
@@ -312,3 +319,24 @@ class LocalTransition(Transition):
         theta, _, _ = K.propose_local(self._Xd, self._cdf, self._covs,
                                       _draw_seed(), 0, 0, size)
         return _as_output(theta.cpu().numpy(), single, _columns(self.X))
+
+
+class _LocalDeviceFit:
+    """LocalTransition state as the generation engine consumes it:
+    ``propose`` = rvs_single for a whole batch (choice by the weight CDF,
+    then N(X_idx, C_idx), local_transition.py:141-145) with the prior-support
+    flag, ``logpdf`` = the density pass (local_transition.py:103-110)."""
+
+    def __init__(self, tr):
+        self.X = tr._Xd
+        self.w = tr._wd
+        self.n = self.X.shape[0]
+        self.cdf = tr._cdf
+        self._covs, self._invs, self._dets = tr._covs, tr._invs, tr._dets
+
+    def propose(self, lo, scale, seed, sid, offset, B):
+        return K.propose_local(self.X, self.cdf, self._covs, seed, sid,
+                               offset, B, lo, scale)
+
+    def logpdf(self, theta):
+        return K.local_logpdf(theta, self.X, self.w, self._invs, self._dets)

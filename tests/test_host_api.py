@@ -103,8 +103,20 @@ def test_batch_spec_support_rules():
     b2 = dict(base, priors=[pa.Distribution(a=pa.RV("norm", 0, 1))])
     assert "uniform" in BatchSpec(1, "smc", [model], **b2).unsupported_reason()
     b3 = dict(base, transitions=[pa.LocalTransition()])
+    assert BatchSpec(1, "smc", [model], **b3).unsupported_reason() is None
+
+    class UserTransition(pa.Transition):
+        def fit(self, X, w):
+            pass
+
+        def rvs_single(self):
+            return None
+
+        def pdf(self, x):
+            return 1.0
+    b4 = dict(base, transitions=[UserTransition()])
     assert "Multivariate" in BatchSpec(1, "smc", [model],
-                                       **b3).unsupported_reason()
+                                       **b4).unsupported_reason()
 
 
 def test_fast_random_choice():

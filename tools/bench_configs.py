@@ -1,0 +1,121 @@
+"""End-to-end runs of BASELINE.json's configs through the drop-in API
+(pyabc_amd.ABCSMC + GPUBatchSampler) on one MI355X.
+
+    python tools/bench_configs.py [--only c1 c2 c4 c5] > gpurun_out/configs.jsonl
+
+One JSON line per config: per-generation sampling wall time (the metric's
+"accepted particles/s per generation" = N / sample_until_n_accepted wall,
+generations t >= 1), acceptance, epsilon trajectory, total wall time and
+the posterior mean.  Config 3 (the KDE pass at N = 1e6, d = 8) is bench.py.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import pyabc_amd as pa  # noqa: E402
+
+
+def linear_problem(d, S, A_scale):
+    A = np.random.RandomState(42).randn(S, d) / A_scale
+    theta_true = np.linspace(-1, 1, d) if d != 4 else np.array(
+        [0.5, -1.0, 1.5, 0.0])
+    x0 = A @ theta_true + 0.5 * np.random.RandomState(7).randn(S)
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k:02d}" for k in range(d)]
+    return A, theta_true, x0, keys, names
+
+
+def run(name, abc, x0, names, theta_true=None, **run_kw):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    abc.new(f"mem://{name}", x0)
+    h = abc.run(**run_kw)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    log = abc.generation_log
+    N = abc.population_size(0) if callable(getattr(abc, "population_size",
+                                                   None)) else None
+    df, w = h.distribution_numpy(0, h.max_t)
+    w = w / w.sum()
+    mean = (df[names].values * w[:, None]).sum(0)
+    gens = [dict(t=e["t"], eps=float(e["eps"]), n_sim=int(e["n_sim"]),
+                 sample_s=float(e["sample_seconds"]), batch=e["batch"])
+            for e in log]
+    n_pop = int(len(w))
+    rates = [n_pop / g["sample_s"] for g in gens if g["t"] >= 1]
+    out = dict(config=name, N=n_pop, generations=len(gens), wall_s=wall,
+               accepted_per_s_median_t_ge_1=float(np.median(rates))
+               if rates else None,
+               all_batch=all(g["batch"] for g in gens), gens=gens,
+               posterior_mean=mean.tolist())
+    if theta_true is not None:
+        out["theta_true"] = list(map(float, theta_true))
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def c1():
+    np.random.seed(0)
+    prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
+    abc = pa.ABCSMC(pa.GaussianMeanModel(), prior, pa.PNormDistance(p=2),
+                    population_size=1000, eps=pa.MedianEpsilon(),
+                    sampler=pa.GPUBatchSampler(seed=1))
+    run("c1_quickstart_N1000", abc, {"data": 2.5}, ["mean"], [2.5],
+        minimum_epsilon=0.1, max_nr_populations=10)
+
+
+def c2(N=100_000, gens=6):
+    A, th, x0, keys, names = linear_problem(4, 100, 2.0)
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.AdaptivePNormDistance(
+        p=2, scale_function=pa.median_absolute_deviation),
+        population_size=N, eps=pa.QuantileEpsilon(alpha=0.5),
+        sampler=pa.GPUBatchSampler(seed=2))
+    run("c2_adaptive_mad_N1e5_d4_S100", abc, dict(zip(keys, x0)), names, th,
+        max_nr_populations=gens)
+
+
+def c4(N=200_000, gens=4):
+    A, th, x0, keys, names = linear_problem(6, 100, np.sqrt(6))
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2),
+                    population_size=N,
+                    transitions=pa.LocalTransition(k=50, k_fraction=None),
+                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.GPUBatchSampler(seed=4))
+    run("c4_local_k50_N2e5_d6", abc, dict(zip(keys, x0)), names, th,
+        max_nr_populations=gens)
+
+
+def c5(N=1_000_000, gens=10):
+    A, th, x0, keys, names = linear_problem(20, 100, np.sqrt(20))
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2),
+                    population_size=N, eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.GPUBatchSampler(seed=5))
+    run("c5_10gen_N1e6_d20_S100", abc, dict(zip(keys, x0)), names, th,
+        max_nr_populations=gens)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=["c1", "c2", "c4", "c5"])
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    for c in args.only:
+        globals()[c]()
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,10 @@ int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
  * out_logpd[i] = log pdf(theta_i) when log_const = -(rank ln 2pi + log_pdet)/2. */
 int abc_kde_padded_dim(int d);
 int abc_kde_row_pad(void);
+/* Number of fixed j-segments of the KDE pass (a function of npad only:
+   every row is the fixed-order sum of its segment partials, so results do
+   not depend on M or on the number of ranks sharing the rows). */
+int abc_kde_segments(int64_t npad);
 int abc_kde_split(int64_t M, int64_t npad, int d);
 size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d);
 int abc_whiten_f32(const double* X, int64_t n, int d, const double* mu,

@@ -58,6 +58,7 @@ _SIGS = {
     # (a3)
     "abc_kde_padded_dim": (c_int, [c_int]),
     "abc_kde_row_pad": (c_int, []),
+    "abc_kde_segments": (c_int, [c_i64]),
     "abc_kde_split": (c_int, [c_i64, c_i64, c_int]),
     "abc_kde_workspace_bytes": (c_size, [c_i64, c_i64, c_int]),
     "abc_whiten_f32": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr, c_ptr,

@@ -22,10 +22,13 @@
 // one wave-instruction does two pairs' work, which keeps a single wave at the
 // SIMD's issue rate (measured +25 % over scalar v_sub/v_fma at d = 8, same
 // bits: each lane still evaluates the identical fp32 expression).  fp32 sums are
-// flushed into fp64 every CH pairs.  The j-range is split over SPLIT blocks
-// (split index = block % SPLIT, so with SPLIT % 8 == 0 every XCD streams its
-// own j-ranges through its own L2), and per-split fp64 partials are summed in
-// fixed order by the finalize kernel (deterministic).  Rows whose sum falls
+// flushed into fp64 every CH pairs.  The j-range is cut into nseg fixed
+// segments (a function of npad only); SPLIT blocks per row block each take
+// nseg/SPLIT consecutive segments (split index = block % SPLIT, so with
+// SPLIT % 8 == 0 every XCD streams its own j-ranges through its own L2) and
+// write one fp64 partial per segment; the finalize kernel sums the nseg
+// partials in fixed order.  A row's result is therefore independent of M
+// and of the launch shape (deterministic, and identical across GPU counts).  Rows whose sum falls
 // below 2^-60 (f32) are re-evaluated by an exact two-pass (max, then sum)
 // fixup kernel, so underflow of the fixed global offset never loses a row.
 #include "common.hpp"
@@ -130,13 +133,10 @@ __global__ __launch_bounds__(256) void pack_prev_kernel(
 template <typename T, int D, int R, int U, int CH>
 __global__ __launch_bounds__(256) void kde_main_kernel(
     const T* __restrict__ Ynew, int64_t M, const T* __restrict__ P,
-    int64_t npad, int split, int64_t jchunk, double* __restrict__ partial) {
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   const int s = blockIdx.x % split;
   const int64_t rb = blockIdx.x / split;
   const int64_t rows_per_block = 256 * R;
-  const int64_t j0 = static_cast<int64_t>(s) * jchunk;
-  int64_t j1 = j0 + jchunk;
-  if (j1 > npad) j1 = npad;
 
   T yi[R][D];
 #pragma unroll
@@ -146,40 +146,45 @@ __global__ __launch_bounds__(256) void kde_main_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) yi[r][k] = Ynew[row * D + k];
   }
-  double S[R];
+  for (int g = 0; g < spb; ++g) {
+    const int seg = s * spb + g;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    int64_t j1 = j0 + jseg;
+    if (j1 > npad) j1 = npad;
+    double S[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) S[r] = 0.0;
-
-  for (int64_t jc = j0; jc < j1; jc += CH) {
-    int64_t je = jc + CH;
-    if (je > j1) je = j1;
-    T sacc[R];
+    for (int r = 0; r < R; ++r) S[r] = 0.0;
+    for (int64_t jc = j0; jc < j1; jc += CH) {
+      int64_t je = jc + CH;
+      if (je > j1) je = j1;
+      T sacc[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) sacc[r] = T(0);
-    for (int64_t j = jc; j < je; j += U) {
-      const T* __restrict__ pj = P + j * (D + 1);
+      for (int r = 0; r < R; ++r) sacc[r] = T(0);
+      for (int64_t j = jc; j < je; j += U) {
+        const T* __restrict__ pj = P + j * (D + 1);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const T lw = pj[u * (D + 1) + D];
+        for (int u = 0; u < U; ++u) {
+          const T lw = pj[u * (D + 1) + D];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          T acc = lw;
+          for (int r = 0; r < R; ++r) {
+            T acc = lw;
 #pragma unroll
-          for (int k = 0; k < D; ++k) {
-            const T df = yi[r][k] - pj[u * (D + 1) + k];
-            acc = fma(-df, df, acc);
+            for (int k = 0; k < D; ++k) {
+              const T df = yi[r][k] - pj[u * (D + 1) + k];
+              acc = fma(-df, df, acc);
+            }
+            sacc[r] += fast_exp2(acc);
           }
-          sacc[r] += fast_exp2(acc);
         }
       }
+#pragma unroll
+      for (int r = 0; r < R; ++r) S[r] += static_cast<double>(sacc[r]);
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) S[r] += static_cast<double>(sacc[r]);
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t row = rb * rows_per_block + r * 256 + threadIdx.x;
-    if (row < M) partial[static_cast<int64_t>(s) * M + row] = S[r];
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = rb * rows_per_block + r * 256 + threadIdx.x;
+      if (row < M) partial[static_cast<int64_t>(seg) * M + row] = S[r];
+    }
   }
 }
 
@@ -187,19 +192,17 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // fp32 main pass, rows held in pairs: lane t of block rb owns rows
 // rb*256*2*R2 + (2r+h)*256 + t (h = half of the float2), the same row map as
-// kde_main_kernel with R = 2*R2.
+// kde_main_kernel with R = 2*R2.  Block (rb, s) covers the spb consecutive
+// j-segments s*spb .. s*spb+spb-1 and writes one fp64 partial per segment.
 template <int D, int R2, int U, int CH>
 __global__ __launch_bounds__(256) void kde_main_pk_kernel(
     const float* __restrict__ Ynew, int64_t M, const float* __restrict__ P,
-    int64_t npad, int split, int64_t jchunk, double* __restrict__ partial) {
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int R = 2 * R2;
   constexpr int W = U * (D + 1);
   const int s = blockIdx.x % split;
   const int64_t rb = blockIdx.x / split;
   const int64_t rows_per_block = 256 * R;
-  const int64_t j0 = static_cast<int64_t>(s) * jchunk;
-  int64_t j1 = j0 + jchunk;
-  if (j1 > npad) j1 = npad;
 
   f32x2 yi[R2][D];
 #pragma unroll
@@ -211,64 +214,68 @@ __global__ __launch_bounds__(256) void kde_main_pk_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) yi[r][k] = f32x2{Ynew[ra * D + k], Ynew[rc * D + k]};
   }
-  double S[R];
+  for (int g = 0; g < spb; ++g) {
+    const int seg = s * spb + g;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    // int32 trip counts keep the loop control on the scalar unit
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const float* __restrict__ base = P + j0 * (D + 1);
+    double S[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) S[r] = 0.0;
-
-  // int32 trip counts keep the loop control on the scalar unit
-  const int nj = static_cast<int>(j1 - j0);
-  const float* __restrict__ base = P + j0 * (D + 1);
-  for (int jc = 0; jc < nj; jc += CH) {
-    const int je = min(jc + CH, nj);
-    f32x2 sacc[R2];
+    for (int r = 0; r < R; ++r) S[r] = 0.0;
+    for (int jc = 0; jc < nj; jc += CH) {
+      const int je = min(jc + CH, nj);
+      f32x2 sacc[R2];
 #pragma unroll
-    for (int r = 0; r < R2; ++r) sacc[r] = f32x2{0.f, 0.f};
-    for (int j = jc; j < je; j += U) {
-      const float* __restrict__ pj = base + static_cast<int64_t>(j) * (D + 1);
-      float cu[W];
+      for (int r = 0; r < R2; ++r) sacc[r] = f32x2{0.f, 0.f};
+      for (int j = jc; j < je; j += U) {
+        const float* __restrict__ pj = base + static_cast<int64_t>(j) * (D + 1);
+        float cu[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) cu[q] = pj[q];
+        for (int q = 0; q < W; ++q) cu[q] = pj[q];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float lw = cu[u * (D + 1) + D];
+        for (int u = 0; u < U; ++u) {
+          const float lw = cu[u * (D + 1) + D];
 #pragma unroll
-        for (int r = 0; r < R2; ++r) {
-          f32x2 acc = f32x2{lw, lw};
+          for (int r = 0; r < R2; ++r) {
+            f32x2 acc = f32x2{lw, lw};
 #pragma unroll
-          for (int k = 0; k < D; ++k) {
-            const float pk = cu[u * (D + 1) + k];
-            const f32x2 df = yi[r][k] - f32x2{pk, pk};
-            acc = __builtin_elementwise_fma(-df, df, acc);
+            for (int k = 0; k < D; ++k) {
+              const float pk = cu[u * (D + 1) + k];
+              const f32x2 df = yi[r][k] - f32x2{pk, pk};
+              acc = __builtin_elementwise_fma(-df, df, acc);
+            }
+            sacc[r] += f32x2{fast_exp2(acc.x), fast_exp2(acc.y)};
           }
-          sacc[r] += f32x2{fast_exp2(acc.x), fast_exp2(acc.y)};
         }
+      }
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        S[2 * r] += static_cast<double>(sacc[r].x);
+        S[2 * r + 1] += static_cast<double>(sacc[r].y);
       }
     }
 #pragma unroll
     for (int r = 0; r < R2; ++r) {
-      S[2 * r] += static_cast<double>(sacc[r].x);
-      S[2 * r + 1] += static_cast<double>(sacc[r].y);
+      const int64_t ra = rb * rows_per_block + (2 * r) * 256 + threadIdx.x;
+      const int64_t rc = ra + 256;
+      double* out = partial + static_cast<int64_t>(seg) * M;
+      if (ra < M) out[ra] = S[2 * r];
+      if (rc < M) out[rc] = S[2 * r + 1];
     }
-  }
-#pragma unroll
-  for (int r = 0; r < R2; ++r) {
-    const int64_t ra = rb * rows_per_block + (2 * r) * 256 + threadIdx.x;
-    const int64_t rc = ra + 256;
-    if (ra < M) partial[static_cast<int64_t>(s) * M + ra] = S[2 * r];
-    if (rc < M) partial[static_cast<int64_t>(s) * M + rc] = S[2 * r + 1];
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void kde_finalize_kernel(
-    const double* __restrict__ partial, int64_t M, int split,
+    const double* __restrict__ partial, int64_t M, int nseg,
     const double* __restrict__ lw2max, double log_const,
     double* __restrict__ out_logpd, int* __restrict__ n_fix,
     int* __restrict__ fix_rows) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= M) return;
   double S = 0.0;
-  for (int s = 0; s < split; ++s) S += partial[static_cast<int64_t>(s) * M + i];
+  for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * M + i];
   const double off = kLn2 * (*lw2max) + log_const;
   if (!(S >= KdeCfg<T>::underflow)) {
     const int slot = atomicAdd(n_fix, 1);
@@ -344,7 +351,9 @@ constexpr int kRowPad = 64;  // Npad multiple (>= U, == CH)
 constexpr int kCH = 64;
 
 // rows per thread; fp32: R = 2*R2 rows in float2 pairs, R2 and the j-unroll
-// U picked per D from the tools/probes/kde_variants.hip sweep on MI355X
+// U picked per D from the tools/probes/kde_variants.hip sweep on MI355X.
+// Small launches drop to fewer rows per thread (tier 1, 2) to fill the chip;
+// the tier only changes how rows map to lanes, never a row's arithmetic.
 template <typename T, int D>
 struct RowsPerThread;
 template <int D>
@@ -358,43 +367,75 @@ struct RowsPerThread<float, D> {
   static constexpr int value = 2 * pairs;
 };
 
+// The j-range [0, npad) is cut into nseg fixed segments that depend on npad
+// ONLY (a power of two, <= 64, segments of >= ~2048 rows, multiples of CH).
+// Every row's density is the fixed-order fp64 sum of its nseg segment sums,
+// each a sequential fp64 sum of 64-pair fp32 chunk sums -- so a row's bits
+// do not depend on M, on the launch shape, or on how many ranks share the
+// rows (multi-GPU results equal single-GPU results bit for bit).
+static int kde_segments(int64_t npad) {
+  const int64_t q = npad / 2048;
+  int n = 1;
+  while (n < 64 && 2 * n <= q) n *= 2;
+  return n;
+}
+
 struct Plan {
-  int split;
-  int64_t jchunk;
+  int split;    // blocks per row block (power of two, divides nseg)
+  int nseg;     // j-segments (power of two)
+  int spb;      // segments per block = nseg / split
+  int jseg;     // rows per segment (multiple of kCH)
+  int tier;     // 0: full rows per thread, 1: half, 2: quarter
+  int rows_per_thread;
   int64_t row_blocks;
 };
 
 template <typename T, int D>
 static Plan make_plan(int64_t M, int64_t npad) {
   constexpr int R = RowsPerThread<T, D>::value;
+  constexpr int64_t target_blocks = 8192;  // ~4 waves of 2048 resident blocks
   Plan p;
-  p.row_blocks = ceil_div(M, 256 * R);
-  const int64_t target_blocks = 8192;  // ~4 waves of 2048 resident blocks
-  int64_t split = ceil_div(target_blocks, p.row_blocks);
-  if (split > 8) split = ceil_div(split, 8) * 8;  // XCD-aligned
-  const int64_t max_split = npad / kCH;
-  if (split > max_split) split = max_split;
-  if (split < 1) split = 1;
-  p.split = static_cast<int>(split);
-  p.jchunk = ceil_div(ceil_div(npad, split), kCH) * kCH;
+  p.nseg = kde_segments(npad);
+  p.jseg = static_cast<int>(ceil_div(ceil_div(npad, p.nseg), kCH) * kCH);
+  constexpr int min_rows = sizeof(T) == 4 ? 2 : 1;  // fp32: one float2 pair
+  p.tier = 0;
+  while (p.tier < 2 && (R >> (p.tier + 1)) >= min_rows &&
+         ceil_div(M, 256 * (R >> p.tier)) * p.nseg < target_blocks / 2)
+    ++p.tier;
+  p.rows_per_thread = R >> p.tier;
+  p.row_blocks = ceil_div(M, 256 * p.rows_per_thread);
+  int split = 1;
+  while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
+  p.split = split;
+  p.spb = p.nseg / split;
   return p;
 }
 
 template <typename T>
 static size_t ws_bytes_impl(int64_t M, int64_t npad, int d) {
-  // partial[split*M] doubles + n_fix (16 B) + fix_rows[M] ints
-  const int D = padded_dim(d);
-  if (D < 0) return 0;
-  int64_t split;
-  switch (D) {
-#define CASE(DD) \
-  case DD: split = make_plan<T, DD>(M, npad).split; break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
-    CASE(20) CASE(24) CASE(32)
-#undef CASE
-    default: return 0;
-  }
-  return static_cast<size_t>(split * M) * 8 + 16 + static_cast<size_t>(M) * 4 + 256;
+  // partial[nseg*M] doubles + n_fix (16 B) + fix_rows[M] ints
+  if (padded_dim(d) < 0) return 0;
+  const int64_t nseg = kde_segments(npad);
+  return static_cast<size_t>(nseg * M) * 8 + 16 + static_cast<size_t>(M) * 4 + 256;
+}
+
+template <int D, int R2>
+static void launch_pk(const Plan& p, unsigned grid, const float* Ynew,
+                      int64_t M, const float* P, int64_t npad, double* partial,
+                      hipStream_t stream) {
+  constexpr int U = RowsPerThread<float, D>::unroll;
+  hipLaunchKernelGGL((kde_main_pk_kernel<D, R2, U, kCH>), dim3(grid), dim3(256),
+                     0, stream, Ynew, M, P, npad, p.split, p.spb, p.jseg,
+                     partial);
+}
+
+template <typename T, int D, int R>
+static void launch_generic(const Plan& p, unsigned grid, const T* Ynew,
+                           int64_t M, const T* P, int64_t npad,
+                           double* partial, hipStream_t stream) {
+  hipLaunchKernelGGL((kde_main_kernel<T, D, R, 2, kCH>), dim3(grid), dim3(256),
+                     0, stream, Ynew, M, P, npad, p.split, p.spb, p.jseg,
+                     partial);
 }
 
 template <typename T, int D>
@@ -403,30 +444,39 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
                        double* out_logpd, void* ws, size_t ws_bytes,
                        hipStream_t stream) {
   const Plan p = make_plan<T, D>(M, npad);
-  const size_t need = static_cast<size_t>(p.split * M) * 8 + 16 +
+  const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
   ABC_REQUIRE(ws_bytes >= need, "kde: workspace too small (%zu < %zu)",
               ws_bytes, need);
   char* base = static_cast<char*>(ws);
   double* partial = reinterpret_cast<double*>(base);
-  int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.split * M) * 8);
+  int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.nseg * M) * 8);
   int* fix_rows = n_fix + 4;
   ABC_HIP(hipMemsetAsync(n_fix, 0, 16, stream));
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
   if constexpr (sizeof(T) == 4) {
-    using RP = RowsPerThread<float, D>;
-    hipLaunchKernelGGL((kde_main_pk_kernel<D, RP::pairs, RP::unroll, kCH>),
-                       dim3(grid), dim3(256), 0, stream, Ynew, M, P, npad,
-                       p.split, p.jchunk, partial);
+    constexpr int R2 = RowsPerThread<float, D>::pairs;
+    if (p.tier == 0)
+      launch_pk<D, R2>(p, grid, Ynew, M, P, npad, partial, stream);
+    else if (p.tier == 1 || R2 < 4)
+      launch_pk<D, (R2 > 1 ? R2 / 2 : 1)>(p, grid, Ynew, M, P, npad, partial,
+                                          stream);
+    else
+      launch_pk<D, 1>(p, grid, Ynew, M, P, npad, partial, stream);
     ABC_LAUNCH_CHECK("kde_main_pk_kernel");
   } else {
     constexpr int R = RowsPerThread<T, D>::value;
-    hipLaunchKernelGGL((kde_main_kernel<T, D, R, 2, kCH>), dim3(grid), dim3(256),
-                       0, stream, Ynew, M, P, npad, p.split, p.jchunk, partial);
+    if (p.tier == 0)
+      launch_generic<T, D, R>(p, grid, Ynew, M, P, npad, partial, stream);
+    else if (p.tier == 1 || R < 4)
+      launch_generic<T, D, (R > 1 ? R / 2 : 1)>(p, grid, Ynew, M, P, npad,
+                                                partial, stream);
+    else
+      launch_generic<T, D, 1>(p, grid, Ynew, M, P, npad, partial, stream);
     ABC_LAUNCH_CHECK("kde_main_kernel");
   }
   hipLaunchKernelGGL((kde_finalize_kernel<T>), dim3(ceil_div(M, 256)),
-                     dim3(256), 0, stream, partial, M, p.split, lw2max,
+                     dim3(256), 0, stream, partial, M, p.nseg, lw2max,
                      log_const, out_logpd, n_fix, fix_rows);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
   hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(64), dim3(256), 0, stream,
@@ -529,6 +579,8 @@ size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d) {
   const size_t b = ws_bytes_impl<double>(M, npad, d);
   return a > b ? a : b;
 }
+
+int abc_kde_segments(int64_t npad) { return kde_segments(npad); }
 
 int abc_kde_split(int64_t M, int64_t npad, int d) {
   switch (padded_dim(d)) {

@@ -507,10 +507,11 @@ int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
   return kOk;
 }
 
-static void local_plan(int64_t M, int64_t N, int& split, int64_t& nchunk) {
-  const int64_t row_blocks = ceil_div(M, 256);
-  int64_t sp = ceil_div(4096, row_blocks);
-  if (sp > 64) sp = 64;
+// The n-range is cut into a fixed number of chunks that depends on N only,
+// so a row's log-sum-exp does not depend on M or on how rows are shared
+// between ranks (multi-GPU results equal single-GPU results bit for bit).
+static void local_plan(int64_t /*M*/, int64_t N, int& split, int64_t& nchunk) {
+  int64_t sp = 64;
   if (sp > N) sp = N;
   if (sp < 1) sp = 1;
   split = static_cast<int>(sp);

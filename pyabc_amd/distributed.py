@@ -1,12 +1,14 @@
 """One process per GPU: rank/world plumbing over torch.distributed.
 
 Backend "nccl" (RCCL on ROCm, over xGMI) on the GPU box; "gloo" for the CPU
-tests.  The generation path uses exactly three collectives per generation
-(engine.py): all-gather of the accepted rows (theta, distance, weight),
-all-reduce of the evaluation count, and an all-gather of per-rank row counts
-that sizes the first one.  Everything after the gather (weight
-normalisation, fit, epsilon) is computed redundantly and deterministically
-on every rank from identical inputs, so no further exchange is needed.
+tests.  The generation path (engine.py) exchanges, per sampling round, the per-rank
+in-support and accepted counts (two R-int all-gathers: they assign global
+evaluation ids and find the n-th acceptance), and once per generation the
+accepted rows (theta, distance; all-gather), the evaluation count
+(all-reduce) and the KDE log-densities of each rank's row slice
+(all-gather).  Everything after that (weight normalisation, fit, epsilon) is
+computed redundantly and deterministically on every rank from identical
+inputs, so no further exchange is needed.
 """
 import os
 
@@ -74,6 +76,41 @@ class Comm:
         bufs = [torch.empty_like(pad) for _ in range(self.world)]
         dist.all_gather(bufs, pad.contiguous())
         return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+
+    def _int_dev(self):
+        return torch.device("cuda", torch.cuda.current_device()) \
+            if torch.cuda.is_available() and \
+            dist.get_backend() == "nccl" else torch.device("cpu")
+
+    def all_gather_ints(self, v):
+        """[v_0, ..., v_{R-1}] from every rank's int (or 1-element tensor)."""
+        if not self.active:
+            return [int(v.item()) if torch.is_tensor(v) else int(v)]
+        dev = self._int_dev()
+        x = v.reshape(1).to(device=dev, dtype=torch.int64) if torch.is_tensor(v) \
+            else torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        bufs = [torch.empty_like(x) for _ in range(self.world)]
+        dist.all_gather(bufs, x)
+        return [int(b.item()) for b in bufs]
+
+    def all_gather_int_lists(self, vals):
+        """Every rank's equal-length int list, indexed [rank][k]."""
+        if not self.active:
+            return [list(vals)]
+        dev = self._int_dev()
+        x = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+        bufs = [torch.empty_like(x) for _ in range(self.world)]
+        dist.all_gather(bufs, x)
+        return [[int(a) for a in b.cpu().tolist()] for b in bufs]
+
+    def all_reduce_ints(self, vals):
+        """Element-wise sum over ranks of an int list (one collective)."""
+        if not self.active:
+            return [int(v) for v in vals]
+        x = torch.tensor([int(v) for v in vals], dtype=torch.int64,
+                         device=self._int_dev())
+        dist.all_reduce(x)
+        return [int(a) for a in x.cpu().tolist()]
 
     def all_reduce_int(self, v):
         if not self.active:

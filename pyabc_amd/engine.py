@@ -104,6 +104,59 @@ class DeviceMVNFit:
                                 sid, offset, B)
 
 
+def selection_plan(nvs, nas, n):
+    """Which rows of each (round k, rank s) segment form the population.
+
+    ``nvs[k][s]`` / ``nas[k][s]``: in-support evaluations / acceptances of
+    rank s in round k; within a round rank s's evaluation ids precede rank
+    s+1's, and rounds follow each other.  Returns ``takes[k][s]`` (the first
+    takes accepted rows of the segment belong to the first n accepted) and
+    ``closing[k][s]`` = 0 before the segment holding the n-th acceptance
+    (all its evaluations count), 1 for that segment, 2 after it.
+    """
+    takes, closing = [], []
+    acc = 0
+    state = 0
+    for nv_k, na_k in zip(nvs, nas):
+        tk, cl = [], []
+        for s in range(len(na_k)):
+            t = int(min(max(n - acc, 0), na_k[s]))
+            if state == 0 and t > 0 and acc + t == n:
+                cl.append(1)
+                state = 2
+            else:
+                cl.append(state)
+            tk.append(t)
+            acc += int(na_k[s])
+        takes.append(tk)
+        closing.append(cl)
+    return takes, closing
+
+
+def gather_segments(comm, pieces, row_shape, counts, device):
+    """Global row order from per-rank pieces: ``pieces`` are this rank's
+    non-empty segments in round order, ``counts[s][k]`` the rows rank s holds
+    from round k.  Returns the rows ordered round-major, then by rank -- the
+    global id order -- on every rank (one all-gather)."""
+    local = torch.cat(pieces) if pieces else torch.empty(
+        (0,) + tuple(row_shape), dtype=F64, device=device)
+    R = comm.world
+    if R == 1:
+        return local
+    allr = comm.all_gather_rows(local)
+    starts = [0]
+    for s in range(R):
+        starts.append(starts[-1] + sum(counts[s]))
+    out = []
+    for k in range(len(counts[0])):
+        for s in range(R):
+            c = counts[s][k]
+            if c:
+                off = starts[s] + sum(counts[s][:k])
+                out.append(allr[off:off + c])
+    return torch.cat(out) if out else allr[:0]
+
+
 class GenerationResult:
     def __init__(self, **kw):
         self.__dict__.update(kw)
@@ -138,112 +191,162 @@ class GenerationEngine:
 
     # ------------------------------------------------------------------
     def _sid(self, t, kind):
-        # disjoint Philox stream ids per (generation, rank, purpose)
-        return ((int(t) * 4096 + self.comm.rank) * 8 + kind)
+        # disjoint Philox stream ids per (generation, purpose); shared by all
+        # ranks -- a proposal's random numbers are keyed by its GLOBAL id, so
+        # the draws do not depend on the number of ranks
+        return int(t) * 8 + kind
 
     def quota(self, n):
-        """Accepted particles this rank contributes to a population of n."""
+        """Rows of a population of n this rank owns for row-parallel work."""
+        lo, hi = self.row_range(n)
+        return hi - lo
+
+    def row_range(self, n):
+        """[lo, hi) of the balanced contiguous row split of n rows."""
         R, r = self.comm.world, self.comm.rank
-        return n // R + (1 if r < n % R else 0)
+        q, m = divmod(n, R)
+        lo = r * q + min(r, m)
+        return lo, lo + q + (1 if r < m else 0)
 
     # ------------------------------------------------------------------
     def sample_prior(self, t, n):
         """t = 0 / calibration: theta ~ prior, all accepted
-        (smc.py:486-534 with all_accepted=True)."""
-        nq = self.quota(n)
+        (smc.py:486-534 with all_accepted=True).  Rank r draws the global
+        rows row_range(n); all-gathering in rank order gives the population
+        a single GPU would draw."""
+        lo, hi = self.row_range(n)
         theta = K.prior_uniform(self.lo, self.scale, self.seed,
-                                self._sid(t, 0), 0, nq)
-        stats = self.model.simulate(theta, self.seed, self._sid(t, 1), 0)
-        return GenerationResult(theta=theta, stats_T=stats, n_eval=nq,
-                                rec_stats_T=stats, n_rec=nq)
+                                self._sid(t, 0), lo, hi - lo)
+        stats = self.model.simulate(theta, self.seed, self._sid(t, 1), lo)
+        return GenerationResult(theta=theta, stats_T=stats, n_eval=hi - lo,
+                                rec_stats_T=stats, n_rec=hi - lo)
 
     def sample_generation(self, t, n, fit, x0, fw, eps, keep_stats=None,
                           record=None, stream_base=0):
-        """Proposals until this rank's quota of n is accepted, then KDE
-        weights.  ``fit=None`` proposes from the prior (generation 0,
-        weight 1).  Returns the rank-local accepted rows; with ``record``
-        also the statistics of every evaluated proposal up to the last
-        acceptance (record_rejected, sampler/base.py:119-141)."""
+        """Proposals until n are accepted (over all ranks), then KDE weights.
+
+        Global-id semantics (SingleCoreSampler, singlecore.py:19-38): raw
+        proposal p draws its resample/perturbation numbers from Philox
+        counter p; the in-support proposals get consecutive evaluation ids
+        (their simulation noise is keyed by that id); the population is the
+        first n accepted evaluation ids.  Each round the ranks take adjacent
+        slices of the raw-id range and exchange their in-support and accepted
+        counts, so the result -- rows, order, evaluation count, recorded
+        statistics -- is the same bit for bit for any number of ranks.
+
+        ``fit=None`` proposes from the prior (generation 0, weight 1).
+        Returns the GLOBAL population (identical on every rank): theta, d,
+        unnormalised w, logpd, n_eval, and with ``keep_stats`` / ``record``
+        the accepted statistics / the statistics of every evaluation up to
+        the n-th acceptance (record_rejected, sampler/base.py:119-141),
+        stat-major."""
         keep_stats = self.record_stats if keep_stats is None else keep_stats
         record = self.record_stats if record is None else record
-        nq = self.quota(n)
+        comm = self.comm
+        R, r = comm.world, comm.rank
         tm = {}
         t0 = time.perf_counter()
         rounds = []
         n_acc = 0
-        prop_off = 0
-        sim_off = 0
-        while n_acc < nq:
-            need = nq - n_acc
-            B = int(min(self.max_batch, max(
+        raw_off = 0
+        eval_off = 0
+        while n_acc < n:
+            need = n - n_acc
+            B_glob = int(min(self.max_batch * R, max(
                 self.min_batch,
                 math.ceil(1.2 * need / max(self.acc_rate_est, 1e-3)
                           / max(self.valid_rate_est, 1e-3)))))
+            B = -(-B_glob // R)
+            my_raw = raw_off + r * B
             if fit is None:
                 theta = K.prior_uniform(self.lo, self.scale, self.seed,
-                                        self._sid(t, stream_base), prop_off, B)
-                nv = B
+                                        self._sid(t, stream_base), my_raw, B)
+                nvs = [B] * R
             else:
                 theta_all, idx, sup = fit.propose(
                     self.lo, self.scale, self.seed,
-                    self._sid(t, stream_base), prop_off, B)
+                    self._sid(t, stream_base), my_raw, B)
                 vpos, vcount = K.compact(sup)
-                nv = int(vcount.item())                             # sync 1
-                self.valid_rate_est = max(nv / B, 1e-3)
+                nvs = comm.all_gather_ints(vcount)                  # sync 1
+                nv = nvs[r]
                 theta = K.gather_rows(theta_all, vpos, nv) if nv else None
-            prop_off += B
-            if nv == 0:
-                continue
-            stats = self.model.simulate(theta, self.seed,
-                                        self._sid(t, stream_base + 1), sim_off)
-            sim_off += nv
+            nv = nvs[r]
+            my_eval = eval_off + sum(nvs[:r])
+            if nv:
+                stats = self.model.simulate(
+                    theta, self.seed, self._sid(t, stream_base + 1), my_eval)
+            else:
+                stats = None
             if x0 is None:
                 # calibration sample: everything accepted, distances later
                 # (smc.py:486-514: accepted_distances = [inf])
                 d = torch.full((nv,), math.inf, dtype=F64, device=self.dev)
                 guard = torch.zeros(nv, dtype=torch.uint8, device=self.dev)
                 apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
-                na = nv
-            else:
+                nas = list(nvs)
+            elif nv:
                 d, acc, guard = K.pnorm_distance(stats, x0, fw, self.p, eps,
                                                  B=nv)
                 apos, acount = K.compact(acc)
-                na = int(acount.item())                             # sync 2
-            self.acc_rate_est = max(na / nv, 1e-4)
-            rounds.append((theta, stats, d, apos, na, nv, guard))
-            n_acc += na
+                nas = comm.all_gather_ints(acount)                  # sync 2
+            else:
+                d = guard = apos = None
+                nas = comm.all_gather_ints(0)
+            rounds.append(dict(theta=theta, stats=stats, d=d, apos=apos,
+                               guard=guard, nvs=nvs, nas=nas, acc0=n_acc))
+            raw_off += R * B
+            eval_off += sum(nvs)
+            n_acc += sum(nas)
+            self.valid_rate_est = max(sum(nvs) / (R * B), 1e-3)
+            if sum(nvs):
+                self.acc_rate_est = max(sum(nas) / sum(nvs), 1e-4)
             if self.max_rounds is not None and len(rounds) >= self.max_rounds \
-                    and n_acc < nq:
+                    and n_acc < n:
                 raise RuntimeError("acceptance rate too low: "
-                                   f"{n_acc}/{sim_off} after {len(rounds)} "
+                                   f"{n_acc}/{eval_off} after {len(rounds)} "
                                    "rounds")
         tm["propose_sim_dist"] = time.perf_counter() - t0
-        # first nq accepted in proposal order; evaluations up to the nq-th
-        thetas, ds, stats_acc, recs = [], [], [], []
-        n_eval = 0
-        left = nq
+
+        # the first n accepted in global id order; evaluations up to the
+        # n-th.  Segment (round k, rank s) holds takes[k][s] accepted rows
+        # and last[k][s] recorded evaluations; the local pieces are ours.
+        takes, closing = selection_plan([rd["nvs"] for rd in rounds],
+                                        [rd["nas"] for rd in rounds], n)
+        lasts = []
+        th_loc, d_loc, st_loc, rec_loc = [], [], [], []
         n_guard = 0
-        for (theta, stats, d, apos, na, nv, guard) in rounds:
-            take = min(left, na)
-            sel = apos[:take]
-            # the round holding the nq-th acceptance counts evaluations up
-            # to and including it (singlecore.py:24-35)
-            last = int(apos[take - 1].item()) + 1 if take == left else nv
-            n_eval += last
-            thetas.append(theta.index_select(0, sel))
-            ds.append(d.index_select(0, sel))
-            if keep_stats:
-                stats_acc.append(stats.index_select(1, sel))
-            if record:
-                recs.append(stats[:, :last])
-            n_guard += int(guard[:last].sum().item())
-            left -= take
-            if left == 0:
-                break
-        theta_acc = torch.cat(thetas) if thetas else torch.empty(
-            (0, self.d), dtype=F64, device=self.dev)
-        d_acc = torch.cat(ds) if ds else torch.empty(0, dtype=F64,
-                                                     device=self.dev)
+        n_eval_loc = 0
+        for rd, take, cl in zip(rounds, takes, closing):
+            k = take[r]
+            if cl[r] == 1:          # this rank holds the n-th acceptance
+                last = int(rd["apos"][k - 1].item()) + 1
+            elif cl[r] == 0:        # before it: every evaluation counts
+                last = rd["nvs"][r]
+            else:                   # after it
+                last = 0
+            lasts.append(last)
+            n_eval_loc += last
+            if k:
+                sel = rd["apos"][:k]
+                th_loc.append(rd["theta"].index_select(0, sel))
+                d_loc.append(rd["d"].index_select(0, sel))
+                if keep_stats:
+                    st_loc.append(rd["stats"].index_select(1, sel))
+            if last:
+                if record:
+                    rec_loc.append(rd["stats"][:, :last])
+                n_guard += int(rd["guard"][:last].sum().item())
+        n_eval, n_guard = comm.all_reduce_ints([n_eval_loc, n_guard])
+        take_counts = [[tk[s] for tk in takes] for s in range(R)]
+        theta_acc = self._gather(th_loc, (self.d,), take_counts)
+        d_acc = self._gather(d_loc, (), take_counts)
+        stats_acc = None
+        if keep_stats:
+            stats_acc = self._gather_cols(st_loc, take_counts)
+        rec = None
+        if record:
+            last_counts = comm.all_gather_int_lists(lasts)
+            rec = self._gather_cols(rec_loc, last_counts)
         torch.cuda.synchronize()
         tm["select"] = time.perf_counter() - t0 - tm["propose_sim_dist"]
         t1 = time.perf_counter()
@@ -251,35 +354,45 @@ class GenerationEngine:
             logpd = None
             w = torch.ones(theta_acc.shape[0], dtype=F64, device=self.dev)
         else:
+            # row-parallel weight pass: rank r weights rows row_range(n)
+            lo, hi = self.row_range(theta_acc.shape[0])
+            mine = theta_acc[lo:hi]
             if self.kde_events is not None and hasattr(fit, "packed"):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                Y = fit.packed.whiten(theta_acc)
+                Y = fit.packed.whiten(mine)
                 e0.record()
-                logpd = fit.packed.logpdf_whitened(Y)
+                lp = fit.packed.logpdf_whitened(Y)
                 e1.record()
-                self.kde_events.append((e0, e1, theta_acc.shape[0], fit.n))
+                self.kde_events.append((e0, e1, hi - lo, fit.n))
             else:
-                logpd = fit.logpdf(theta_acc)
+                lp = fit.logpdf(mine)
+            logpd = comm.all_gather_rows(lp)
             w = K.importance_weights(logpd, None, self.prior_pd)
         torch.cuda.synchronize()
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm
         return GenerationResult(
             theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
-            n_guard=n_guard,
-            stats_T=torch.cat(stats_acc, 1) if stats_acc else None,
-            rec_stats_T=torch.cat(recs, 1) if recs else None)
+            n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec)
+
+    def _gather(self, pieces, row_shape, counts):
+        return gather_segments(self.comm, pieces, row_shape, counts, self.dev)
+
+    def _gather_cols(self, pieces, counts):
+        """Stat-major [S, cols] version of :meth:`_gather` (contiguous)."""
+        S = self.model.n_stats
+        if self.comm.world == 1:
+            return torch.cat(pieces, 1) if pieces else torch.empty(
+                (S, 0), dtype=F64, device=self.dev)
+        rows = self._gather([x.t() for x in pieces], (S,), counts)
+        return rows.t().contiguous()
 
     # ------------------------------------------------------------------
     def gather_population(self, res):
-        """All-gather the rank-local accepted rows (rank-major order) and
-        normalise the weights by the global sum (population.py:120-142)."""
-        comm = self.comm
-        theta = comm.all_gather_rows(res.theta)
-        d = comm.all_gather_rows(res.d)
-        w = comm.all_gather_rows(res.w)
+        """Normalise the (already global) population's weights by their sum
+        (population.py:120-142).  Kept for callers of the per-rank API."""
+        w = res.w.clone()
         s = K.dsum(w)
         K.scale_inplace(w, s)
-        n_eval = comm.all_reduce_int(res.n_eval)
-        return theta, d, w, n_eval, s
+        return res.theta, res.d, w, res.n_eval, s

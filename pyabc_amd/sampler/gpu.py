@@ -168,21 +168,14 @@ class GPUBatchSampler(Sampler):
                                         keep_stats=True, record=record)
             eng.model = spec.models[0]
             keys = keys_d
-        comm = eng.comm
-        theta = comm.all_gather_rows(res.theta)
-        d = comm.all_gather_rows(res.d)
-        w = comm.all_gather_rows(res.w)
-        stats = comm.all_gather_rows(res.stats_T.t().contiguous()).t() \
-            if res.stats_T is not None else None
+        # the engine returns the global population, identical on every rank
         rec = None
         if res.rec_stats_T is not None:
-            rec = DeviceStats(comm.all_gather_rows(
-                res.rec_stats_T.t().contiguous()).t().contiguous(), keys)
-        self.nr_evaluations_ = comm.all_reduce_int(res.n_eval)
+            rec = DeviceStats(res.rec_stats_T, keys)
+        self.nr_evaluations_ = int(res.n_eval)
         self.last_timers = dict(eng.timers)
-        pop = ColumnarPopulation(theta, w, d, names,
-                                 stats.contiguous() if stats is not None
-                                 else None, keys)
+        pop = ColumnarPopulation(res.theta, res.w, res.d, names,
+                                 res.stats_T, keys)
         return BatchSample(pop, rec, record)
 
     def _closure_path(self, n, simulate_one, max_eval):

@@ -2,9 +2,10 @@
 
 Two ranks share cuda:0 and exchange through gloo (host-staged all-gather),
 so the exact engine / bench code that runs one rank per GPU over RCCL is
-exercised with real HIP kernels: per-rank Philox streams and quotas, the
-all-gather of the accepted rows, the all-reduced evaluation count, and the
-redundant deterministic fit / epsilon on every rank.
+exercised with real HIP kernels: global-id Philox streams, the per-round
+count exchange, the all-gather of the accepted rows, the row-parallel KDE
+pass with its all-gathered log-densities, and the redundant deterministic
+fit / epsilon on every rank -- checked bit for bit against one rank.
 """
 import json
 import math
@@ -31,23 +32,20 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, n, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    sys.path.insert(0, ROOT)
+def _generation(comm, n, min_batch, record):
+    """Prior population, one SMC generation, the next epsilon: the bench's
+    and the sampler's sequence of engine calls."""
     from pyabc_amd import kernels as K
     from pyabc_amd.batch_models import LinearGaussianModel
-    from pyabc_amd.distributed import Comm
     from pyabc_amd.engine import GenerationEngine, DeviceMVNFit
-    comm = Comm.from_env("gloo", device=0)
     d, S = 4, 20
     model = LinearGaussianModel.benchmark(d, S)
     x0 = torch.as_tensor(model._x0, device="cuda")
     fw = torch.ones(S, dtype=torch.float64, device="cuda")
     eng = GenerationEngine(model, np.full(d, -5.0), np.full(d, 10.0),
                            distance_p=2.0, comm=comm, seed=7,
-                           min_batch=1 << 12)
+                           min_batch=min_batch)
+    eng.max_batch = min_batch     # several sampling rounds per generation
     r0 = eng.sample_prior(0, n)
     d0, _, _ = K.pnorm_distance(r0.stats_T, x0, fw, 2.0, math.inf,
                                 with_accept=False)
@@ -57,45 +55,63 @@ def _rank_main(rank, world, port, n, out):
                    dtype=torch.float64, device="cuda")
     eps = float(K.weighted_quantile(dist, w, 0.5)[0].item())
     fit = DeviceMVNFit(theta, w)
-    res = eng.sample_generation(1, n, fit, x0, fw, eps)
+    res = eng.sample_generation(1, n, fit, x0, fw, eps, keep_stats=True,
+                                record=record)
     th, dd, ww, n_eval, _ = eng.gather_population(res)
     eps1 = float(K.weighted_quantile(dd, ww, 0.5)[0].item())
-    # the rank-local KDE weights must equal a recomputation of the same rows
-    # against the same (gathered) previous population
-    logpd = fit.logpdf(res.theta)
-    out[rank] = dict(
-        n_local=int(res.theta.shape[0]), quota=eng.quota(n),
-        n_total=int(th.shape[0]), n_eval=int(n_eval),
-        local_eval=int(res.n_eval),
-        wsum=float(ww.sum().item()),
-        theta_sum=float(th.sum().item()), eps0=eps, eps1=eps1,
-        all_accepted=bool((dd <= eps).all().item()),
-        logpd_err=float((logpd - res.logpd).abs().max().item()),
-        mean=th.mul(ww[:, None]).sum(0).cpu().numpy().tolist())
+    fit1 = DeviceMVNFit(th, ww)
+    return dict(theta0=theta.cpu().numpy(), eps0=eps, theta=th.cpu().numpy(),
+                d=dd.cpu().numpy(), w=ww.cpu().numpy(),
+                logpd=res.logpd.cpu().numpy(), n_eval=int(n_eval),
+                stats=res.stats_T.cpu().numpy(),
+                rec=None if res.rec_stats_T is None
+                else res.rec_stats_T.cpu().numpy(),
+                eps1=eps1, cov1=fit1.cov)
+
+
+def _rank_main(rank, world, port, n, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from pyabc_amd.distributed import Comm
+    comm = Comm.from_env("gloo", device=0)
+    multi = _generation(comm, n, 1 << 11, record=True)
+    if rank == 0:
+        # the same generation on one rank, with a different round size
+        single = _generation(Comm.single(), n, 1 << 12, record=True)
+        out["single"] = single
+    out[rank] = multi
     torch.distributed.destroy_process_group()
 
 
 @pytest.mark.timeout(240)
-def test_two_ranks_share_one_gpu_generation():
+def test_two_ranks_equal_one_rank_bit_for_bit():
+    """Global-id sampling (engine.sample_generation): two ranks sharing
+    cuda:0 over gloo produce exactly the population, distances, weights,
+    evaluation count, recorded statistics, next epsilon and next fit that
+    one rank produces -- with different sampling-round sizes too."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    n = 6001          # odd: uneven per-rank quotas
+    n = 6001          # odd: uneven row slices for the weight pass
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_rank_main, args=(2, port, n, out), nprocs=2, join=True)
         res = dict(out)
-    r0, r1 = res[0], res[1]
-    assert r0["quota"] + r1["quota"] == n and abs(r0["quota"] - r1["quota"]) == 1
-    assert r0["n_local"] == r0["quota"] and r1["n_local"] == r1["quota"]
-    for k in ("n_total", "n_eval", "wsum", "theta_sum", "eps0", "eps1", "mean"):
-        assert r0[k] == r1[k], k           # identical replicated state
-    assert r0["n_total"] == n
-    assert r0["n_eval"] == r0["local_eval"] + r1["local_eval"]
-    assert abs(r0["wsum"] - 1.0) < 1e-12
-    assert r0["all_accepted"] and r0["eps1"] <= r0["eps0"]
-    assert r0["logpd_err"] == 0.0 and r1["logpd_err"] == 0.0
-    assert np.all(np.abs(r0["mean"]) < 5.0)     # inside the prior box
+    one = res["single"]
+    for r in (0, 1):
+        got = res[r]
+        for k in ("theta0", "theta", "d", "w", "logpd", "stats", "rec",
+                  "cov1"):
+            np.testing.assert_array_equal(got[k], one[k], err_msg=k)
+        for k in ("eps0", "eps1", "n_eval"):
+            assert got[k] == one[k], k
+    assert one["theta"].shape == (n, 4)
+    assert one["rec"].shape[1] == one["n_eval"] >= n
+    assert np.all(one["d"] <= one["eps0"])
+    assert abs(one["w"].sum() - 1.0) < 1e-12
+    assert one["eps1"] <= one["eps0"]
 
 
 @pytest.mark.timeout(300)

@@ -181,3 +181,97 @@ def test_comm_gloo_world2():
         np.testing.assert_array_equal(np.array(res[r][0]), exp)
         assert res[r][1] == 3
         assert res[r][2] == 1.5
+
+
+def _emulate_rounds(sup, acc, n, R, B):
+    """The engine's round loop on host flags: raw ids split into rounds of
+    R adjacent slices of B; returns the selected eval ids and n_eval."""
+    from pyabc_amd.engine import selection_plan
+    nvs, nas, apos, evals = [], [], [], []
+    raw = 0
+    ev = 0
+    tot = 0
+    while tot < n:
+        nv_k, na_k, ap_k, ev_k = [], [], [], []
+        for s in range(R):
+            sl = slice(raw + s * B, raw + (s + 1) * B)
+            ids_ev = ev + np.arange(int(sup[sl].sum()))
+            ev += len(ids_ev)
+            a = acc[ids_ev]
+            nv_k.append(len(ids_ev))
+            na_k.append(int(a.sum()))
+            ap_k.append(np.flatnonzero(a))
+            ev_k.append(ids_ev)
+        raw += R * B
+        tot += sum(na_k)
+        nvs.append(nv_k)
+        nas.append(na_k)
+        apos.append(ap_k)
+        evals.append(ev_k)
+    takes, closing = selection_plan(nvs, nas, n)
+    sel, n_eval = [], 0
+    for k in range(len(nvs)):
+        for s in range(R):
+            t = takes[k][s]
+            sel.extend(evals[k][s][apos[k][s][:t]])
+            if closing[k][s] == 1:
+                n_eval += apos[k][s][t - 1] + 1
+            elif closing[k][s] == 0:
+                n_eval += nvs[k][s]
+    return np.array(sel, dtype=np.int64), n_eval
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_selection_plan_global_id_order(seed):
+    """The population is the first n accepted evaluation ids and n_eval
+    counts evaluations through the n-th acceptance, for any rank count and
+    round size (SingleCoreSampler semantics, singlecore.py:19-38)."""
+    rng = np.random.default_rng(seed)
+    sup = rng.uniform(size=200000) < 0.8
+    acc = rng.uniform(size=200000) < 0.3
+    for n in [1, 17, 1000, 5003]:
+        ev_acc = np.flatnonzero(acc)
+        want = ev_acc[:n]
+        want_eval = want[-1] + 1
+        for R, B in [(1, 64), (1, 4096), (2, 50), (3, 1000), (8, 257)]:
+            got, n_eval = _emulate_rounds(sup, acc, n, R, B)
+            np.testing.assert_array_equal(got, want)
+            assert n_eval == want_eval
+
+
+def _gather_worker(rank, world, port, out):
+    from pyabc_amd.engine import gather_segments
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    comm = Comm.from_env("gloo")
+    # counts[s][k]: rows rank s holds from round k; row value = global id
+    counts = [[2, 0, 1], [0, 3, 2], [1, 1, 0]][:world]
+    ids, gid = {}, 0
+    for k in range(3):
+        for s in range(world):
+            ids[(s, k)] = list(range(gid, gid + counts[s][k]))
+            gid += counts[s][k]
+    pieces = [torch.tensor(ids[(rank, k)], dtype=torch.float64).view(-1, 1)
+              .repeat(1, 2) for k in range(3) if counts[rank][k]]
+    g = gather_segments(comm, pieces, (2,), counts, torch.device("cpu"))
+    ints = comm.all_gather_ints(rank * 10 + 1)
+    lists = comm.all_gather_int_lists([rank, rank + 5])
+    red = comm.all_reduce_ints([rank, 2])
+    out[rank] = (g[:, 0].tolist(), ints, lists, red, gid)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_segments_gloo(world):
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_gather_worker, args=(world, port, out), nprocs=world,
+                 join=True)
+        res = dict(out)
+    for r in range(world):
+        g, ints, lists, red, gid = res[r]
+        assert g == list(range(gid))            # global id order
+        assert ints == [s * 10 + 1 for s in range(world)]
+        assert lists == [[s, s + 5] for s in range(world)]
+        assert red == [sum(range(world)), 2 * world]

@@ -48,8 +48,9 @@ int abc_weighted_moments_f64(const double* X, const double* w, int64_t n,
  * and the support test prior.pdf(theta) > 0         smc.py:643-645,
  *                                                    random_variables.py:425-452
  * lo/scale may be NULL (no support test). */
-int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf,
-                         hipStream_t stream);
+size_t abc_resample_cdf_workspace_bytes(int64_t n);
+int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf, void* ws,
+                         size_t ws_bytes, hipStream_t stream);
 int abc_resample_perturb_f64(const double* X, int64_t N, int d,
                              const double* cdf, const double* u,
                              const double* z, const double* A,

@@ -38,7 +38,9 @@ _SIGS = {
     "abc_weighted_moments_f64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
                                          c_ptr, c_size, c_ptr]),
     # (a2)
-    "abc_resample_cdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr]),
+    "abc_resample_cdf_workspace_bytes": (c_size, [c_i64]),
+    "abc_resample_cdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_size,
+                                     c_ptr]),
     "abc_resample_perturb_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                          c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
                                          c_ptr, c_ptr, c_ptr, c_ptr]),

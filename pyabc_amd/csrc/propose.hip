@@ -26,147 +26,404 @@ namespace abc {
 // u = 2^(e-52), so with C = c/u (an integer < 2^53) and v = w * 2^(52-e)
 // (exact scaling) the rounded sum is fl(c + w) = u * (C + floor(v) +
 // [frac(v) > 1/2]) -- except when frac(v) == 1/2 (a tie, resolved by the
-// parity of the result) or when the sum leaves the binade.  So a block turns
-// each 8192-element tile into INTEGER increments, prefix-sums them exactly
-// (int64), and writes every c_k up to the first element that ties or leaves
-// the binade; that element is evaluated with the real fp64 add, the grid is
-// re-derived from the new c, and the tile continues.  Breaks happen about
-// once per binade crossing (~60 for any N), so the result is bit-identical to
-// the sequential chain at tile-scan cost.
-constexpr int kScanThreads = 1024;
-constexpr int kScanItems = 8;
-constexpr int kScanTile = kScanThreads * kScanItems;
+// parity of the result) or when the sum leaves the binade.  Inside a binade
+// the chain is therefore an INTEGER prefix sum of increments that do not
+// depend on the chain itself, and a whole 1024-element tile advances it by
+// one precomputed integer T_t.
+//
+//   1. cdf_tile_sum    (tiles in parallel)  approximate fp64 tile sums
+//   2. cdf_prefix      (one block)          approximate tile-start prefixes
+//   3. cdf_tile_plan   (tiles in parallel)  the tile's binade e_t from its
+//      approximate prefix range (with a relative margin far above the
+//      chain's accumulated rounding), its integer increment total T_t under
+//      grid e_t; ties / negative / non-finite / binade-straddling tiles are
+//      marked slow
+//   4. cdf_chain       (one wave)           walks the tiles: a run of fast
+//      tiles of one binade is advanced in parallel (C_in = run start + prefix
+//      of T_t), each step VERIFIED against the exact chain value (c in
+//      binade e_t and C + T_t <= 2^53 - 2, i.e. no element leaves the
+//      binade); any other tile runs the exact walk (exact_tile_wave: integer
+//      increments, wave scan, real fp64 add at the first tie / binade exit,
+//      re-grid, continue) -- ~1 slow tile per binade crossing
+//   5. cdf_write       (tiles in parallel)  rebuilds every fast tile's
+//      elements from its exact start value C_t and the in-tile integer
+//      prefix, and divides by the last value (numpy's cdf /= cdf[-1])
+//
+// The plan only decides which tiles take which path; the chain kernel checks
+// every fast step exactly, so the result is bit-identical to the sequential
+// chain for any input.
+constexpr int kCdfThreads = 256;
+constexpr int kCdfItems = 4;
+constexpr int kCdfTile = kCdfThreads * kCdfItems;
+constexpr int kCdfSlow = -100000;
+constexpr int kChainChunk = 2048;       // tile records per LDS batch
+constexpr long long kBinadeTop = (1ll << 53) - 2;
 
-__global__ __launch_bounds__(kScanThreads) void cdf_scan_kernel(
-    const double* __restrict__ w, int64_t n, double* __restrict__ cdf) {
-  __shared__ long long wsum[kScanThreads / 64];
-  __shared__ int first_bad;
-  __shared__ double sh_c;
-  __shared__ int sh_s;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  double c = 0.0;  // running value (uniform)
-  for (int64_t base = 0; base < n; base += kScanTile) {
-    double wv[kScanItems];
+constexpr int kWaveItems = kCdfTile / 64;  // one wave walks a whole tile
+
+__device__ inline long long wave_incl_scan(long long v) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < kScanItems; ++q) {
-      const int64_t i = base + static_cast<int64_t>(tid) * kScanItems + q;
-      wv[q] = i < n ? w[i] : 0.0;
-    }
-    const int tile_n = static_cast<int>(n - base < kScanTile ? n - base : kScanTile);
-    int s = 0;  // first unprocessed element of the tile (uniform)
-    while (s < tile_n) {
-      // grid of the current binade
-      int ex;
-      const double mant = frexp(c, &ex);  // c = mant * 2^ex, mant in [0.5,1)
-      (void)mant;
-      const bool exact_mode = c >= 0x1p-1000;
-      const int e = ex - 1;
-      const long long C = exact_mode ? static_cast<long long>(ldexp(c, 52 - e)) : 0;
-      long long dl[kScanItems];
-      bool bad[kScanItems];
-      long long tsum = 0;
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ inline int wave_min_int(int v) {
 #pragma unroll
-      for (int q = 0; q < kScanItems; ++q) {
-        const int k = tid * kScanItems + q;
-        long long dq = 0;
-        bool b = false;
-        if (k >= s && k < tile_n) {
-          if (!exact_mode || wv[q] < 0.0) {
-            b = (c != 0.0) || (wv[q] != 0.0);
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ inline double wave_incl_scan_f64(double v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// The exact chain over w[base, base + tile_n) by ONE wave (no barriers):
+// integer increments on the current binade grid, a wave scan, the real fp64
+// add at the first tie / binade exit, re-grid, continue.  The integers are
+// held in fp64: every partial sum up to the first break is an integer below
+// 2^53 and therefore exact (and a sum at or past 2^53 still compares >= the
+// representable bound after rounding), which avoids int64<->fp64
+// conversions on this latency-bound single-wave path.  c (wave-uniform) in
+// and out; raw (un-normalised) values written to cdf.
+__device__ void exact_tile_wave(const double* __restrict__ w, int64_t base,
+                                int tile_n, double& c,
+                                double* __restrict__ cdf) {
+  const int lane = threadIdx.x & 63;
+  double wv[kWaveItems];
+#pragma unroll
+  for (int q = 0; q < kWaveItems; ++q) {
+    const int k = lane * kWaveItems + q;
+    wv[q] = k < tile_n ? w[base + k] : 0.0;
+  }
+  int s = 0;  // first unprocessed element of the tile (uniform)
+  while (s < tile_n) {
+    int ex;
+    (void)frexp(c, &ex);  // c = mant * 2^ex, mant in [0.5,1)
+    const bool exact_mode = c >= 0x1p-1000;
+    const int e = ex - 1;
+    const double C = exact_mode ? ldexp(c, 52 - e) : 0.0;  // integer
+    double dl[kWaveItems];
+    int my_bad = 1 << 30;
+    double tsum = 0.0;
+#pragma unroll
+    for (int q = 0; q < kWaveItems; ++q) {
+      const int k = lane * kWaveItems + q;
+      double dq = 0.0;
+      bool b = false;
+      if (k >= s && k < tile_n) {
+        if (!exact_mode || wv[q] < 0.0) {
+          b = (c != 0.0) || (wv[q] != 0.0);
+        } else {
+          const double v = ldexp(wv[q], 52 - e);
+          if (!(v < 0x1p53)) {
+            b = true;
           } else {
-            const double v = ldexp(wv[q], 52 - e);
-            if (!(v < 0x1p62)) {
-              b = true;
-            } else {
-              const double fl = floor(v);
-              const double fr = v - fl;
-              dq = static_cast<long long>(fl) + (fr > 0.5 ? 1 : 0);
-              b = (fr == 0.5);
-            }
-          }
-        }
-        tsum += dq;
-        dl[q] = tsum;  // inclusive within the thread
-        bad[q] = b;
-      }
-      // block exclusive scan of the thread totals
-      long long incl = tsum;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const long long t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      if (lane == 63) wsum[wid] = incl;
-      if (tid == 0) first_bad = 1 << 30;
-      __syncthreads();
-      long long woff = 0;
-      for (int q = 0; q < wid; ++q) woff += wsum[q];
-      const long long excl = woff + incl - tsum;
-      // binade exit: C + prefix must stay below 2^53 (with one unit margin)
-      int my_bad = 1 << 30;
-#pragma unroll
-      for (int q = 0; q < kScanItems; ++q) {
-        const int k = tid * kScanItems + q;
-        if (k >= s && k < tile_n) {
-          const long long Ck = C + excl + dl[q];
-          if (bad[q] || (exact_mode && Ck + 1 >= (1ll << 53))) {
-            my_bad = k;
-            break;
+            const double fl = floor(v);
+            const double fr = v - fl;
+            dq = fl + (fr > 0.5 ? 1.0 : 0.0);
+            b = (fr == 0.5);
           }
         }
       }
-      if (my_bad < (1 << 30)) atomicMin(&first_bad, my_bad);
-      __syncthreads();
-      const int b = first_bad;
-      // write every element before the first break
+      tsum += dq;
+      dl[q] = tsum;  // inclusive within the lane
+      if (b && my_bad == (1 << 30)) my_bad = k;
+    }
+    const double incl = wave_incl_scan_f64(tsum);
+    // exclusive prefix = the previous lane's inclusive one (NOT incl - tsum:
+    // a lane past the break may hold a sum above 2^53, inexact in fp64)
+    double excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = 0.0;
+    // binade exit: C + prefix must stay below 2^53 (one unit margin)
+    const double Cx = C + excl;
 #pragma unroll
-      for (int q = 0; q < kScanItems; ++q) {
-        const int k = tid * kScanItems + q;
-        if (k >= s && k < tile_n && k < b) {
-          const long long Ck = C + excl + dl[q];
-          cdf[base + k] = ldexp(static_cast<double>(Ck), e - 52);
-        }
-      }
-      // the breaking element: the real fp64 add, by its owner
-      if (b < tile_n && b / kScanItems == tid) {
-        const int q0 = b - tid * kScanItems;
+    for (int q = 0; q < kWaveItems; ++q) {
+      const int k = lane * kWaveItems + q;
+      if (exact_mode && k >= s && k < tile_n && k < my_bad &&
+          Cx + dl[q] >= 0x1p53 - 1.0)
+        my_bad = k;
+    }
+    const int b = wave_min_int(my_bad);
+#pragma unroll
+    for (int q = 0; q < kWaveItems; ++q) {
+      const int k = lane * kWaveItems + q;
+      if (k >= s && k < tile_n && k < b)
+        cdf[base + k] = ldexp(Cx + dl[q], e - 52);
+    }
+    if (b < tile_n) {
+      // the breaking element: the real fp64 add, by its owner lane
+      const int owner = b / kWaveItems;
+      double cb = 0.0;
+      if (lane == owner) {
+        const int q0 = b - lane * kWaveItems;
         double prev = c;
         double wb = 0.0;
-        long long dprev = 0;
+        double dprev = 0.0;
 #pragma unroll
-        for (int q = 0; q < kScanItems; ++q) {
+        for (int q = 0; q < kWaveItems; ++q) {
           if (q == q0) wb = wv[q];
           if (q == q0 - 1) dprev = dl[q];
         }
-        if (b > s) prev = ldexp(static_cast<double>(C + excl + dprev), e - 52);
-        const double cb = (base + b == 0) ? wb : prev + wb;
+        if (b > s) prev = ldexp(Cx + dprev, e - 52);
+        cb = (base + b == 0) ? wb : prev + wb;
         cdf[base + b] = cb;
-        sh_c = cb;
-        sh_s = b + 1;
       }
-      __syncthreads();
-      if (b < tile_n) {
-        c = sh_c;
-        s = sh_s;
-      } else {
-        // value at the end of the tile = C + total
-        long long total = 0;
-        for (int q = 0; q < kScanThreads / 64; ++q) total += wsum[q];
-        if (exact_mode) c = ldexp(static_cast<double>(C + total), e - 52);
-        s = tile_n;
-      }
-      __syncthreads();
+      c = __shfl(cb, owner, 64);
+      s = b + 1;
+    } else {
+      const double total = __shfl(incl, 63, 64);
+      if (exact_mode) c = ldexp(C + total, e - 52);
+      s = tile_n;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void cdf_normalize_kernel(double* __restrict__ cdf,
-                                                            int64_t n) {
-  const double last = cdf[n - 1];
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
-    cdf[i] = cdf[i] / last;
+__global__ __launch_bounds__(kCdfThreads) void cdf_tile_sum_kernel(
+    const double* __restrict__ w, int64_t n, double* __restrict__ tsum) {
+  __shared__ double red[kCdfThreads / 64];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kCdfTile;
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < kCdfItems; ++q) {
+    const int64_t i = base + q * kCdfThreads + threadIdx.x;
+    if (i < n) v += w[i];
+  }
+  v = block_sum<double, kCdfThreads>(v, red);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = v;
 }
+
+__global__ __launch_bounds__(1024) void cdf_prefix_kernel(
+    const double* __restrict__ tsum, int64_t nt, double* __restrict__ pstart) {
+  __shared__ double wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  double carry = 0.0;
+  for (int64_t b0 = 0; b0 < nt; b0 += 1024) {
+    const int64_t i = b0 + tid;
+    const double v = i < nt ? tsum[i] : 0.0;
+    double incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    double woff = 0.0, tot = 0.0;
+    for (int q = 0; q < 16; ++q) {
+      if (q < wid) woff += wsum[q];
+      tot += wsum[q];
+    }
+    if (i < nt) pstart[i] = carry + woff + incl - v;
+    __syncthreads();
+    carry += tot;
+  }
+}
+
+// integer increment of w on the grid of binade e; false if it cannot be
+// taken on the fast path (tie, negative, non-finite, too large)
+__device__ inline bool grid_increment(double w, int e, long long& dq) {
+  const double v = ldexp(w, 52 - e);
+  if (!(w >= 0.0) || !(v < 0x1p62)) return false;
+  const double fl = floor(v);
+  const double fr = v - fl;
+  dq = static_cast<long long>(fl) + (fr > 0.5 ? 1 : 0);
+  return fr != 0.5;
+}
+
+__global__ __launch_bounds__(kCdfThreads) void cdf_tile_plan_kernel(
+    const double* __restrict__ w, int64_t n, const double* __restrict__ tsum,
+    const double* __restrict__ pstart, double rel, int* __restrict__ e_t,
+    long long* __restrict__ T_t) {
+  __shared__ long long red[kCdfThreads / 64];
+  __shared__ int any_bad;
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * kCdfTile;
+  const double P0 = pstart[t];
+  const double P1 = P0 + tsum[t];
+  bool slow = !(P0 >= 0x1p-1000) || !(P1 < 0x1p1000) || t == 0;
+  int e = 0;
+  if (!slow) {
+    e = ilogb(P0 * (1.0 - rel));
+    slow = e != ilogb(P1 * (1.0 + rel));
+  }
+  if (slow) {  // block-uniform
+    if (threadIdx.x == 0) {
+      e_t[t] = kCdfSlow;
+      T_t[t] = 0;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) any_bad = 0;
+  __syncthreads();
+  long long sum = 0;
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < kCdfItems; ++q) {
+    const int64_t i = base + q * kCdfThreads + threadIdx.x;
+    if (i < n) {
+      long long dq = 0;
+      ok &= grid_increment(w[i], e, dq);
+      sum += dq;
+    }
+  }
+  if (!ok) any_bad = 1;
+  sum = block_sum<long long, kCdfThreads>(sum, red);
+  if (threadIdx.x == 0) {
+    e_t[t] = any_bad ? kCdfSlow : e;
+    T_t[t] = sum;
+  }
+}
+
+// One wave walks the tile records.  A run of fast tiles of one binade e is
+// advanced in parallel: C_in(k) = C_i + (prefix of T over the run), valid up
+// to the first tile whose end would leave the binade (found by a wave min);
+// the chain value at the run start is checked to lie in binade e.  A tile
+// that cannot start a run goes through exact_tile_wave.
+constexpr int kChainPer = kChainChunk / 64;
+
+__global__ __launch_bounds__(64) void cdf_chain_kernel(
+    const double* __restrict__ w, int64_t n, int64_t nt,
+    const int* __restrict__ e_t, const long long* __restrict__ T_t,
+    long long* __restrict__ c_start, double* __restrict__ cdf,
+    double* __restrict__ last) {
+  const int lane = threadIdx.x;
+  double c = 0.0;  // chain value (wave-uniform)
+  for (int64_t t0 = 0; t0 < nt; t0 += kChainChunk) {
+    const int cn = static_cast<int>(nt - t0 < kChainChunk ? nt - t0 : kChainChunk);
+    // this lane's records k = lane*kChainPer + q: e, T, exclusive prefix
+    int re[kChainPer];
+    long long rT[kChainPer], rP[kChainPer];
+    long long run = 0;
+#pragma unroll
+    for (int q = 0; q < kChainPer; ++q) {
+      const int k = lane * kChainPer + q;
+      re[q] = k < cn ? e_t[t0 + k] : kCdfSlow;
+      rT[q] = k < cn ? T_t[t0 + k] : 0;
+      rP[q] = run;
+      run += rT[q];
+    }
+    const long long lincl = wave_incl_scan(run);
+    const long long lexcl = lincl - run;
+#pragma unroll
+    for (int q = 0; q < kChainPer; ++q) rP[q] += lexcl;
+    int i = 0;
+    while (i < cn) {
+      const int owner = i / kChainPer, qi = i - owner * kChainPer;
+      int e_i = 0;
+      long long P_i = 0;
+#pragma unroll
+      for (int q = 0; q < kChainPer; ++q)
+        if (q == qi) {
+          e_i = re[q];
+          P_i = rP[q];
+        }
+      e_i = __shfl(e_i, owner, 64);
+      P_i = __shfl(P_i, owner, 64);
+      int j = i;
+      if (e_i != kCdfSlow) {
+        const double lo = ldexp(1.0, e_i);
+        if (c >= lo && c < 2.0 * lo) {
+          const long long Ci = static_cast<long long>(ldexp(c, 52 - e_i));
+          // first record >= i that breaks the run
+          int my_end = cn;
+#pragma unroll
+          for (int q = 0; q < kChainPer; ++q) {
+            const int k = lane * kChainPer + q;
+            if (k >= i && k < cn && k < my_end &&
+                (re[q] != e_i || Ci + (rP[q] - P_i) + rT[q] > kBinadeTop))
+              my_end = k;
+          }
+          j = wave_min_int(my_end);
+#pragma unroll
+          for (int q = 0; q < kChainPer; ++q) {
+            const int k = lane * kChainPer + q;
+            if (k >= i && k < j) c_start[t0 + k] = Ci + (rP[q] - P_i);
+          }
+          if (j > i) {
+            // chain value after tile j-1 = start of j (or chunk end)
+            long long Pj = 0;
+            const int oj = (j - 1) / kChainPer, qj = (j - 1) - oj * kChainPer;
+#pragma unroll
+            for (int q = 0; q < kChainPer; ++q)
+              if (q == qj) Pj = rP[q] + rT[q];
+            Pj = __shfl(Pj, oj, 64);
+            c = ldexp(static_cast<double>(Ci + (Pj - P_i)), e_i - 52);
+          }
+        }
+      }
+      if (j == i) {  // tile i cannot start a run: exact walk
+        const int64_t t = t0 + i;
+        const int64_t base = t * kCdfTile;
+        const int tile_n = static_cast<int>(n - base < kCdfTile ? n - base : kCdfTile);
+        exact_tile_wave(w, base, tile_n, c, cdf);
+        if (lane == 0) c_start[t] = -1;
+        j = i + 1;
+      }
+      i = j;
+    }
+  }
+  if (lane == 0) *last = c;
+}
+
+__global__ __launch_bounds__(kCdfThreads) void cdf_write_kernel(
+    const double* __restrict__ w, int64_t n, const int* __restrict__ e_t,
+    const long long* __restrict__ c_start, const double* __restrict__ last,
+    double* __restrict__ cdf) {
+  __shared__ long long wsum[kCdfThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * kCdfTile;
+  const double L = *last;
+  const long long C0 = c_start[t];
+  if (C0 < 0) {  // slow tile: raw values written by the chain kernel
+#pragma unroll
+    for (int q = 0; q < kCdfItems; ++q) {
+      const int64_t i = base + q * kCdfThreads + tid;
+      if (i < n) cdf[i] = cdf[i] / L;
+    }
+    return;
+  }
+  const int e = e_t[t];
+  long long dl[kCdfItems];
+  long long tsum = 0;
+#pragma unroll
+  for (int q = 0; q < kCdfItems; ++q) {
+    const int64_t i = base + static_cast<int64_t>(tid) * kCdfItems + q;
+    long long dq = 0;
+    if (i < n) (void)grid_increment(w[i], e, dq);
+    tsum += dq;
+    dl[q] = tsum;
+  }
+  long long incl = tsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  long long woff = 0;
+  for (int q = 0; q < wid; ++q) woff += wsum[q];
+  const long long excl = woff + incl - tsum;
+#pragma unroll
+  for (int q = 0; q < kCdfItems; ++q) {
+    const int64_t i = base + static_cast<int64_t>(tid) * kCdfItems + q;
+    if (i < n)
+      cdf[i] = ldexp(static_cast<double>(C0 + excl + dl[q]), e - 52) / L;
+  }
+}
+
+static int64_t cdf_tiles(int64_t n) { return ceil_div(n, kCdfTile); }
 
 // first index i with cdf[i] > u (numpy searchsorted side='right')
 __device__ inline int64_t search_right(const double* __restrict__ cdf, int64_t n,
@@ -402,15 +659,38 @@ using namespace abc;
 
 extern "C" {
 
-int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf,
-                         hipStream_t st) {
-  ABC_REQUIRE(n > 0 && w && cdf, "resample_cdf: need n > 0 and buffers");
-  hipLaunchKernelGGL(cdf_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, w,
-                     n, cdf);
-  ABC_LAUNCH_CHECK("cdf_scan_kernel");
-  hipLaunchKernelGGL(cdf_normalize_kernel, dim3(stream_grid(n, 256, 1024)),
-                     dim3(256), 0, st, cdf, n);
-  ABC_LAUNCH_CHECK("cdf_normalize_kernel");
+size_t abc_resample_cdf_workspace_bytes(int64_t n) {
+  // tsum, pstart, T_t, c_start (8 B each), e_t (4 B) per tile + last
+  return static_cast<size_t>(cdf_tiles(n > 0 ? n : 1)) * 40 + 256;
+}
+
+int abc_resample_cdf_f64(const double* w, int64_t n, double* cdf, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && w && cdf && ws, "resample_cdf: need n > 0 and buffers");
+  ABC_REQUIRE(ws_bytes >= abc_resample_cdf_workspace_bytes(n),
+              "resample_cdf: workspace too small");
+  const int64_t nt = cdf_tiles(n);
+  double* tsum = static_cast<double*>(ws);
+  double* pstart = tsum + nt;
+  long long* T_t = reinterpret_cast<long long*>(pstart + nt);
+  long long* c_start = T_t + nt;
+  double* last = reinterpret_cast<double*>(c_start + nt);
+  int* e_t = reinterpret_cast<int*>(last + 4);
+  // relative margin of the plan's binade test: far above both the chain's
+  // accumulated rounding (<= n ulp) and the approximate prefix's
+  const double rel = fmax(1e-9, 8.0 * static_cast<double>(n) * 0x1p-53);
+  const unsigned g = static_cast<unsigned>(nt);
+  hipLaunchKernelGGL(cdf_tile_sum_kernel, dim3(g), dim3(kCdfThreads), 0, st,
+                     w, n, tsum);
+  hipLaunchKernelGGL(cdf_prefix_kernel, dim3(1), dim3(1024), 0, st, tsum, nt,
+                     pstart);
+  hipLaunchKernelGGL(cdf_tile_plan_kernel, dim3(g), dim3(kCdfThreads), 0, st,
+                     w, n, tsum, pstart, rel, e_t, T_t);
+  hipLaunchKernelGGL(cdf_chain_kernel, dim3(1), dim3(64), 0, st, w, n,
+                     nt, e_t, T_t, c_start, cdf, last);
+  hipLaunchKernelGGL(cdf_write_kernel, dim3(g), dim3(kCdfThreads), 0, st, w, n,
+                     e_t, c_start, last, cdf);
+  ABC_LAUNCH_CHECK("resample_cdf kernels");
   return kOk;
 }
 

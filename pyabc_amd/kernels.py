@@ -66,7 +66,10 @@ def philox_normal(seed, sid, offset, n):
 def resample_cdf(w):
     w = _contig(w, F64)
     cdf = torch.empty_like(w)
-    call("abc_resample_cdf_f64", ptr(w), w.numel(), ptr(cdf), nat.stream())
+    wsb = nat.lib().abc_resample_cdf_workspace_bytes(w.numel())
+    ws = WS.get(wsb, "cdf")
+    call("abc_resample_cdf_f64", ptr(w), w.numel(), ptr(cdf), ptr(ws), wsb,
+         nat.stream())
     return cdf
 
 

@@ -284,12 +284,13 @@ def test_sim_linear_gaussian(K):
 
 
 @pytest.mark.parametrize("kind", ["uniform", "lognormal", "zeros", "ties",
-                                  "tiny", "steps"])
+                                  "tiny", "steps", "equal", "descending"])
 def test_cdf_scan_bit_exact(K, kind):
     """The parallel binade-grid scan equals numpy's sequential cumsum bit for
     bit (then /= cdf[-1]) on adversarial weight vectors."""
     rng = np.random.default_rng({"uniform": 1, "lognormal": 2, "zeros": 3,
-                                 "ties": 4, "tiny": 5, "steps": 6}[kind])
+                                 "ties": 4, "tiny": 5, "steps": 6, "equal": 7,
+                                 "descending": 8}[kind])
     n = 1_000_003
     if kind == "uniform":
         w = rng.uniform(size=n)
@@ -301,6 +302,10 @@ def test_cdf_scan_bit_exact(K, kind):
     elif kind == "ties":
         # dyadic weights: many increments land exactly half-way on the grid
         w = rng.integers(1, 1 << 12, size=n) * 2.0 ** -40
+    elif kind == "equal":
+        w = np.full(n, 1.0 / n)         # a prior population's weights
+    elif kind == "descending":
+        w = np.sort(rng.pareto(1.5, size=n))[::-1].copy()
     elif kind == "tiny":
         w = rng.uniform(size=n) * 1e-300
         w[n // 2:] *= 1e290
@@ -312,3 +317,14 @@ def test_cdf_scan_bit_exact(K, kind):
     ref_cdf = ref.resample_cdf(w)
     got = host(K.resample_cdf(dev(w)))
     np.testing.assert_array_equal(got, ref_cdf)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1023, 1024, 1025, 4097, 2049 * 1024 + 5])
+def test_cdf_scan_sizes(K, n):
+    """Tile edges of the tiled exact scan (1024-element tiles, 2048 tile
+    records per chain batch)."""
+    rng = np.random.default_rng(n)
+    w = rng.uniform(0.5, 1.5, size=n)
+    w /= w.sum()
+    np.testing.assert_array_equal(host(K.resample_cdf(dev(w))),
+                                  ref.resample_cdf(w))

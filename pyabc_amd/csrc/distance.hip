@@ -29,6 +29,7 @@ __global__ __launch_bounds__(256) void pnorm_kernel(
     const double* __restrict__ x0, const double* __restrict__ fw, int64_t B,
     int S, double p, double eps, double* __restrict__ d_out,
     uint8_t* __restrict__ accept, uint8_t* __restrict__ guard) {
+#pragma clang fp contract(off)  // t*t then +, separately rounded (ref. pow, sum)
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double acc = 0.0;

@@ -6,13 +6,11 @@
 //   pdf:  sum_n w_n exp(-q_n/2) / sqrt((2 pi)^d det_n) / sum w,
 //         q_n = (theta - X_n)^T inv_n (theta - X_n)                   (:103-110)
 //
-// kNN: fp64 squared distances (sequential over dimensions, no FMA
-// contraction, as the reference tree computes them), one WAVE per group of
-// R rows; candidate tiles of X are staged in LDS and shared by the block's
-// waves; every lane tests one candidate against the R rows and appends it to
-// the row's LDS buffer when it beats the row's current k-th distance tau;
-// a full buffer is bitonic-sorted by the wave and cut back to k (tau shrinks),
-// so the kernel makes ONE pass over the candidates.  k <= kMaxK.
+// kNN: one wave per 8 rows streams every candidate through a provably safe
+// packed-fp32 filter; passing candidates' indices go to a per-row LDS
+// buffer that is re-ranked by EXACT fp64 squared distance (sequential over
+// dimensions, no FMA contraction, as the reference tree computes them) in
+// registers and cut back to k, setting the pruning threshold tau.
 // cov/det/inv: one thread per particle, weighted moments of the k neighbour
 // deltas, LU with partial pivoting for det and inverse (fp64).
 // pdf: one thread per evaluation point; the previous population's
@@ -24,137 +22,263 @@
 
 namespace abc {
 
-constexpr int kKnnRows = 8;     // rows per wave
-constexpr int kKnnWaves = 4;    // waves per block
-constexpr int kKnnCap = 256;    // buffer capacity per row (power of two)
-constexpr int kMaxK = kKnnCap - 64;
-constexpr int kKnnTile = 256;   // candidates staged per LDS tile
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-__device__ inline double dsub(double a, double b) { return __dsub_rn(a, b); }
-__device__ inline double dadd(double a, double b) { return __dadd_rn(a, b); }
-__device__ inline double dmul(double a, double b) { return __dmul_rn(a, b); }
+constexpr int kKnnRows = 8;     // rows per wave (one wave per block)
+constexpr int kMaxK = 192;      // buffer of 256 = k kept + 64 appended
 
-// bitonic sort (ascending by d2, ties by index) of one row buffer by a wave
-__device__ inline void wave_bitonic(double* bd, int* bi, int lane) {
-  for (int size = 2; size <= kKnnCap; size <<= 1) {
+// Separately rounded fp64 ops: hipcc contracts a*b+c into an FMA by default
+// (-ffp-contract=fast, and __dmul_rn/__dadd_rn are plain operators), so the
+// pragma keeps the reference's sub / mul / add sequence.
+__device__ inline double dsub(double a, double b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+__device__ inline double dadd(double a, double b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ inline double dmul(double a, double b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+
+// fp32 filter of the kNN candidate test.  Coordinates are centred on X[0]
+// and rounded to fp32 once (knn_prep_kernel, A = max |x - x0| in fp64); the
+// filter distance d2f = sum fl32(xf_j - xf_i)^2 then satisfies
+//   |d2f - d2| <= (d+2) 2^-24 d2 + 2^-22 A sqrt(d d2)
+// so  d2 < tau  =>  d2f < T(tau) = tau (1 + (d+4) 2^-22) + 2^-20 A sqrt(d tau)
+// (both terms 4x the bound), rounded up to fp32.  Only lanes passing the
+// filter compute the exact fp64 distance (the reference's sub/mul/add
+// sequence) and take the exact test d2 < tau, so the neighbour sets, their
+// order and their distances are exactly those of the all-fp64 scan.
+__device__ inline float knn_filter_bound(double tau, int d, double A) {
+  if (!(tau < INFINITY)) return INFINITY;
+  const double T = tau * (1.0 + (d + 4) * 0x1p-22) +
+                   0x1p-20 * A * sqrt(static_cast<double>(d) * tau) + 1e-300;
+  return __double2float_ru(T);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void knn_prep_kernel(
+    const double* __restrict__ X, int64_t N, float* __restrict__ Xf,
+    unsigned long long* __restrict__ amax) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  double m = 0.0;
+  if (i < N) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const double v = X[i * D + q] - X[q];
+      Xf[i * D + q] = static_cast<float>(v);
+      m = fmax(m, fabs(v));
+    }
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(amax, static_cast<unsigned long long>(__double_as_longlong(m)));
+}
+
+// (d2, idx) lexicographic order, ascending; the reference breaks no ties
+// (tie-free inputs), the index order makes the result deterministic
+__device__ inline bool knn_less(double a, int ia, double b, int ib) {
+  return a < b || (a == b && ia < ib);
+}
+
+// Bitonic sort of H*64 (d2, idx) pairs held in registers, element
+// i = h*64 + lane: strides < 64 exchange across lanes (shuffles), stride >= 64
+// within a lane.
+template <int H>
+__device__ inline void reg_bitonic(double (&v)[H], int (&ix)[H], int lane) {
+#pragma unroll
+  for (int size = 2; size <= H * 64; size <<= 1) {
+#pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = lane; t < kKnnCap / 2; t += 64) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const double a = bd[lo], b = bd[hi];
-        const int ia = bi[lo], ib = bi[hi];
-        const bool gt = (a > b) || (a == b && ia > ib);
-        if (gt == up) {
-          bd[lo] = b;
-          bd[hi] = a;
-          bi[lo] = ib;
-          bi[hi] = ia;
+      if (stride >= 64) {
+        const int hs = stride / 64;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          if (h & hs) continue;
+          const int i = h * 64 + lane;
+          const bool up = (i & size) == 0;
+          const int g = h | hs;
+          const bool gt = knn_less(v[g], ix[g], v[h], ix[h]);
+          if (gt == up) {
+            const double tv = v[h];
+            v[h] = v[g];
+            v[g] = tv;
+            const int ti = ix[h];
+            ix[h] = ix[g];
+            ix[g] = ti;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const int i = h * 64 + lane;
+          const bool up = (i & size) == 0;
+          const bool lower = (lane & stride) == 0;
+          const double pv = __shfl_xor(v[h], stride, 64);
+          const int pi = __shfl_xor(ix[h], stride, 64);
+          // the lower element keeps the min when ascending
+          const bool p_less = knn_less(pv, pi, v[h], ix[h]);
+          const bool take = (lower == up) ? p_less : !p_less;
+          if (take) {
+            v[h] = pv;
+            ix[h] = pi;
+          }
         }
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
   }
 }
 
+// Exact fp64 squared distance (the reference's sequential sub/mul/add).
 template <int D>
-__global__ __launch_bounds__(256) void knn_kernel(const double* __restrict__ X,
-                                                  int64_t N, int k,
-                                                  int32_t* __restrict__ nbr,
-                                                  double* __restrict__ nbr_d2) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* tile = reinterpret_cast<double*>(smem);                 // [kKnnTile][D]
-  double* bufd = tile + kKnnTile * D;                              // [rows][cap]
-  int* bufi = reinterpret_cast<int*>(bufd + kKnnWaves * kKnnRows * kKnnCap);
-  int* bufn = bufi + kKnnWaves * kKnnRows * kKnnCap;               // [rows]
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kKnnWaves + wid) * kKnnRows;
-
-  double xr[kKnnRows][D];
-  double tau[kKnnRows];
+__device__ inline double knn_exact_d2(const double* __restrict__ X, int64_t i,
+                                      int64_t j) {
+  double d2 = 0.0;
 #pragma unroll
-  for (int r = 0; r < kKnnRows; ++r) {
-    const int64_t row = row0 + r < N ? row0 + r : N - 1;
-#pragma unroll
-    for (int q = 0; q < D; ++q) xr[r][q] = X[row * D + q];
-    tau[r] = INFINITY;
+  for (int q = 0; q < D; ++q) {
+    const double df = dsub(X[j * D + q], X[i * D + q]);
+    d2 = dadd(d2, dmul(df, df));
   }
-  double* myd = bufd + wid * kKnnRows * kKnnCap;
-  int* myi = bufi + wid * kKnnRows * kKnnCap;
-  int* myn = bufn + wid * kKnnRows;
-  if (lane < kKnnRows) myn[lane] = 0;
-  __builtin_amdgcn_wave_barrier();
+  return d2;
+}
 
-  for (int64_t base = 0; base < N; base += kKnnTile) {
-    __syncthreads();
-    for (int t = threadIdx.x; t < kKnnTile * D; t += 256) {
-      const int64_t j = base + t / D;
-      tile[t] = j < N ? X[base * D + t] : 0.0;
+// Sort one row's candidate buffer (cnt indices) by exact distance; keep the
+// first k (written back), return tau = the k-th exact distance; with out
+// pointers, write the final neighbours instead.
+template <int D, int H>
+__device__ inline double knn_sort_cut(const double* __restrict__ X,
+                                      int64_t row, int* __restrict__ buf,
+                                      int cnt, int k, int lane,
+                                      int32_t* __restrict__ out_idx,
+                                      double* __restrict__ out_d2) {
+  double v[H];
+  int ix[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const int i = h * 64 + lane;
+    if (i < cnt) {
+      ix[h] = buf[i];
+      v[h] = knn_exact_d2<D>(X, row, ix[h]);
+    } else {
+      ix[h] = 0x7fffffff;
+      v[h] = INFINITY;
     }
-    __syncthreads();
-    for (int c0 = 0; c0 < kKnnTile; c0 += 64) {
-      const int64_t j = base + c0 + lane;
-      const bool valid = j < N;
-      double xj[D];
+  }
+  reg_bitonic<H>(v, ix, lane);
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int q = 0; q < D; ++q) xj[q] = tile[(c0 + lane) * D + q];
-#pragma unroll
-      for (int r = 0; r < kKnnRows; ++r) {
-        double d2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-          const double df = dsub(xj[q], xr[r][q]);
-          d2 = dadd(d2, dmul(df, df));
-        }
-        const bool take = valid && j != row0 + r && d2 < tau[r];
-        const uint64_t m = __ballot(take);
-        if (m) {
-          int cnt = myn[r];
-          if (cnt + __popcll(m) > kKnnCap) {
-            // sort + cut back to k, shrinking tau; pad with +inf
-            for (int t = cnt + lane; t < kKnnCap; t += 64) {
-              myd[r * kKnnCap + t] = INFINITY;
-              myi[r * kKnnCap + t] = 0x7fffffff;
-            }
-            __builtin_amdgcn_wave_barrier();
-            wave_bitonic(myd + r * kKnnCap, myi + r * kKnnCap, lane);
-            cnt = k;
-            tau[r] = myd[r * kKnnCap + k - 1];
-            if (lane == 0) myn[r] = k;
-            __builtin_amdgcn_wave_barrier();
-          }
-          const bool take2 = take && d2 < tau[r];
-          const uint64_t m2 = __ballot(take2);
-          const int pos = cnt + __popcll(m2 & ((1ull << lane) - 1ull));
-          if (take2) {
-            myd[r * kKnnCap + pos] = d2;
-            myi[r * kKnnCap + pos] = static_cast<int>(j);
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (lane == 0) myn[r] = cnt + __popcll(m2);
-          __builtin_amdgcn_wave_barrier();
-        }
+  for (int h = 0; h < H; ++h) {
+    const int i = h * 64 + lane;
+    if (i < k) {
+      if (out_idx) {
+        out_idx[i] = ix[h];
+        if (out_d2) out_d2[i] = v[h];
+      } else {
+        buf[i] = ix[h];
       }
     }
   }
-  // final selection
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int hk = (k - 1) / 64, lk = (k - 1) % 64;
+  double tk = 0.0;
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+    if (h == hk) tk = v[h];
+  return __shfl(tk, lk, 64);
+}
+
+// One wave per kNN_ROWS rows, no block barriers: every lane streams one
+// candidate per step (fp32 centred coordinates, prefetched one step ahead)
+// against the wave's rows (packed-fp32 pairs in VGPRs); lanes passing the
+// fp32 filter append the candidate INDEX to the row's LDS buffer; a full
+// buffer is re-ranked by exact fp64 distance in registers (reg_bitonic) and
+// cut back to k, which sets tau.  Buffers hold indices only (H*64*4 B per
+// row), so many waves fit per CU.
+template <int D, int H>
+__global__ __launch_bounds__(64) void knn_kernel(
+    const double* __restrict__ X, const float* __restrict__ Xf,
+    const unsigned long long* __restrict__ amax, int64_t N, int k,
+    int32_t* __restrict__ nbr, double* __restrict__ nbr_d2) {
+  constexpr int CAP = H * 64;
+  __shared__ int buf[kKnnRows][CAP];
+  const int lane = threadIdx.x;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kKnnRows;
+  const double A = __longlong_as_double(static_cast<long long>(*amax));
+
+  f32x2 xrf[kKnnRows / 2][D];   // rows in pairs for packed fp32 math
+#pragma unroll
+  for (int p = 0; p < kKnnRows / 2; ++p) {
+    const int64_t ra = row0 + 2 * p < N ? row0 + 2 * p : N - 1;
+    const int64_t rb = row0 + 2 * p + 1 < N ? row0 + 2 * p + 1 : N - 1;
+#pragma unroll
+    for (int q = 0; q < D; ++q) xrf[p][q] = f32x2{Xf[ra * D + q], Xf[rb * D + q]};
+  }
+  float Tf[kKnnRows];
+  int cnt[kKnnRows];
+#pragma unroll
+  for (int r = 0; r < kKnnRows; ++r) {
+    Tf[r] = INFINITY;
+    cnt[r] = 0;
+  }
+  float nx[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) nx[q] = lane < N ? Xf[lane * D + q] : 0.f;
+
+  for (int64_t base = 0; base < N; base += 64) {
+    const int64_t j = base + lane;
+    const bool valid = j < N;
+    float xj[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xj[q] = nx[q];
+    const int64_t jn = j + 64;
+    if (jn < N) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) nx[q] = Xf[jn * D + q];
+    }
+    float d2f[kKnnRows];
+#pragma unroll
+    for (int p = 0; p < kKnnRows / 2; ++p) {
+      f32x2 acc = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        const f32x2 df = xrf[p][q] - f32x2{xj[q], xj[q]};
+        acc = __builtin_elementwise_fma(df, df, acc);
+      }
+      d2f[2 * p] = acc.x;
+      d2f[2 * p + 1] = acc.y;
+    }
+#pragma unroll
+    for (int r = 0; r < kKnnRows; ++r) {
+      const int64_t row = row0 + r;
+      bool cand = valid && j != row && row < N &&
+                  (d2f[r] < Tf[r] || Tf[r] == INFINITY);
+      uint64_t m = __ballot(cand);
+      if (!m) continue;
+      if (cnt[r] + __popcll(m) > CAP) {
+        const double tau = knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane,
+                                              nullptr, nullptr);
+        cnt[r] = k;
+        Tf[r] = knn_filter_bound(tau, D, A);
+        cand = cand && d2f[r] < Tf[r];
+        m = __ballot(cand);
+      }
+      if (cand) buf[r][cnt[r] + __popcll(m & ((1ull << lane) - 1ull))] =
+          static_cast<int>(j);
+      cnt[r] += __popcll(m);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
   for (int r = 0; r < kKnnRows; ++r) {
     const int64_t row = row0 + r;
-    const int cnt = myn[r];
-    for (int t = cnt + lane; t < kKnnCap; t += 64) {
-      myd[r * kKnnCap + t] = INFINITY;
-      myi[r * kKnnCap + t] = 0x7fffffff;
-    }
-    __builtin_amdgcn_wave_barrier();
-    wave_bitonic(myd + r * kKnnCap, myi + r * kKnnCap, lane);
-    if (row < N) {
-      for (int t = lane; t < k; t += 64) {
-        nbr[row * k + t] = myi[r * kKnnCap + t];
-        if (nbr_d2) nbr_d2[row * k + t] = myd[r * kKnnCap + t];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+    if (row < N)
+      knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane, nbr + row * k,
+                         nbr_d2 ? nbr_d2 + row * k : nullptr);
   }
 }
 
@@ -447,24 +571,33 @@ int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
 }
 
 size_t abc_knn_workspace_bytes(int64_t N, int k) {
-  (void)N;
   (void)k;
-  return 0;
+  // fp32 centred coordinates [N][8] + the coordinate bound A
+  return static_cast<size_t>(N > 0 ? N : 1) * 8 * 4 + 256;
 }
 
 int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
                 double* nbr_d2, void* ws, size_t ws_bytes, hipStream_t st) {
-  (void)ws;
-  (void)ws_bytes;
   ABC_REQUIRE(N > 1 && k >= 1 && k <= N - 1, "knn: need 1 <= k <= N-1");
   ABC_REQUIRE(k <= kMaxK, "knn: k=%d exceeds the one-pass limit %d", k, kMaxK);
-  const unsigned grid = static_cast<unsigned>(ceil_div(N, kKnnRows * kKnnWaves));
-  const int rows = kKnnWaves * kKnnRows;
-#define L(DD)                                                                  \
-  {                                                                            \
-    const size_t lds = kKnnTile * DD * 8 + rows * kKnnCap * 12 + rows * 4;     \
-    hipLaunchKernelGGL((knn_kernel<DD>), dim3(grid), dim3(256), lds, st, X, N, \
-                       k, nbr, nbr_d2);                                        \
+  ABC_REQUIRE(N < (1ll << 31), "knn: N must fit int32 indices");
+  ABC_REQUIRE(X && nbr && ws, "knn: null pointer");
+  ABC_REQUIRE(ws_bytes >= abc_knn_workspace_bytes(N, k), "knn: workspace too small");
+  unsigned long long* amax = static_cast<unsigned long long*>(ws);
+  float* Xf = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
+  ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
+  const unsigned pg = static_cast<unsigned>(ceil_div(N, 256));
+  const unsigned grid = static_cast<unsigned>(ceil_div(N, kKnnRows));
+#define L(DD)                                                                   \
+  {                                                                             \
+    hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(pg), dim3(256), 0, st, X, N, \
+                       Xf, amax);                                               \
+    if (k <= 64)                                                                \
+      hipLaunchKernelGGL((knn_kernel<DD, 2>), dim3(grid), dim3(64), 0, st, X,   \
+                         Xf, amax, N, k, nbr, nbr_d2);                          \
+    else                                                                        \
+      hipLaunchKernelGGL((knn_kernel<DD, 4>), dim3(grid), dim3(64), 0, st, X,   \
+                         Xf, amax, N, k, nbr, nbr_d2);                          \
   }
   switch (d) {
     case 1: L(1) break;

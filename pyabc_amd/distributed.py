@@ -58,17 +58,17 @@ class Comm:
         if self.active:
             dist.barrier()
 
-    def all_gather_rows(self, t):
+    def all_gather_rows(self, t, sizes=None):
         """Concatenate each rank's rows (possibly different counts) in rank
-        order."""
+        order.  ``sizes`` (every rank's row count, when the caller knows
+        them) saves the count exchange."""
         if not self.active:
             return t
         if self._host_staged and t.is_cuda:
-            return self.all_gather_rows(t.cpu()).to(t.device)
-        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-        sizes = [torch.zeros_like(n) for _ in range(self.world)]
-        dist.all_gather(sizes, n)
-        sizes = [int(s.item()) for s in sizes]
+            return self.all_gather_rows(t.cpu(), sizes).to(t.device)
+        if sizes is None:
+            sizes = self.all_gather_ints(t.shape[0])
+        assert sizes[self.rank] == t.shape[0], "all_gather_rows: bad sizes"
         mx = max(sizes)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
@@ -91,7 +91,7 @@ class Comm:
             else torch.tensor([int(v)], dtype=torch.int64, device=dev)
         bufs = [torch.empty_like(x) for _ in range(self.world)]
         dist.all_gather(bufs, x)
-        return [int(b.item()) for b in bufs]
+        return [int(a) for a in torch.cat(bufs).cpu().tolist()]   # one sync
 
     def all_gather_int_lists(self, vals):
         """Every rank's equal-length int list, indexed [rank][k]."""
@@ -101,7 +101,7 @@ class Comm:
         x = torch.tensor(list(vals), dtype=torch.int64, device=dev)
         bufs = [torch.empty_like(x) for _ in range(self.world)]
         dist.all_gather(bufs, x)
-        return [[int(a) for a in b.cpu().tolist()] for b in bufs]
+        return torch.stack(bufs).cpu().tolist()                    # one sync
 
     def all_reduce_ints(self, vals):
         """Element-wise sum over ranks of an int list (one collective)."""

@@ -143,7 +143,7 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     R = comm.world
     if R == 1:
         return local
-    allr = comm.all_gather_rows(local)
+    allr = comm.all_gather_rows(local, [sum(c) for c in counts])
     starts = [0]
     for s in range(R):
         starts.append(starts[-1] + sum(counts[s]))
@@ -201,12 +201,16 @@ class GenerationEngine:
         lo, hi = self.row_range(n)
         return hi - lo
 
-    def row_range(self, n):
-        """[lo, hi) of the balanced contiguous row split of n rows."""
-        R, r = self.comm.world, self.comm.rank
+    def row_ranges(self, n):
+        """[lo, hi) of every rank in the balanced contiguous split of n."""
+        R = self.comm.world
         q, m = divmod(n, R)
-        lo = r * q + min(r, m)
-        return lo, lo + q + (1 if r < m else 0)
+        return [(r * q + min(r, m), r * q + min(r, m) + q + (1 if r < m else 0))
+                for r in range(R)]
+
+    def row_range(self, n):
+        """[lo, hi) of this rank's rows."""
+        return self.row_ranges(n)[self.comm.rank]
 
     # ------------------------------------------------------------------
     def sample_prior(self, t, n):
@@ -367,7 +371,8 @@ class GenerationEngine:
                 self.kde_events.append((e0, e1, hi - lo, fit.n))
             else:
                 lp = fit.logpdf(mine)
-            logpd = comm.all_gather_rows(lp)
+            logpd = comm.all_gather_rows(
+                lp, [b - a for a, b in self.row_ranges(theta_acc.shape[0])])
             w = K.importance_weights(logpd, None, self.prior_pd)
         torch.cuda.synchronize()
         tm["kde"] = time.perf_counter() - t1

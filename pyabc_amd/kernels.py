@@ -313,7 +313,9 @@ def knn(X, k):
     N, d = X.shape
     nbr = torch.empty((N, k), dtype=torch.int32, device=_dev())
     d2 = torch.empty((N, k), dtype=F64, device=_dev())
-    call("abc_knn_f64", ptr(X), N, d, k, ptr(nbr), ptr(d2), None, 0,
+    wsb = nat.lib().abc_knn_workspace_bytes(N, k)
+    ws = WS.get(wsb, "knn")
+    call("abc_knn_f64", ptr(X), N, d, k, ptr(nbr), ptr(d2), ptr(ws), wsb,
          nat.stream())
     return nbr, d2
 

@@ -328,3 +328,37 @@ def test_cdf_scan_sizes(K, n):
     w /= w.sum()
     np.testing.assert_array_equal(host(K.resample_cdf(dev(w))),
                                   ref.resample_cdf(w))
+
+
+@pytest.mark.parametrize("case", ["offset", "clustered", "d1", "d8"])
+def test_knn_fp32_filter_exact(K, case):
+    """The fp32 candidate filter never drops a true neighbour: sets, order
+    and distances equal an fp64 brute force (the reference's sub/mul/add
+    sequence) on data far from the origin (large fp32 rounding of the
+    centred coordinates), near-duplicate clusters and d = 1 / 8."""
+    rng = np.random.default_rng({"offset": 1, "clustered": 2, "d1": 3,
+                                 "d8": 4}[case])
+    n, d, k = 3000, 6, 50
+    if case == "offset":
+        X = rng.normal(size=(n, d)) * 1e-3 + 1e3
+        X[0] -= 5e3                         # x0 far away: large bound A
+    elif case == "clustered":
+        X = np.repeat(rng.normal(size=(n // 30, d)), 30, axis=0)
+        X += rng.normal(size=X.shape) * 1e-7
+    elif case == "d1":
+        d = 1
+        X = rng.uniform(size=(n, d))
+    else:
+        d = 8
+        X = rng.normal(size=(n, d))
+    nbr, d2 = K.knn(dev(X), k)
+    nbr, d2 = host(nbr), host(d2)
+    diff = X[None, :, :] - X[:, None, :]
+    D2 = np.zeros((n, n))
+    for q in range(d):                        # sequential, no FMA
+        D2 = D2 + diff[:, :, q] * diff[:, :, q]
+    np.fill_diagonal(D2, np.inf)
+    order = np.lexsort((np.broadcast_to(np.arange(n), (n, n)), D2), axis=1)
+    want = order[:, :k]
+    np.testing.assert_array_equal(nbr, want)
+    np.testing.assert_array_equal(d2, np.take_along_axis(D2, want, axis=1))

@@ -162,7 +162,7 @@ def main():
     w4 /= w4.sum()
     nbr, _ = K.knn(X4, k4)
     t = timed(lambda: K.knn(X4, k4), reps=2)
-    report("knn_f64", t, N4 * N4, "pairs", 3 * d4, "valu_f64",
+    report("knn_f64", t, N4 * N4, "pairs", 3 * d4, "valu_f32",
            {"N": N4, "d": d4, "k": k4})
     covs, invs, dets = K.local_cov(X4, w4, nbr)
     t = timed(lambda: K.local_cov(X4, w4, nbr))

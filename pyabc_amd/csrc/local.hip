@@ -14,9 +14,9 @@
 // cov/det/inv: one thread per particle, weighted moments of the k neighbour
 // deltas, LU with partial pivoting for det and inverse (fp64).
 // pdf: one thread per evaluation point; the previous population's
-// (X_n, inv_n, log(w_n / norm_n)) stream through the scalar path (wave-
-// uniform), d^2 FMAs per pair for the quadratic form, online log-sum-exp
-// in fp64.
+// (X_n, packed symmetric inv_n, log(w_n / norm_n)) stream through the scalar
+// path (wave-uniform), d(d+1)/2 + d FMAs per pair for the quadratic form,
+// fp64 terms under one global offset, exact fixup for underflowing rows.
 #include "common.hpp"
 #include "philox.hpp"
 
@@ -409,30 +409,76 @@ __global__ __launch_bounds__(128) void local_cov_kernel(
   dets[n] = det;
 }
 
-// per-previous-particle constant: lc_n = log(w_n) - 0.5 (d log 2pi + log det_n)
-__global__ __launch_bounds__(256) void local_const_kernel(const double* __restrict__ w,
-                                                          const double* __restrict__ dets,
-                                                          int64_t N, int d,
-                                                          double* __restrict__ lc) {
+// per-previous-particle constants: lc_n = log(w_n / sqrt((2 pi)^d det_n)),
+// the global offset L = max_n lc_n (ordered-key atomic max), and the
+// symmetric quadratic-form coefficients of inv_n packed row by row:
+// (A_aa, A_ab + A_ba for b > a), d(d+1)/2 per particle.
+__global__ __launch_bounds__(256) void local_const_kernel(
+    const double* __restrict__ w, const double* __restrict__ dets,
+    const double* __restrict__ invs, int64_t N, int d,
+    double* __restrict__ lc, double* __restrict__ coef,
+    unsigned long long* __restrict__ lc_max_key) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (n >= N) return;
-  const double norm = sqrt(pow(2.0 * 3.141592653589793, d) * dets[n]);
-  lc[n] = w[n] > 0.0 ? log(w[n] / norm) : -INFINITY;
+  uint64_t key = 0;
+  if (n < N) {
+    const double norm = sqrt(pow(2.0 * 3.141592653589793, d) * dets[n]);
+    const double v = w[n] > 0.0 ? log(w[n] / norm) : -INFINITY;
+    lc[n] = v;
+    if (v == v) key = f64_key(v);
+    const double* A = invs + n * d * d;
+    double* c = coef + n * (d * (d + 1) / 2);
+    int t = 0;
+    for (int a = 0; a < d; ++a) {
+      c[t++] = A[a * d + a];
+      for (int b = a + 1; b < d; ++b) c[t++] = A[a * d + b] + A[b * d + a];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t u = __shfl_xor(key, o, 64);
+    key = u > key ? u : key;
+  }
+  if ((threadIdx.x & 63) == 0 && key)
+    atomicMax(lc_max_key, static_cast<unsigned long long>(key));
 }
 
+// q = (theta - X_n)^T inv_n (theta - X_n) from the packed symmetric form
+// (d(d+1)/2 + d FMAs instead of d^2 + d)
+template <int D>
+__device__ inline double local_qform(const double (&dl)[D],
+                                     const double* __restrict__ c) {
+  double q = 0.0;
+  int t = 0;
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    double r = c[t++] * dl[a];
+#pragma unroll
+    for (int b = a + 1; b < D; ++b) r = fma(c[t++], dl[b], r);
+    q = fma(dl[a], r, q);
+  }
+  return q;
+}
+
+// Main pass: one thread per evaluation point, the previous population's
+// (X_n, coef_n, lc_n) streaming through the scalar path (wave-uniform n).
+// Terms are exp(lc_n - q_n/2 - L) <= 1 (q >= 0), summed in fp64 without a
+// running max; the n-range is cut into a fixed number of chunks (a function
+// of N only) whose partial sums are added in fixed order.
 template <int D>
 __global__ __launch_bounds__(256) void local_pdf_kernel(
     const double* __restrict__ pts, int64_t M, const double* __restrict__ X,
-    const double* __restrict__ invs, const double* __restrict__ lc, int64_t N,
-    int split, int64_t nchunk, double* __restrict__ part_m,
-    double* __restrict__ part_s) {
+    const double* __restrict__ coef, const double* __restrict__ lc,
+    const unsigned long long* __restrict__ lc_max_key, int64_t N, int split,
+    int64_t nchunk, double* __restrict__ part) {
+  constexpr int NC = D * (D + 1) / 2;
   const int s = blockIdx.x % split;
   const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
   const int64_t i = i0 < M ? i0 : M - 1;
+  const double L = key_f64(*lc_max_key);
   double th[D];
 #pragma unroll
   for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
-  double m = -INFINITY, acc = 0.0;
+  double acc = 0.0;
   const int64_t n0 = static_cast<int64_t>(s) * nchunk;
   int64_t n1 = n0 + nchunk;
   if (n1 > N) n1 = N;
@@ -440,44 +486,69 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
     double dl[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
-    double qf = 0.0;
-    const double* A = invs + n * D * D;
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-      double r = 0.0;
-#pragma unroll
-      for (int b = 0; b < D; ++b) r = fma(A[a * D + b], dl[b], r);
-      qf = fma(dl[a], r, qf);
-    }
-    const double e = lc[n] - 0.5 * qf;
-    if (e > m) {
-      acc = acc * exp(m - e) + 1.0;
-      m = e;
-    } else {
-      acc += exp(e - m);
-    }
+    const double qf = local_qform<D>(dl, coef + n * NC);
+    acc += exp(fma(-0.5, qf, lc[n] - L));
   }
-  if (i0 < M) {
-    part_m[static_cast<int64_t>(s) * M + i0] = m;
-    part_s[static_cast<int64_t>(s) * M + i0] = acc;
-  }
+  if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
 }
 
 __global__ __launch_bounds__(256) void local_pdf_final_kernel(
-    const double* __restrict__ part_m, const double* __restrict__ part_s,
-    int64_t M, int split, const double* __restrict__ logsumw,
-    double* __restrict__ out) {
+    const double* __restrict__ part, int64_t M, int split,
+    const unsigned long long* __restrict__ lc_max_key,
+    const double* __restrict__ logsumw, double* __restrict__ out,
+    int* __restrict__ n_fix, int* __restrict__ fix_rows) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= M) return;
-  double m = -INFINITY;
-  for (int s = 0; s < split; ++s) m = fmax(m, part_m[s * M + i]);
-  double acc = 0.0;
-  if (m > -INFINITY)
-    for (int s = 0; s < split; ++s) {
-      const double ms = part_m[s * M + i];
-      if (ms > -INFINITY) acc += part_s[s * M + i] * exp(ms - m);
+  double S = 0.0;
+  for (int s = 0; s < split; ++s) S += part[s * M + i];
+  if (S >= 1e-280) {
+    out[i] = key_f64(*lc_max_key) + log(S) - *logsumw;
+  } else {  // the fixed offset underflowed: exact two-pass evaluation
+    fix_rows[atomicAdd(n_fix, 1)] = static_cast<int>(i);
+    out[i] = -INFINITY;
+  }
+}
+
+// exact max-then-sum for rows whose fixed-offset sum underflowed
+template <int D>
+__global__ __launch_bounds__(256) void local_pdf_fixup_kernel(
+    const double* __restrict__ pts, const double* __restrict__ X,
+    const double* __restrict__ coef, const double* __restrict__ lc, int64_t N,
+    const double* __restrict__ logsumw, const int* __restrict__ n_fix,
+    const int* __restrict__ fix_rows, double* __restrict__ out) {
+  constexpr int NC = D * (D + 1) / 2;
+  __shared__ double red[4];
+  const int count = *n_fix;
+  for (int f = blockIdx.x; f < count; f += gridDim.x) {
+    const int64_t i = fix_rows[f];
+    double th[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
+    double m = -INFINITY;
+    for (int64_t n = threadIdx.x; n < N; n += 256) {
+      double dl[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
+      m = fmax(m, fma(-0.5, local_qform<D>(dl, coef + n * NC), lc[n]));
     }
-  out[i] = (m > -INFINITY ? m + log(acc) : -INFINITY) - *logsumw;
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    double sum = 0.0;
+    if (m > -INFINITY)
+      for (int64_t n = threadIdx.x; n < N; n += 256) {
+        double dl[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
+        sum += exp(fma(-0.5, local_qform<D>(dl, coef + n * NC), lc[n]) - m);
+      }
+    sum = block_sum<double, 256>(sum, red);
+    if (threadIdx.x == 0)
+      out[i] = (m > -INFINITY ? m + log(sum) : -INFINITY) - *logsumw;
+    __syncthreads();
+  }
 }
 
 
@@ -655,7 +726,10 @@ size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N) {
   int split;
   int64_t nchunk;
   local_plan(M > 0 ? M : 1, N > 0 ? N : 1, split, nchunk);
-  return static_cast<size_t>(N) * 8 + static_cast<size_t>(split) * M * 16 + 512;
+  // logsumw, lc_max_key, n_fix (64 B) | lc[N] | coef[N][36] (d <= 8)
+  // | part[split][M] | fix_rows[M]
+  return 64 + static_cast<size_t>(N) * 8 * 37 +
+         static_cast<size_t>(split) * M * 8 + static_cast<size_t>(M) * 4 + 512;
 }
 
 __global__ __launch_bounds__(256) void local_sumw_kernel(const double* __restrict__ w,
@@ -675,6 +749,9 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
                          hipStream_t st) {
   ABC_REQUIRE(M >= 0 && N >= 1, "local_logpdf: bad sizes");
   if (M == 0) return kOk;
+  ABC_REQUIRE(d >= 1 && d <= 8, "local_logpdf: unsupported d=%d (d <= 8)", d);
+  ABC_REQUIRE(pts && X && w && inv_covs && dets && out_logpdf && ws,
+              "local_logpdf: null pointer");
   ABC_REQUIRE(ws_bytes >= abc_local_logpdf_workspace_bytes(M, N),
               "local_logpdf: workspace too small");
   int split;
@@ -682,16 +759,25 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
   local_plan(M, N, split, nchunk);
   char* base = static_cast<char*>(ws);
   double* logsumw = reinterpret_cast<double*>(base);
-  double* lc = logsumw + 8;
-  double* part_m = lc + N;
-  double* part_s = part_m + static_cast<int64_t>(split) * M;
+  unsigned long long* lc_max_key = reinterpret_cast<unsigned long long*>(base + 8);
+  int* n_fix = reinterpret_cast<int*>(base + 16);
+  double* lc = reinterpret_cast<double*>(base + 64);
+  double* coef = lc + N;
+  double* part = coef + N * 36;
+  int* fix_rows = reinterpret_cast<int*>(part + static_cast<int64_t>(split) * M);
+  ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
   hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
   hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
-                     st, w, dets, N, d, lc);
+                     st, w, dets, inv_covs, N, d, lc, coef, lc_max_key);
   const unsigned grid = static_cast<unsigned>(ceil_div(M, 256) * split);
-#define L(DD)                                                                  \
-  hipLaunchKernelGGL((local_pdf_kernel<DD>), dim3(grid), dim3(256), 0, st, pts, \
-                     M, X, inv_covs, lc, N, split, nchunk, part_m, part_s);
+#define L(DD)                                                                   \
+  hipLaunchKernelGGL((local_pdf_kernel<DD>), dim3(grid), dim3(256), 0, st, pts,  \
+                     M, X, coef, lc, lc_max_key, N, split, nchunk, part);       \
+  hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256), \
+                     0, st, part, M, split, lc_max_key, logsumw, out_logpdf,    \
+                     n_fix, fix_rows);                                          \
+  hipLaunchKernelGGL((local_pdf_fixup_kernel<DD>), dim3(64), dim3(256), 0, st,  \
+                     pts, X, coef, lc, N, logsumw, n_fix, fix_rows, out_logpdf);
   switch (d) {
     case 1: L(1) break;
     case 2: L(2) break;
@@ -701,13 +787,8 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
     case 6: L(6) break;
     case 7: L(7) break;
     case 8: L(8) break;
-    default:
-      set_error("local_logpdf: unsupported d=%d (d <= 8)", d);
-      return kUnsupported;
   }
 #undef L
-  hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),
-                     0, st, part_m, part_s, M, split, logsumw, out_logpdf);
   ABC_LAUNCH_CHECK("local_logpdf kernels");
   return kOk;
 }

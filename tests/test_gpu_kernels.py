@@ -362,3 +362,26 @@ def test_knn_fp32_filter_exact(K, case):
     want = order[:, :k]
     np.testing.assert_array_equal(nbr, want)
     np.testing.assert_array_equal(d2, np.take_along_axis(D2, want, axis=1))
+
+
+def test_local_logpdf_underflow_fixup(K):
+    """Points far from every particle: the fixed-offset sum underflows and
+    the rows go through the exact max-then-sum fixup (log space), matching a
+    numpy log-sum-exp of the same terms; near points take the main pass."""
+    rng = np.random.default_rng(11)
+    n, d, k = 3000, 4, 20
+    X = rng.normal(size=(n, d))
+    w = rng.uniform(0.1, 1.0, size=n)
+    nbr, _ = K.knn(dev(X), k)
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    pts = np.concatenate([rng.normal(size=(5, d)),
+                          np.full((3, d), 25.0) + rng.normal(size=(3, d))])
+    got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
+    inv, det = host(invs), host(dets)
+    diff = pts[:, None, :] - X[None, :, :]
+    q = np.einsum("mna,nab,mnb->mn", diff, inv, diff)
+    e = np.log(w) - 0.5 * q - 0.5 * np.log((2 * np.pi) ** d * det)
+    mx = e.max(axis=1, keepdims=True)
+    want = (mx[:, 0] + np.log(np.exp(e - mx).sum(axis=1))) - np.log(w.sum())
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, want, rtol=1e-11)

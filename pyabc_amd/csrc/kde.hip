@@ -31,6 +31,8 @@
 // and of the launch shape (deterministic, and identical across GPU counts).  Rows whose sum falls
 // below 2^-60 (f32) are re-evaluated by an exact two-pass (max, then sum)
 // fixup kernel, so underflow of the fixed global offset never loses a row.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace abc {
@@ -400,8 +402,13 @@ static Plan make_plan(int64_t M, int64_t npad) {
   constexpr int min_rows = sizeof(T) == 4 ? 2 : 1;  // fp32: one float2 pair
   p.tier = 0;
   while (p.tier < 2 && (R >> (p.tier + 1)) >= min_rows &&
-         ceil_div(M, 256 * (R >> p.tier)) * p.nseg < target_blocks / 2)
+         ceil_div(M, 256 * (R >> p.tier)) * p.nseg < target_blocks)
     ++p.tier;
+  // tuning override (tools/bench_kde.py sweeps): ABC_KDE_TIER=0|1|2
+  if (const char* env = getenv("ABC_KDE_TIER")) {
+    const int t = atoi(env);
+    if (t >= 0 && t <= 2 && (R >> t) >= min_rows) p.tier = t;
+  }
   p.rows_per_thread = R >> p.tier;
   p.row_blocks = ceil_div(M, 256 * p.rows_per_thread);
   int split = 1;

@@ -45,6 +45,20 @@ def run(N, M, d, prec="f32", reps=3):
 
 
 if __name__ == "__main__":
+    import os
+    if len(sys.argv) > 1 and sys.argv[1] == "tiers":
+        # per-rank shapes of the N=1e6 bench at 1/2/4/8 GPUs, every tier
+        for M in [1000000, 500000, 250000, 125000]:
+            for tier in ["0", "1", "2"]:
+                os.environ["ABC_KDE_TIER"] = tier
+                print(f"tier {tier}:", end=" ")
+                run(1000000, M, 8, "f32", reps=2)
+        for M in [100000]:
+            for tier in ["0", "1", "2"]:
+                os.environ["ABC_KDE_TIER"] = tier
+                print(f"tier {tier}:", end=" ")
+                run(100000, M, 4, "f32", reps=3)
+        sys.exit(0)
     for (N, M, d, p) in [(262144, 262144, 8, "f32"), (1000000, 1000000, 8, "f32"),
                          (262144, 262144, 4, "f32"), (262144, 262144, 20, "f32"),
                          (65536, 65536, 8, "f64")]:

@@ -28,9 +28,10 @@
 // SPLIT % 8 == 0 every XCD streams its own j-ranges through its own L2) and
 // write one fp64 partial per segment; the finalize kernel sums the nseg
 // partials in fixed order.  A row's result is therefore independent of M
-// and of the launch shape (deterministic, and identical across GPU counts).  Rows whose sum falls
-// below 2^-60 (f32) are re-evaluated by an exact two-pass (max, then sum)
-// fixup kernel, so underflow of the fixed global offset never loses a row.
+// and of the launch shape (deterministic, and identical across GPU counts).
+// Rows whose sum falls below 2^-60 (f32) are re-evaluated by an exact
+// two-pass (max, then sum) fixup kernel, so underflow of the fixed global
+// offset never loses a row.
 #include <cstdlib>
 
 #include "common.hpp"
@@ -370,13 +371,13 @@ struct RowsPerThread<float, D> {
 };
 
 // The j-range [0, npad) is cut into nseg fixed segments that depend on npad
-// ONLY (a power of two, <= 64, segments of >= ~2048 rows, multiples of CH).
+// ONLY (a power of two, <= 64, segments of >= ~1024 rows, multiples of CH).
 // Every row's density is the fixed-order fp64 sum of its nseg segment sums,
 // each a sequential fp64 sum of 64-pair fp32 chunk sums -- so a row's bits
 // do not depend on M, on the launch shape, or on how many ranks share the
 // rows (multi-GPU results equal single-GPU results bit for bit).
 static int kde_segments(int64_t npad) {
-  const int64_t q = npad / 2048;
+  const int64_t q = npad / 1024;
   int n = 1;
   while (n < 64 && 2 * n <= q) n *= 2;
   return n;

@@ -202,6 +202,52 @@ int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
                               uint64_t seed, uint64_t sid, uint64_t offset,
                               double* out, hipStream_t stream);
 
+/* ---------------- (f3) exact inference: stochastic acceptance -------------
+ * SURVEY 8(f) rank 3.  Replaces, per evaluation b (stat-major stats_T):
+ *   IndependentNormalKernel.__call__  (kind 0, prm = var)  distance/kernel.py:256-282
+ *     pd = -0.5 * (c + np.sum(diff**2 / var))
+ *   IndependentLaplaceKernel.__call__ (kind 1, prm = b)    distance/kernel.py:332-357
+ *     pd = -(c + np.sum(|diff| / b))
+ * with c the kernel's constant np.sum(log 2 [+ log pi] + log prm) (host) and
+ * numpy's pairwise summation order (bit-identical); S <= 4096.  When accept
+ * is non-NULL the StochasticAcceptor decision is fused (SCALE_LOG):
+ *   StochasticAcceptor.__call__                            acceptor/acceptor.py:440-473
+ *     acc = exp((pd - pdf_norm) * inv_temp); accept = acc >= u;
+ *     accw = acc == 0 ? 0 : (apply_iw ? acc / min(1, acc) : 1)
+ * u[b] is injected (u != NULL) or Philox stream (seed, stream) counter
+ * offset + b; guard[b] flags |acc - u| <= 4 ulp. */
+int abc_stochastic_kernel_f64(const double* stats_T, int64_t ld,
+                              const double* x0, const double* prm, int S,
+                              int kind, double c, int64_t B, double* pd,
+                              double pdf_norm, double inv_temp, int apply_iw,
+                              const double* u, uint64_t seed, uint64_t stream,
+                              uint64_t offset, uint8_t* accept, double* accw,
+                              uint8_t* guard, hipStream_t stream_);
+/* StochasticAcceptor decision for given densities, SCALE_LOG (log_scale=1)
+ * or SCALE_LIN: acc = (pd / pdf_norm) ** inv_temp.   acceptor/acceptor.py:456-473 */
+int abc_stochastic_accept_f64(const double* pd, int64_t B, double pdf_norm,
+                              double inv_temp, int log_scale, int apply_iw,
+                              const double* u, uint64_t seed, uint64_t stream,
+                              uint64_t offset, uint8_t* accept, double* accw,
+                              uint8_t* guard, hipStream_t stream_);
+/* weight = prior_pd * acceptance_weight * 1 / transition_pd  smc.py:776-792
+ * (logpd == NULL at t = 0: prior_const * s_i,                smc.py:762-770) */
+int abc_importance_weights_scaled_f64(const double* logpd, const double* s,
+                                      double prior_const, int64_t M, double* w,
+                                      hipStream_t stream);
+/* Temperature-scheme sums (epsilon/temperature.py:306-345 AcceptanceRateScheme
+ * objective with weights t_pd / t_pd_prev, :695-742 EssScheme):
+ *   w_i = (w ? w_i : 1) * (logw_num ? exp(logw_num_i - (logw_den ? logw_den_i : 0)) : 1)
+ *   v = exp((pd - c) beta_k) [log] or (pd / c)^beta_k [lin], min(v, 1) if clamp
+ *   out[0] = sum w, out[1] = sum w^2, out[2+2k] = sum w v, out[3+2k] = sum (w v)^2
+ * for k < K (<= 16).  Deterministic fixed-order reduction. */
+size_t abc_tempered_sums_workspace_bytes(int K);
+int abc_tempered_sums_f64(const double* pd, const double* w,
+                          const double* logw_num, const double* logw_den,
+                          int64_t n, double c, int log_scale,
+                          const double* betas, int K, int clamp, double* out,
+                          void* ws, size_t ws_bytes, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -440,3 +440,124 @@ def philox_normal(seed, stream, n):
     ang = 2.0 * np.pi * u2
     odd = (i & np.uint64(1)).astype(bool)
     return np.where(odd, r * np.sin(ang), r * np.cos(ang))
+
+
+# ---------------------------------------------------------------------------
+# (f3) exact inference: stochastic kernels, stochastic acceptance,
+#      temperature schemes
+# ---------------------------------------------------------------------------
+def np_pairwise_sum(a):
+    """numpy's float64 ``np.sum`` of a contiguous vector: 0 + pairwise(a).
+
+    pairwise(n < 8): sequential; n <= 128: eight strided accumulators seeded
+    with a[0..7], combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the
+    n % 8 tail sequentially; n > 128: split at n2 = n//2 rounded down to a
+    multiple of 8 (numpy/_core/src/umath/loops_utils.h.src pairwise_sum)."""
+    a = [float(x) for x in a]
+
+    def pw(lo, n):
+        if n < 8:
+            r = 0.0
+            for i in range(lo, lo + n):
+                r += a[i]
+            return r
+        if n <= 128:
+            r = a[lo:lo + 8]
+            i = 8
+            while i < n - (n % 8):
+                for j in range(8):
+                    r[j] += a[lo + i + j]
+                i += 8
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+            while i < n:
+                res += a[lo + i]
+                i += 1
+            return res
+        n2 = n // 2
+        n2 -= n2 % 8
+        return pw(lo, n2) + pw(lo + n2, n - n2)
+    return 0.0 + pw(0, len(a))
+
+
+def independent_normal_logpdf(stats, x0, var):
+    """IndependentNormalKernel.__call__ (distance/kernel.py:256-282), rows of
+    ``stats[B,S]`` in the kernel's key order:
+    -0.5 * (sum(log 2 + log pi + log var) + sum(diff**2 / var)), both sums
+    numpy pairwise, diff = x - x_0."""
+    stats = np.atleast_2d(np.asarray(stats, dtype=np.float64))
+    var = np.asarray(var, dtype=np.float64)
+    c = np.sum(np.log(2) + np.log(np.pi) + np.log(var))
+    diff = stats - np.asarray(x0, dtype=np.float64)[None, :]
+    sq = np.array([np_pairwise_sum((r ** 2) / var) for r in diff])
+    return -0.5 * (c + sq)
+
+
+def independent_laplace_logpdf(stats, x0, scale):
+    """IndependentLaplaceKernel.__call__ (distance/kernel.py:332-357):
+    -(sum(log 2 + log b) + sum(|diff| / b))."""
+    stats = np.atleast_2d(np.asarray(stats, dtype=np.float64))
+    scale = np.asarray(scale, dtype=np.float64)
+    c = np.sum(np.log(2) + np.log(scale))
+    diff = stats - np.asarray(x0, dtype=np.float64)[None, :]
+    ab = np.array([np_pairwise_sum(np.abs(r) / scale) for r in diff])
+    return -(c + ab)
+
+
+def stochastic_accept(pd, pdf_norm, temp, u, log_scale=True,
+                      apply_importance_weighting=True):
+    """StochasticAcceptor.__call__ (acceptor/acceptor.py:440-473):
+    acc_prob = exp((pd - c) * (1/T)) [log] or (pd / c) ** (1/T) [lin];
+    accept iff acc_prob >= u; weight 0 if acc_prob == 0, else
+    acc_prob / min(1, acc_prob) (or 1 without importance weighting)."""
+    pd = np.asarray(pd, dtype=np.float64)
+    inv_t = 1 / temp
+    if log_scale:
+        with np.errstate(over="ignore"):
+            acc = np.exp((pd - pdf_norm) * inv_t)   # numpy's exp, as the ref
+    else:
+        acc = np.array([(p / pdf_norm) ** inv_t for p in pd])
+    accept = acc >= np.asarray(u)
+    w = np.where(acc == 0.0, 0.0,
+                 acc / np.minimum(1.0, acc) if apply_importance_weighting
+                 else 1.0)
+    return acc, accept, w
+
+
+def pdf_norm_max_found(prev_pdf_norm, pds):
+    """max(prev, *pds) (acceptor/pdf_norm.py:17-38)."""
+    prev = -np.inf if prev_pdf_norm is None else prev_pdf_norm
+    return max(prev, *pds)
+
+
+def match_acceptance_rate(weights, pds, pdf_norm, log_scale, target_rate):
+    """epsilon/temperature.py:306-345: bisection in b = log(beta) on
+    sum(w * min(acc_prob(beta), 1)) - target over [-100, 0]; T = 1/exp(b)."""
+    import scipy.optimize
+    weights = np.asarray(weights, dtype=np.float64)
+    pds = np.asarray(pds, dtype=np.float64)
+
+    def obj(b):
+        beta = np.exp(b)
+        if log_scale:
+            acc = np.exp((pds - pdf_norm) * beta)
+        else:
+            acc = (pds / pdf_norm) ** beta
+        return np.sum(weights * np.minimum(acc, 1.0)) - target_rate
+    min_b = -100
+    if obj(0) > 0:
+        b = 0
+    elif obj(min_b) < 0:
+        b = min_b
+    else:
+        b = scipy.optimize.bisect(obj, min_b, 0, maxiter=100000)
+    return 1. / np.exp(b)
+
+
+def acceptance_rate_temperature(pds, t_pd_prev, t_pd, pdf_norm, log_scale,
+                                target_rate=0.3):
+    """AcceptanceRateScheme.__call__ (epsilon/temperature.py:280-303):
+    importance weights t_pd / t_pd_prev normalised by a sequential sum."""
+    w = np.asarray(t_pd, dtype=np.float64) / np.asarray(t_pd_prev,
+                                                         dtype=np.float64)
+    w = w / sum(w)
+    return match_acceptance_rate(w, pds, pdf_norm, log_scale, target_rate)

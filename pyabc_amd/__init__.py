@@ -23,12 +23,24 @@ from .distance import (Distance, NoDistance, SimpleFunctionDistance,  # noqa: E4
                        mean_absolute_deviation_to_observation,
                        combined_median_absolute_deviation,
                        combined_mean_absolute_deviation,
-                       standard_deviation_to_observation, span, mean, median)
+                       standard_deviation_to_observation, span, mean, median,
+                       SCALE_LIN, SCALE_LOG, StochasticKernel,
+                       SimpleFunctionKernel, NormalKernel,
+                       IndependentNormalKernel, IndependentLaplaceKernel,
+                       BinomialKernel, PoissonKernel, NegativeBinomialKernel)
 from .epsilon import (Epsilon, NoEpsilon, ConstantEpsilon,  # noqa: E402
                       ListEpsilon, QuantileEpsilon, MedianEpsilon)
 from .acceptor import (Acceptor, SimpleFunctionAcceptor,  # noqa: E402
                        UniformAcceptor, AcceptorResult,
-                       accept_use_current_time, accept_use_complete_history)
+                       accept_use_current_time, accept_use_complete_history,
+                       StochasticAcceptor, pdf_norm_from_kernel,
+                       pdf_norm_max_found, ScaledPDFNorm)
+from .temperature import (TemperatureBase, ListTemperature,  # noqa: E402
+                          Temperature, TemperatureScheme,
+                          AcceptanceRateScheme, ExpDecayFixedIterScheme,
+                          ExpDecayFixedRatioScheme,
+                          PolynomialDecayFixedIterScheme, DalyScheme,
+                          FrielPettittScheme, EssScheme)
 from .model import (Model, SimpleModel, ModelResult,  # noqa: E402
                     IntegratedModel, BatchModel, LinearGaussianModel,
                     GaussianMeanModel)
@@ -37,12 +49,13 @@ from .populationstrategy import (PopulationStrategy,  # noqa: E402
                                  ConstantPopulationSize, ListPopulationSize)
 from .sampler import (Sample, SampleFactory, Sampler,  # noqa: E402
                       SingleCoreSampler, GPUBatchSampler)
-from .storage import History  # noqa: E402
+from .storage import History, create_sqlite_db_id  # noqa: E402
 from .transition import (Transition, MultivariateNormalTransition,  # noqa: E402
                          LocalTransition, NotEnoughParticles,
                          silverman_rule_of_thumb, scott_rule_of_thumb)
 from .smc import ABCSMC  # noqa: E402
 from . import weighted_statistics  # noqa: E402
+from . import storage  # noqa: E402
 
 DefaultSampler = GPUBatchSampler
 

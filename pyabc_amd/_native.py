@@ -111,6 +111,20 @@ _SIGS = {
                                              c_ptr, c_ptr, c_ptr, c_u64,
                                              c_u64, c_u64, c_i64, c_ptr,
                                              c_ptr, c_ptr, c_ptr]),
+    # (f3) exact inference: stochastic kernels / acceptor / temperatures
+    "abc_stochastic_kernel_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_int,
+                                          c_int, c_dbl, c_i64, c_ptr, c_dbl,
+                                          c_dbl, c_int, c_ptr, c_u64, c_u64,
+                                          c_u64, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_stochastic_accept_f64": (c_int, [c_ptr, c_i64, c_dbl, c_dbl, c_int,
+                                          c_int, c_ptr, c_u64, c_u64, c_u64,
+                                          c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_importance_weights_scaled_f64": (c_int, [c_ptr, c_ptr, c_dbl, c_i64,
+                                                  c_ptr, c_ptr]),
+    "abc_tempered_sums_workspace_bytes": (c_size, [c_int]),
+    "abc_tempered_sums_f64": (c_int, [c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
+                                      c_dbl, c_int, c_ptr, c_int, c_int,
+                                      c_ptr, c_ptr, c_size, c_ptr]),
     # simulators
     "abc_sim_linear_gaussian_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                             c_int, c_dbl, c_u64, c_u64, c_u64,

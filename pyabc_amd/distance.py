@@ -108,6 +108,17 @@ class DeviceStats:
         return dict(zip(self.keys, self.stats_T[:, j].cpu().numpy()))
 
 
+def _rows_in_order(stats_T, have, want):
+    """Rows of stat-major ``stats_T`` (statistics ``have``) reordered to the
+    statistics ``want``; unchanged when the orders agree or ``have`` is
+    unknown."""
+    if have is None or list(have) == list(want):
+        return stats_T
+    idx = torch.as_tensor([list(have).index(k) for k in want],
+                          device=stats_T.device)
+    return stats_T.index_select(0, idx).contiguous()
+
+
 def _stats_matrix(keys, all_sum_stats):
     """[S, n] device matrix from a DeviceStats or a list of dicts."""
     if isinstance(all_sum_stats, DeviceStats):
@@ -237,9 +248,11 @@ class PNormDistance(Distance):
                                    fwd, self.p, with_accept=False)
         return float(d.item())
 
-    def batch(self, stats_T, t, x_0, eps=np.inf, n=None):
-        """Distances (and accept flags) of n stat-major columns."""
-        _, x0d, fwd = self.device_params(t, x_0)
+    def batch(self, stats_T, t, x_0, eps=np.inf, n=None, keys=None):
+        """Distances (and accept flags) of n stat-major columns whose rows
+        are the statistics ``keys`` (default: the distance's key order)."""
+        dkeys, x0d, fwd = self.device_params(t, x_0)
+        stats_T = _rows_in_order(stats_T, keys, dkeys)
         return K.pnorm_distance(stats_T, x0d, fwd, self.p, eps, B=n)
 
     def get_config(self):
@@ -339,3 +352,296 @@ class AdaptivePNormDistance(PNormDistance):
                 "scale_function": self.scale_function.__name__,
                 "normalize_weights": self.normalize_weights,
                 "max_weight_ratio": self.max_weight_ratio}
+
+
+# ---------------------------------------------------------------------------
+# stochastic kernels (distance/kernel.py:1-588): densities for the
+# StochasticAcceptor.  Independent normal / Laplace kernels evaluate through
+# abc_stochastic_kernel_f64 (single calls and the batch sampler alike).
+# ---------------------------------------------------------------------------
+SCALE_LIN = "SCALE_LIN"
+SCALE_LOG = "SCALE_LOG"
+SCALES = [SCALE_LIN, SCALE_LOG]
+
+
+def _flat(x, keys):
+    """Values of ``keys`` flattened into one float64 vector (kernel.py:563-588
+    ``_diff_arr`` / ``_arr``: array-valued statistics are extended)."""
+    out = []
+    for key in keys:
+        v = x[key]
+        try:
+            out.extend(v)
+        except TypeError:
+            out.append(v)
+    return np.array(out, dtype=np.float64)
+
+
+class StochasticKernel(Distance):
+    """Base of the density kernels (kernel.py:12-80); ``ret_scale`` is
+    SCALE_LIN or SCALE_LOG, ``keys`` default to sorted(x_0), ``pdf_max`` the
+    density at x_0 unless given."""
+
+    def __init__(self, ret_scale=SCALE_LIN, keys=None, pdf_max=None):
+        super().__init__()
+        StochasticKernel.check_ret_scale(ret_scale)
+        self.ret_scale = ret_scale
+        self.keys = keys
+        self.pdf_max = pdf_max
+
+    def initialize(self, t, get_all_sum_stats, x_0=None):
+        if self.keys is None:
+            self.initialize_keys(x_0)
+
+    @staticmethod
+    def check_ret_scale(ret_scale):
+        if ret_scale not in SCALES:
+            raise ValueError(
+                f"The ret_scale {ret_scale} must be one of {SCALES}.")
+
+    def initialize_keys(self, x):
+        self.keys = sorted(x)
+
+    def get_config(self):
+        return {"name": self.__class__.__name__, "ret_scale": self.ret_scale,
+                "keys": self.keys, "pdf_max": self.pdf_max}
+
+    def to_json(self):
+        return json.dumps(self.get_config(), default=str)
+
+
+class SimpleFunctionKernel(StochasticKernel):
+    """User density function fun(x, x_0, t, par) (kernel.py:82-107)."""
+
+    def __init__(self, fun, ret_scale=SCALE_LIN, keys=None, pdf_max=None):
+        super().__init__(ret_scale=ret_scale, keys=keys, pdf_max=pdf_max)
+        self.fun = fun
+
+    def __call__(self, x, x_0, t=None, par=None):
+        return self.fun(x=x, x_0=x_0, t=t, par=par)
+
+
+class NormalKernel(StochasticKernel):
+    """Multivariate normal density of x - x_0 (kernel.py:110-187), scipy's
+    ``multivariate_normal`` semantics (host; d x d parameters)."""
+
+    def __init__(self, cov=None, ret_scale=SCALE_LOG, keys=None,
+                 pdf_max=None):
+        super().__init__(ret_scale=ret_scale, keys=keys, pdf_max=pdf_max)
+        self.cov = cov
+
+    def initialize(self, t, get_all_sum_stats, x_0=None):
+        super().initialize(t, get_all_sum_stats, x_0)
+        if self.cov is None:
+            self.cov = np.eye(sum(np.size(x_0[k]) for k in self.keys))
+        self.cov = np.array(self.cov)
+        import scipy.stats
+        self.rv = scipy.stats.multivariate_normal(
+            mean=np.zeros(self.cov.shape[0]), cov=self.cov)
+        if self.pdf_max is None:
+            self.pdf_max = self(x_0, x_0)
+
+    def __call__(self, x, x_0, t=None, par=None):
+        if self.keys is None:
+            self.initialize_keys(x_0)
+        diff = _flat(x, self.keys) - _flat(x_0, self.keys)
+        if self.ret_scale == SCALE_LIN:
+            return self.rv.pdf(diff)
+        return self.rv.logpdf(diff)
+
+
+class _IndependentKernel(StochasticKernel):
+    """Shared device evaluation of the independent normal / Laplace kernels
+    (kernel.py:190-357): prm is the variance (normal) or scale (Laplace)
+    vector, a scalar broadcast over the statistics, or a callable of the
+    parameters."""
+    _kind = None
+
+    def __init__(self, prm, keys=None, pdf_max=None):
+        super().__init__(ret_scale=SCALE_LOG, keys=keys, pdf_max=pdf_max)
+        self._prm = prm
+        self._dev_cache = None
+
+    def _const(self, prm):
+        """The kernel's log-normalisation term c (numpy, as the reference)."""
+        raise NotImplementedError
+
+    def initialize(self, t, get_all_sum_stats, x_0=None):
+        super().initialize(t, get_all_sum_stats, x_0)
+        dim = sum(np.size(x_0[k]) for k in self.keys)
+        if self._prm is None:
+            self._prm = np.ones(dim)
+        if not callable(self._prm):
+            self._prm = np.array(self._prm) * np.ones(dim)
+        self._dev_cache = None
+        if self.pdf_max is None and not callable(self._prm):
+            self.pdf_max = self(x_0, x_0)
+
+    def _evaluate(self, xs, x0s, prm):
+        prm = np.asarray(prm, dtype=np.float64) * np.ones(xs.shape[0])
+        dev = torch.device("cuda", torch.cuda.current_device())
+        col = torch.as_tensor(xs.reshape(-1, 1), device=dev)
+        pd, _, _, _ = K.stochastic_kernel(
+            col, torch.as_tensor(x0s, device=dev),
+            torch.as_tensor(prm, device=dev), self._kind, self._const(prm))
+        return float(pd.item())
+
+    def __call__(self, x, x_0, t=None, par=None):
+        if self.keys is None:
+            self.initialize_keys(x_0)
+        prm = self._prm(par) if callable(self._prm) else self._prm
+        return self._evaluate(_flat(x, self.keys), _flat(x_0, self.keys), prm)
+
+    # --- batch (device) interface -----------------------------------------
+    def batch_unsupported_reason(self, x_0):
+        if callable(self._prm):
+            return "kernel parameters depend on the particle parameters"
+        if any(np.size(x_0[k]) != 1 for k in self.keys):
+            return "array-valued summary statistics"
+        return None
+
+    def device_params(self, t, x_0):
+        """(keys, x0[S], prm[S], kind, c) for the batch kernel, in the
+        kernel's key order."""
+        if self._dev_cache is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            prm = np.asarray(self._prm, dtype=np.float64)
+            self._dev_cache = (
+                list(self.keys),
+                torch.as_tensor(_flat(x_0, self.keys), device=dev),
+                torch.as_tensor(prm, device=dev), self._kind,
+                self._const(prm))
+        return self._dev_cache
+
+    def batch(self, stats_T, t, x_0, eps=np.inf, n=None, keys=None):
+        """Log-densities of n stat-major columns whose rows are the
+        statistics ``keys`` (default: the kernel's key order)."""
+        dkeys, x0d, prmd, kind, c = self.device_params(t, x_0)
+        stats_T = _rows_in_order(stats_T, keys, dkeys)
+        pd, _, _, _ = K.stochastic_kernel(stats_T, x0d, prmd, kind, c, B=n)
+        return pd, None, None
+
+
+class IndependentNormalKernel(_IndependentKernel):
+    """-0.5 (sum log(2 pi var) + sum diff^2 / var)  (kernel.py:190-282)."""
+    _kind = K.KERNEL_NORMAL
+
+    def __init__(self, var=None, keys=None, pdf_max=None):
+        super().__init__(var, keys=keys, pdf_max=pdf_max)
+
+    @property
+    def var(self):
+        return self._prm
+
+    @var.setter
+    def var(self, v):
+        self._prm = v
+        self._dev_cache = None
+
+    def _const(self, prm):
+        return float(np.sum(np.log(2) + np.log(np.pi) + np.log(prm)))
+
+
+class IndependentLaplaceKernel(_IndependentKernel):
+    """-(sum log(2 b) + sum |diff| / b)  (kernel.py:285-357)."""
+    _kind = K.KERNEL_LAPLACE
+
+    def __init__(self, scale=None, keys=None, pdf_max=None):
+        super().__init__(scale, keys=keys, pdf_max=pdf_max)
+
+    @property
+    def scale(self):
+        return self._prm
+
+    @scale.setter
+    def scale(self, v):
+        self._prm = v
+        self._dev_cache = None
+
+    def _const(self, prm):
+        return float(np.sum(np.log(2) + np.log(prm)))
+
+
+class _DiscreteKernel(StochasticKernel):
+    """Count-data likelihoods (kernel.py:360-560), scipy.stats pmfs of the
+    observed counts given the simulated ones (host, closure sampler path)."""
+
+    def __init__(self, p=None, ret_scale=SCALE_LOG, keys=None, pdf_max=None):
+        super().__init__(ret_scale=ret_scale, keys=keys, pdf_max=pdf_max)
+        if p is not None and not callable(p) and (p > 1 or p < 0):
+            raise ValueError(
+                f"The success probability p={p} must be in the interval"
+                f"[0, 1].")
+        self.p = p
+
+    def _dist(self):
+        raise NotImplementedError
+
+    def _args(self, k, n, p):
+        return dict(k=k, n=n, p=p)
+
+    def __call__(self, x, x_0, t=None, par=None):
+        n = _flat(x, self.keys).astype(int)
+        k = _flat(x_0, self.keys).astype(int)
+        p = self.p(par) if callable(self.p) else self.p
+        dist, args = self._dist(), self._args(k, n, p)
+        if self.ret_scale == SCALE_LIN:
+            return np.prod(dist.pmf(**args))
+        return np.sum(dist.logpmf(**args))
+
+
+class BinomialKernel(_DiscreteKernel):
+    """binom.pmf(k=x_0, n=x, p) (kernel.py:360-419)."""
+
+    def __init__(self, p, ret_scale=SCALE_LOG, keys=None, pdf_max=None):
+        super().__init__(p, ret_scale, keys, pdf_max)
+
+    def initialize(self, t, get_all_sum_stats, x_0=None):
+        super().initialize(t, get_all_sum_stats, x_0)
+        if self.pdf_max is None and not callable(self.p):
+            self.pdf_max = binomial_pdf_max(x_0, self.keys, self.p,
+                                            self.ret_scale)
+
+    def _dist(self):
+        import scipy.stats
+        return scipy.stats.binom
+
+
+class PoissonKernel(_DiscreteKernel):
+    """poisson.pmf(k=x_0, mu=x) (kernel.py:422-470)."""
+
+    def __init__(self, ret_scale=SCALE_LOG, keys=None, pdf_max=None):
+        super().__init__(None, ret_scale, keys, pdf_max)
+
+    def initialize(self, t, get_all_sum_stats, x_0=None):
+        super().initialize(t, get_all_sum_stats, x_0)
+        if self.pdf_max is None:
+            self.pdf_max = self(x_0, x_0)
+
+    def _dist(self):
+        import scipy.stats
+        return scipy.stats.poisson
+
+    def _args(self, k, n, p):
+        return dict(k=k, mu=n)
+
+
+class NegativeBinomialKernel(_DiscreteKernel):
+    """nbinom.pmf(k=x_0, n=x, p) (kernel.py:473-529)."""
+
+    def __init__(self, p, ret_scale=SCALE_LOG, keys=None, pdf_max=None):
+        super().__init__(p, ret_scale, keys, pdf_max)
+
+    def _dist(self):
+        import scipy.stats
+        return scipy.stats.nbinom
+
+
+def binomial_pdf_max(x_0, keys, p, ret_scale):
+    """Max over n of binom.pmf(k=x_0, n, p): n = max(ceil((k-p)/p), 0)
+    (kernel.py:532-551)."""
+    import scipy.stats
+    ks = _flat(x_0, keys).astype(int)
+    ns = np.maximum(np.ceil((ks - p) / p), 0)
+    lp = np.sum(scipy.stats.binom.logpmf(k=ks, n=ns, p=p))
+    return np.exp(lp) if ret_scale == SCALE_LIN else lp

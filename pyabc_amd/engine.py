@@ -157,6 +157,40 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     return torch.cat(out) if out else allr[:0]
 
 
+class PNormAcceptance:
+    """Uniform acceptance d <= eps of a p-norm distance
+    (distance/distance.py:76-102, acceptor/acceptor.py:235-244)."""
+
+    def __init__(self, x0, fw, p, eps):
+        self.x0, self.fw, self.p, self.eps = x0, fw, p, eps
+
+    def __call__(self, stats, nv, seed, stream, eval_off):
+        d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
+                                         self.eps, B=nv)
+        return d, acc, guard, None
+
+
+class StochasticAcceptance:
+    """StochasticAcceptor over an independent normal / Laplace kernel
+    (acceptor/acceptor.py:440-473, distance/kernel.py:256-357): the log
+    density, u ~ U[0,1) from Philox keyed by the GLOBAL evaluation id, the
+    decision acc >= u and the acceptance weight, in one fused kernel."""
+
+    def __init__(self, x0, prm, kind, c, pdf_norm, temperature,
+                 apply_importance_weighting=True):
+        self.x0, self.prm, self.kind, self.c = x0, prm, kind, c
+        self.pdf_norm = float(pdf_norm)
+        self.inv_temp = 1 / temperature
+        self.apply_iw = apply_importance_weighting
+
+    def __call__(self, stats, nv, seed, stream, eval_off):
+        pd, acc, accw, guard = K.stochastic_kernel(
+            stats, self.x0, self.prm, self.kind, self.c, B=nv,
+            pdf_norm=self.pdf_norm, inv_temp=self.inv_temp,
+            apply_iw=self.apply_iw, seed=seed, stream=stream, offset=eval_off)
+        return pd, acc, guard, accw
+
+
 class GenerationResult:
     def __init__(self, **kw):
         self.__dict__.update(kw)
@@ -193,8 +227,13 @@ class GenerationEngine:
     def _sid(self, t, kind):
         # disjoint Philox stream ids per (generation, purpose); shared by all
         # ranks -- a proposal's random numbers are keyed by its GLOBAL id, so
-        # the draws do not depend on the number of ranks
+        # the draws do not depend on the number of ranks.  Proposal kernels
+        # use the raw streams 2*sid and 2*sid+1; single-stream consumers get
+        # _stream() = 2*sid, so no two purposes ever share a raw stream.
         return int(t) * 8 + kind
+
+    def _stream(self, t, kind):
+        return 2 * self._sid(t, kind)
 
     def quota(self, n):
         """Rows of a population of n this rank owns for row-parallel work."""
@@ -220,13 +259,14 @@ class GenerationEngine:
         a single GPU would draw."""
         lo, hi = self.row_range(n)
         theta = K.prior_uniform(self.lo, self.scale, self.seed,
-                                self._sid(t, 0), lo, hi - lo)
-        stats = self.model.simulate(theta, self.seed, self._sid(t, 1), lo)
+                                self._stream(t, 0), lo, hi - lo)
+        stats = self.model.simulate(theta, self.seed, self._stream(t, 1), lo)
         return GenerationResult(theta=theta, stats_T=stats, n_eval=hi - lo,
                                 rec_stats_T=stats, n_rec=hi - lo)
 
     def sample_generation(self, t, n, fit, x0, fw, eps, keep_stats=None,
-                          record=None, stream_base=0):
+                          record=None, stream_base=0, acceptance=None,
+                          record_particles=False):
         """Proposals until n are accepted (over all ranks), then KDE weights.
 
         Global-id semantics (SingleCoreSampler, singlecore.py:19-38): raw
@@ -243,9 +283,16 @@ class GenerationEngine:
         unnormalised w, logpd, n_eval, and with ``keep_stats`` / ``record``
         the accepted statistics / the statistics of every evaluation up to
         the n-th acceptance (record_rejected, sampler/base.py:119-141),
-        stat-major."""
+        stat-major.  ``acceptance`` (default: p-norm with ``x0, fw, eps``)
+        decides acceptance per evaluation; a stochastic acceptance also
+        returns acceptance weights that enter the importance weights.
+        ``record_particles`` keeps parameters, distances and accept flags of
+        the recorded evaluations (the temperature schemes' records,
+        smc.py:990-1017)."""
         keep_stats = self.record_stats if keep_stats is None else keep_stats
         record = self.record_stats if record is None else record
+        if acceptance is None and x0 is not None:
+            acceptance = PNormAcceptance(x0, fw, self.p, eps)
         comm = self.comm
         R, r = comm.world, comm.rank
         tm = {}
@@ -264,7 +311,8 @@ class GenerationEngine:
             my_raw = raw_off + r * B
             if fit is None:
                 theta = K.prior_uniform(self.lo, self.scale, self.seed,
-                                        self._sid(t, stream_base), my_raw, B)
+                                        self._stream(t, stream_base), my_raw,
+                                        B)
                 nvs = [B] * R
             else:
                 theta_all, idx, sup = fit.propose(
@@ -278,10 +326,12 @@ class GenerationEngine:
             my_eval = eval_off + sum(nvs[:r])
             if nv:
                 stats = self.model.simulate(
-                    theta, self.seed, self._sid(t, stream_base + 1), my_eval)
+                    theta, self.seed, self._stream(t, stream_base + 1),
+                    my_eval)
             else:
                 stats = None
-            if x0 is None:
+            accw = acc = None
+            if acceptance is None:
                 # calibration sample: everything accepted, distances later
                 # (smc.py:486-514: accepted_distances = [inf])
                 d = torch.full((nv,), math.inf, dtype=F64, device=self.dev)
@@ -289,15 +339,17 @@ class GenerationEngine:
                 apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
                 nas = list(nvs)
             elif nv:
-                d, acc, guard = K.pnorm_distance(stats, x0, fw, self.p, eps,
-                                                 B=nv)
+                d, acc, guard, accw = acceptance(
+                    stats, nv, self.seed, self._stream(t, stream_base + 4),
+                    my_eval)
                 apos, acount = K.compact(acc)
                 nas = comm.all_gather_ints(acount)                  # sync 2
             else:
                 d = guard = apos = None
                 nas = comm.all_gather_ints(0)
             rounds.append(dict(theta=theta, stats=stats, d=d, apos=apos,
-                               guard=guard, nvs=nvs, nas=nas, acc0=n_acc))
+                               guard=guard, accw=accw, acc=acc, nvs=nvs,
+                               nas=nas, acc0=n_acc))
             raw_off += R * B
             eval_off += sum(nvs)
             n_acc += sum(nas)
@@ -318,6 +370,8 @@ class GenerationEngine:
                                         [rd["nas"] for rd in rounds], n)
         lasts = []
         th_loc, d_loc, st_loc, rec_loc = [], [], [], []
+        aw_loc, rth_loc, rd_loc, ra_loc = [], [], [], []
+        stochastic = isinstance(acceptance, StochasticAcceptance)
         n_guard = 0
         n_eval_loc = 0
         for rd, take, cl in zip(rounds, takes, closing):
@@ -334,11 +388,19 @@ class GenerationEngine:
                 sel = rd["apos"][:k]
                 th_loc.append(rd["theta"].index_select(0, sel))
                 d_loc.append(rd["d"].index_select(0, sel))
+                if stochastic:
+                    aw_loc.append(rd["accw"].index_select(0, sel))
                 if keep_stats:
                     st_loc.append(rd["stats"].index_select(1, sel))
             if last:
                 if record:
                     rec_loc.append(rd["stats"][:, :last])
+                if record_particles:
+                    rth_loc.append(rd["theta"][:last])
+                    rd_loc.append(rd["d"][:last])
+                    ra_loc.append(rd["acc"][:last].to(F64) if rd["acc"]
+                                  is not None else torch.ones(
+                                      last, dtype=F64, device=self.dev))
                 n_guard += int(rd["guard"][:last].sum().item())
         n_eval, n_guard = comm.all_reduce_ints([n_eval_loc, n_guard])
         take_counts = [[tk[s] for tk in takes] for s in range(R)]
@@ -347,16 +409,27 @@ class GenerationEngine:
         stats_acc = None
         if keep_stats:
             stats_acc = self._gather_cols(st_loc, take_counts)
+        accw_acc = self._gather(aw_loc, (), take_counts) if stochastic \
+            else None
         rec = None
-        if record:
+        last_counts = None
+        if record or record_particles:
             last_counts = comm.all_gather_int_lists(lasts)
+        if record:
             rec = self._gather_cols(rec_loc, last_counts)
+        rec_theta = rec_d = rec_acc = None
+        if record_particles:
+            rec_theta = self._gather(rth_loc, (self.d,), last_counts)
+            rec_d = self._gather(rd_loc, (), last_counts)
+            rec_acc = self._gather(ra_loc, (), last_counts)
         torch.cuda.synchronize()
         tm["select"] = time.perf_counter() - t0 - tm["propose_sim_dist"]
         t1 = time.perf_counter()
         if fit is None:
             logpd = None
-            w = torch.ones(theta_acc.shape[0], dtype=F64, device=self.dev)
+            # t = 0: weight = 1 * prod(acceptance weights) (smc.py:762-770)
+            w = accw_acc.clone() if stochastic else torch.ones(
+                theta_acc.shape[0], dtype=F64, device=self.dev)
         else:
             # row-parallel weight pass: rank r weights rows row_range(n)
             lo, hi = self.row_range(theta_acc.shape[0])
@@ -373,13 +446,17 @@ class GenerationEngine:
                 lp = fit.logpdf(mine)
             logpd = comm.all_gather_rows(
                 lp, [b - a for a, b in self.row_ranges(theta_acc.shape[0])])
-            w = K.importance_weights(logpd, None, self.prior_pd)
+            if stochastic:
+                w = K.importance_weights_scaled(logpd, accw_acc, self.prior_pd)
+            else:
+                w = K.importance_weights(logpd, None, self.prior_pd)
         torch.cuda.synchronize()
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm
         return GenerationResult(
             theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
-            n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec)
+            n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec,
+            accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc)
 
     def _gather(self, pieces, row_shape, counts):
         return gather_segments(self.comm, pieces, row_shape, counts, self.dev)

@@ -381,3 +381,78 @@ def sim_gaussian_mean(theta, sigma, seed, sid, offset, out=None, B=None):
     call("abc_sim_gaussian_mean_f64", ptr(_contig(theta, F64)), B,
          float(sigma), seed, sid, offset, ptr(out), nat.stream())
     return out
+
+
+# ---------------------------------------------------------------------------
+# exact inference: stochastic kernels and acceptance
+# ---------------------------------------------------------------------------
+KERNEL_NORMAL = 0
+KERNEL_LAPLACE = 1
+
+
+def stochastic_kernel(stats_T, x0, prm, kind, c, B=None, pdf_norm=None,
+                      inv_temp=1.0, apply_iw=True, u=None, seed=0, stream=0,
+                      offset=0):
+    """Log-densities of an independent normal / Laplace kernel per column of
+    stat-major ``stats_T`` ([S, ld]); with ``pdf_norm`` also the fused
+    stochastic acceptance.  Returns (pd, accept, accw, guard)."""
+    S, ld = stats_T.shape
+    B = ld if B is None else B
+    pd = torch.empty(B, dtype=F64, device=_dev())
+    acc = accw = guard = None
+    if pdf_norm is not None:
+        acc = torch.empty(B, dtype=torch.uint8, device=_dev())
+        accw = torch.empty(B, dtype=F64, device=_dev())
+        guard = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_stochastic_kernel_f64", ptr(stats_T), ld, ptr(_contig(x0, F64)),
+         ptr(_contig(prm, F64)), S, int(kind), float(c), B, ptr(pd),
+         float(pdf_norm if pdf_norm is not None else 0.0), float(inv_temp),
+         1 if apply_iw else 0, ptr(None if u is None else _contig(u, F64)),
+         int(seed), int(stream), int(offset), ptr(acc), ptr(accw), ptr(guard),
+         nat.stream())
+    return pd, acc, accw, guard
+
+
+def stochastic_accept(pd, pdf_norm, inv_temp, log_scale=True, apply_iw=True,
+                      u=None, seed=0, stream=0, offset=0):
+    """StochasticAcceptor decisions for given densities: (accept, accw, guard)."""
+    pd = _contig(pd, F64)
+    B = pd.numel()
+    acc = torch.empty(B, dtype=torch.uint8, device=_dev())
+    accw = torch.empty(B, dtype=F64, device=_dev())
+    guard = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_stochastic_accept_f64", ptr(pd), B, float(pdf_norm),
+         float(inv_temp), 1 if log_scale else 0, 1 if apply_iw else 0,
+         ptr(None if u is None else _contig(u, F64)), int(seed), int(stream),
+         int(offset), ptr(acc), ptr(accw), ptr(guard), nat.stream())
+    return acc, accw, guard
+
+
+def importance_weights_scaled(logpd, s, prior_const=1.0, M=None):
+    """(prior_const * s_i) / exp(logpd_i); logpd None -> prior_const * s_i."""
+    M = (s if logpd is None else logpd).numel() if M is None else M
+    w = torch.empty(M, dtype=F64, device=_dev())
+    call("abc_importance_weights_scaled_f64",
+         ptr(None if logpd is None else _contig(logpd, F64)),
+         ptr(None if s is None else _contig(s, F64)), float(prior_const), M,
+         ptr(w), nat.stream())
+    return w
+
+
+def tempered_sums(pd, c, betas, w=None, logw_num=None, logw_den=None,
+                  log_scale=True, clamp=True):
+    """Device [K+1, 2]: row 0 = (sum w, sum w^2), row 1+k = (sum w v_k,
+    sum (w v_k)^2) for v_k = exp((pd-c) beta_k) [log] or (pd/c)^beta_k [lin]
+    (clamped at 1 when ``clamp``); w = w * exp(logw_num - logw_den)."""
+    pd = _contig(pd, F64)
+    b = np.asarray(betas, dtype=np.float64).ravel()
+    K = b.size
+    bt = torch.as_tensor(b, device=_dev()) if K else None
+    out = torch.empty((K + 1, 2), dtype=F64, device=_dev())
+    wsb = nat.lib().abc_tempered_sums_workspace_bytes(K)
+    ws = WS.get(wsb, "tempered")
+    opt = lambda t: ptr(None if t is None else _contig(t, F64))  # noqa: E731
+    call("abc_tempered_sums_f64", ptr(pd), opt(w), opt(logw_num),
+         opt(logw_den), pd.numel(), float(c), 1 if log_scale else 0, ptr(bt),
+         K, 1 if clamp else 0, ptr(out), ptr(ws), wsb, nat.stream())
+    return out

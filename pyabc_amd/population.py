@@ -120,6 +120,13 @@ class WeightedDistances:
     def __len__(self):
         return self.distance_tensor.numel()
 
+    def __getitem__(self, col):
+        if col == "distance":
+            return self.distance
+        if col == "w":
+            return self.w
+        raise KeyError(col)
+
     def to_pandas(self):
         return pd.DataFrame({"distance": self.distance.values,
                              "w": self.w.values})
@@ -171,7 +178,8 @@ class ColumnarPopulation:
         with the batch kernel."""
         if self.stats_T is None:
             raise ValueError("statistics of this population were not kept")
-        self.d, _, _ = distance.batch(self.stats_T, t, x_0, np.inf)
+        self.d, _, _ = distance.batch(self.stats_T, t, x_0, np.inf,
+                                      keys=self.stat_keys)
         return self.d
 
     def update_distances(self, distance_to_ground_truth):

@@ -6,8 +6,10 @@ The reference hands the sampler an opaque per-proposal closure
 (``_create_simulate_function``, smc.py:536-600).  :class:`pyabc_amd.ABCSMC`
 attaches a :class:`BatchSpec` to that closure; when the spec describes a
 configuration the device engine covers (one :class:`BatchModel`, uniform-box
-prior, :class:`MultivariateNormalTransition`, p-norm distance, uniform
-acceptance, one simulation per parameter), the generation runs through
+prior, :class:`MultivariateNormalTransition` / :class:`LocalTransition`,
+p-norm distance with uniform acceptance or an independent normal / Laplace
+kernel with the :class:`StochasticAcceptor`, one simulation per parameter),
+the generation runs through
 :mod:`pyabc_amd.engine`.  Otherwise the closure is called proposal by
 proposal with SingleCoreSampler semantics (user Python models), its
 transition / distance / epsilon calls still computing on the device.
@@ -16,9 +18,9 @@ import numpy as np
 import torch
 
 from .base import Sampler, Sample
-from ..distance import DeviceStats, PNormDistance
+from ..distance import DeviceStats, PNormDistance, _IndependentKernel
 from ..distributed import Comm
-from ..engine import GenerationEngine
+from ..engine import GenerationEngine, StochasticAcceptance
 from ..population import ColumnarPopulation
 from ..batch_models import BatchModel
 
@@ -42,6 +44,10 @@ class BatchSpec:
         self.summary_statistics = summary_statistics
         self.model_probabilities = model_probabilities
 
+    def stochastic(self):
+        from ..acceptor import StochasticAcceptor
+        return isinstance(self.acceptor, StochasticAcceptor)
+
     def unsupported_reason(self):
         from ..acceptor import UniformAcceptor
         from ..transition import MultivariateNormalTransition, LocalTransition
@@ -55,12 +61,20 @@ class BatchSpec:
             return "nr_samples_per_parameter != 1"
         if getattr(self.summary_statistics, "__name__", "") != "identity":
             return "custom summary_statistics"
-        if self.kind == "smc":
+        if self.kind == "smc" and self.stochastic():
+            if not isinstance(self.distance, _IndependentKernel):
+                return ("StochasticAcceptor kernel is not an Independent"
+                        "Normal/LaplaceKernel")
+            why = self.distance.batch_unsupported_reason(self.x_0)
+            if why is not None:
+                return why
+        elif self.kind == "smc":
             if not isinstance(self.distance, PNormDistance):
                 return "distance is not a (Adaptive)PNormDistance"
             if not isinstance(self.acceptor, UniformAcceptor) or \
                     self.acceptor.use_complete_history:
                 return "acceptor is not UniformAcceptor(current time)"
+        if self.kind == "smc":
             if self.t > 0 and not isinstance(
                     self.transitions[0],
                     (MultivariateNormalTransition, LocalTransition)):
@@ -72,10 +86,14 @@ class BatchSample(Sample):
     """Columnar sample: the accepted population on the device plus the
     recorded statistics (accepted and rejected, evaluation order)."""
 
-    def __init__(self, population, recorded, record_rejected, ok=True):
+    def __init__(self, population, recorded, record_rejected, ok=True,
+                 rec_particles=None):
         super().__init__(record_rejected=record_rejected, ok=ok)
         self.population = population
         self.recorded = recorded
+        # (theta [n_rec, d], distance [n_rec], accepted [n_rec]) of every
+        # recorded evaluation, for the temperature schemes' records
+        self.rec_particles = rec_particles
 
     @property
     def n_accepted(self):
@@ -156,16 +174,30 @@ class GPUBatchSampler(Sampler):
             # calibration distances are computed later (smc.py:516-534)
             res.d = torch.full_like(res.w, np.inf)
         else:
-            keys_d, x0d, fwd = spec.distance.device_params(spec.t, spec.x_0)
+            fit = spec.transitions[0].device_fit if spec.t > 0 and \
+                spec.transitions[0].device_fit is not None else None
+            if spec.stochastic():
+                keys_d, x0d, prmd, kind, c = spec.distance.device_params(
+                    spec.t, spec.x_0)
+                acceptance = StochasticAcceptance(
+                    x0d, prmd, kind, c, spec.acceptor.pdf_norms[spec.t],
+                    spec.eps(spec.t),
+                    spec.acceptor.apply_importance_weighting)
+                x0d = fwd = eps = None
+            else:
+                keys_d, x0d, fwd = spec.distance.device_params(spec.t,
+                                                               spec.x_0)
+                eps = spec.eps(spec.t)
+                acceptance = None
             if keys_d != keys:
                 perm = [keys.index(k) for k in keys_d]
                 model = _PermutedModel(model, perm)
                 eng.model = model
-            eps = spec.eps(spec.t)
-            fit = spec.transitions[0].device_fit if spec.t > 0 and \
-                spec.transitions[0].device_fit is not None else None
             res = eng.sample_generation(spec.t, n, fit, x0d, fwd, eps,
-                                        keep_stats=True, record=record)
+                                        keep_stats=True, record=record,
+                                        acceptance=acceptance,
+                                        record_particles=record and
+                                        acceptance is not None)
             eng.model = spec.models[0]
             keys = keys_d
         # the engine returns the global population, identical on every rank
@@ -176,7 +208,10 @@ class GPUBatchSampler(Sampler):
         self.last_timers = dict(eng.timers)
         pop = ColumnarPopulation(res.theta, res.w, res.d, names,
                                  res.stats_T, keys)
-        return BatchSample(pop, rec, record)
+        recp = None
+        if getattr(res, "rec_theta", None) is not None:
+            recp = (res.rec_theta, res.rec_d, res.rec_acc)
+        return BatchSample(pop, rec, record, rec_particles=recp)
 
     def _closure_path(self, n, simulate_one, max_eval):
         nr = 0

@@ -13,6 +13,7 @@ import logging
 
 import numpy as np
 import pandas as pd
+import torch
 
 from .acceptor import UniformAcceptor, SimpleFunctionAcceptor
 from .distance import PNormDistance, to_distance
@@ -26,6 +27,7 @@ from .sampler import GPUBatchSampler
 from .sampler.gpu import BatchSpec
 from .storage import History
 from .transition import MultivariateNormalTransition
+from .temperature import DeviceRecords, TemperatureBase
 from .weighted_statistics import effective_sample_size
 
 logger = logging.getLogger("ABC")
@@ -153,9 +155,9 @@ class ABCSMC:
         def get_initial_records():
             pop = _pop_with_distances()
             if isinstance(pop, ColumnarPopulation):
-                d = pop.d.cpu().numpy()
-                return [{"distance": x, "transition_pd_prev": 1.0,
-                         "transition_pd": 1.0, "accepted": True} for x in d]
+                # dummy densities 1 (only their quotient matters)
+                zero = torch.zeros_like(pop.d)
+                return DeviceRecords(pop.d, zero, zero, zero + 1.0)
             return [{"distance": d, "transition_pd_prev": 1.0,
                      "transition_pd": 1.0, "accepted": True}
                     for p in pop.get_list() for d in p.accepted_distances]
@@ -342,8 +344,11 @@ class ABCSMC:
     def run(self, minimum_epsilon=None, max_nr_populations=np.inf,
             min_acceptance_rate=0.):
         """Generation loop (smc.py:796-940)."""
-        self.minimum_epsilon = 0.0 if minimum_epsilon is None \
-            else minimum_epsilon
+        if minimum_epsilon is None:
+            # a temperature schedule stops at T = 1 (smc.py:843-847)
+            minimum_epsilon = 1.0 if isinstance(self.eps, TemperatureBase) \
+                else 0.0
+        self.minimum_epsilon = minimum_epsilon
         self.max_nr_populations = max_nr_populations
         self.min_acceptance_rate = min_acceptance_rate
         t0 = self.history.max_t + 1
@@ -421,6 +426,8 @@ class ABCSMC:
                              acceptance_rate)
 
         def get_all_records():
+            if getattr(sample, "rec_particles", None) is not None:
+                return self._device_records(t, sample, prev_transitions)
             recorded = sample.first_m_particles(self.max_nr_recorded_particles)
             tp_prev = self._create_transition_pdf(t - 1, prev_transitions)
             tp = self._create_transition_pdf(t)
@@ -437,6 +444,30 @@ class ABCSMC:
 
         self.eps.update(t, get_weighted_distances, get_all_records,
                         acceptance_rate, self.acceptor.get_epsilon_config(t))
+
+    def _device_records(self, t, sample, prev_transitions):
+        """get_all_records of a device generation (smc.py:990-1017): the
+        previous and current transition log-densities of every recorded
+        evaluation by the device KDE pass (or the prior's, at t - 1 = 0)."""
+        theta, d, acc = sample.rec_particles
+        m = int(self.max_nr_recorded_particles) if np.isfinite(
+            self.max_nr_recorded_particles) else theta.shape[0]
+        theta, d, acc = theta[:m], d[:m], acc[:m]
+        return DeviceRecords(d, self._log_transition_pd(t - 1, prev_transitions,
+                                                        theta),
+                             self._log_transition_pd(t, self.transitions,
+                                                     theta), acc)
+
+    def _log_transition_pd(self, t, transitions, theta):
+        if t == 0:
+            # prior density: constant on the (uniform-box) support, where
+            # every recorded proposal lies (smc.py:737-749)
+            names = self.parameter_priors[0].uniform_box()[0]
+            par = Parameter(dict(zip(names, theta[0].cpu().numpy())))
+            pd0 = self._create_prior_pdf()(0, par)
+            return torch.full((theta.shape[0],), float(np.log(pd0)),
+                              dtype=theta.dtype, device=theta.device)
+        return transitions[0].logpdf_device(theta)
 
     def _adapt_population_size(self, t):
         if t == 0:

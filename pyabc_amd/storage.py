@@ -10,6 +10,7 @@ import numpy as np
 import pandas as pd
 
 from .population import ColumnarPopulation
+from .acceptor import save_dict_to_json, load_dict_from_json  # noqa: F401
 
 _REGISTRY = {}
 
@@ -128,6 +129,13 @@ class History:
         if hasattr(w, "cpu"):
             w = w.cpu().numpy()
         return df, np.asarray(w)
+
+
+def create_sqlite_db_id(dir_=None, file_="pyabc_test.db"):
+    """A fresh in-memory history id (history.py:57-75 names a sqlite file;
+    the in-memory History only needs a unique key)."""
+    import uuid
+    return f"sqlite:///{dir_ or '/tmp'}/{uuid.uuid4().hex}_{file_}"
 
 
 def is_columnar(pop):

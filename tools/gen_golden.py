@@ -355,5 +355,212 @@ def gen_e2e():
 GENS["e2e"] = gen_e2e
 
 
+# --------------------------------------------------------------------------
+# (f3) exact inference: stochastic kernels, acceptor, temperature schemes
+# --------------------------------------------------------------------------
+def gen_stochastic():
+    from pyabc.distance import (IndependentNormalKernel,
+                                IndependentLaplaceKernel, NormalKernel,
+                                SimpleFunctionKernel, SCALE_LIN, SCALE_LOG)
+    from pyabc.acceptor import StochasticAcceptor, pdf_norm_from_kernel
+    rng = np.random.default_rng(31)
+    for S, B in [(100, 400), (300, 120), (5, 200)]:
+        keys = [f"s{k:03d}" for k in range(S)]
+        x0v = rng.normal(size=S)
+        X = x0v[None, :] + rng.normal(size=(B, S)) * rng.uniform(0.2, 3, S)
+        var = rng.uniform(0.1, 4.0, S)
+        scale = rng.uniform(0.1, 4.0, S)
+        x0 = dict(zip(keys, x0v))
+        kn = IndependentNormalKernel(var=var)
+        kn.initialize(0, None, x0)
+        kl = IndependentLaplaceKernel(scale=scale)
+        kl.initialize(0, None, x0)
+        rows = [dict(zip(keys, r)) for r in X]
+        ln = np.array([kn(x, x0) for x in rows])
+        ll = np.array([kl(x, x0) for x in rows])
+        save(f"stoch_kernel_S{S}", X=X, x0=x0v, var=var, scale=scale,
+             normal=ln, laplace=ll, normal_pdf_max=kn.pdf_max,
+             laplace_pdf_max=kl.pdf_max,
+             _ref=np.array("distance/kernel.py:256-282 "
+                           "(IndependentNormalKernel), :332-357 "
+                           "(IndependentLaplaceKernel); keys sorted"))
+    # NormalKernel (full covariance, scipy multivariate_normal), S=6
+    S, B = 6, 200
+    keys = [f"s{k}" for k in range(S)]
+    L = np.tril(rng.normal(size=(S, S))) + 2 * np.eye(S)
+    cov = L @ L.T
+    x0v = rng.normal(size=S)
+    X = x0v[None, :] + rng.normal(size=(B, S)) * 2
+    x0 = dict(zip(keys, x0v))
+    out = {}
+    for scale_name in ["log", "lin"]:
+        k = NormalKernel(cov=cov, ret_scale=SCALE_LOG if scale_name == "log"
+                         else SCALE_LIN)
+        k.initialize(0, None, x0)
+        out[f"normal_full_{scale_name}"] = np.array(
+            [k(dict(zip(keys, r)), x0) for r in X])
+        out[f"pdf_max_{scale_name}"] = k.pdf_max
+    save("stoch_kernel_full", X=X, x0=x0v, cov=cov, **out,
+         _ref=np.array("distance/kernel.py:108-187 (NormalKernel)"))
+    # StochasticAcceptor.__call__ on given densities, both scales
+    B = 3000
+    res = {}
+    for scale_name, sc in [("log", SCALE_LOG), ("lin", SCALE_LIN)]:
+        if scale_name == "log":
+            pdv = rng.normal(-5, 3, size=B)
+            pdf_max = -1.0
+        else:
+            pdv = np.exp(rng.normal(-2, 1.5, size=B))
+            pdf_max = 0.4
+        kern = SimpleFunctionKernel(lambda x, x_0, t, par: x["pd"],
+                                    ret_scale=sc, pdf_max=pdf_max)
+        for temp in [1.0, 3.7]:
+            for iw in [True, False]:
+                acc = StochasticAcceptor(pdf_norm_method=pdf_norm_from_kernel,
+                                         apply_importance_weighting=iw)
+                acc.initialize(0, lambda: None, kern, {})
+                np.random.seed(77)
+                r = [acc(kern, lambda t: temp, {"pd": p}, {}, 0, None)
+                     for p in pdv]
+                np.random.seed(77)
+                u = np.random.uniform(0, 1, size=B)
+                tag = f"{scale_name}_T{temp}_iw{int(iw)}"
+                res[f"accept_{tag}"] = np.array([x.accept for x in r])
+                res[f"weight_{tag}"] = np.array([x.weight for x in r])
+                res[f"u_{tag}"] = u
+        res[f"pd_{scale_name}"] = pdv
+        res[f"pdf_max_{scale_name}"] = pdf_max
+    save("stoch_accept", **res,
+         _ref=np.array("acceptor/acceptor.py:440-473 "
+                       "(StochasticAcceptor.__call__), pdf_norm.py:6-14"))
+
+
+def gen_temperature():
+    import pyabc.epsilon as E
+    from pyabc.distance import SCALE_LOG, SCALE_LIN
+    from pyabc.acceptor import pdf_norm_max_found, ScaledPDFNorm
+    rng = np.random.default_rng(41)
+    n = 5000
+    pds = rng.normal(-20, 6, size=n)
+    tpp = np.exp(rng.normal(0, 1, size=n))
+    tp = tpp * np.exp(rng.normal(0, 0.3, size=n))
+    acc_flag = rng.random(n) < 0.3
+    records = [dict(distance=a, transition_pd_prev=b, transition_pd=c,
+                    accepted=bool(f)) for a, b, c, f in
+               zip(pds, tpp, tp, acc_flag)]
+    wd = pd.DataFrame({"distance": pds[:2000],
+                       "w": rng.uniform(0.2, 1.0, 2000)})
+    out = dict(pds=pds, tpp=tpp, tp=tp, wd_d=wd.distance.values,
+               wd_w=wd.w.values)
+    pdf_norm = float(np.max(pds))
+    for rate in [0.3, 0.05, 0.9]:
+        for sc in ["log", "lin"]:
+            if sc == "log":
+                args = dict(pdf_norm=pdf_norm, kernel_scale=SCALE_LOG)
+                recs = records
+            else:
+                lin = np.exp(pds / 10)
+                recs = [dict(r, distance=v) for r, v in zip(records, lin)]
+                args = dict(pdf_norm=float(lin.max()), kernel_scale=SCALE_LIN)
+            s = E.AcceptanceRateScheme(target_rate=rate)
+            out[f"accrate_{rate}_{sc}"] = s(
+                t=1, get_weighted_distances=lambda: wd,
+                get_all_records=lambda: recs, max_nr_populations=10,
+                prev_temperature=50., acceptance_rate=0.3, **args)
+    # obj(0) > 0 (T = 1) and the numerics-limit branch
+    s = E.AcceptanceRateScheme(target_rate=0.3)
+    out["accrate_norm_min"] = s(
+        t=1, get_weighted_distances=lambda: wd,
+        get_all_records=lambda: records, max_nr_populations=10,
+        pdf_norm=float(np.min(pds)), kernel_scale=SCALE_LOG,
+        prev_temperature=50., acceptance_rate=0.3)
+    base = dict(get_weighted_distances=lambda: wd,
+                get_all_records=lambda: records, pdf_norm=pdf_norm,
+                kernel_scale=SCALE_LOG)
+    for t, prev, rate in [(1, 50., 0.4), (3, 12.5, 1e-5), (2, 7.3, 0.7)]:
+        for name, sch in [("expiter", E.ExpDecayFixedIterScheme()),
+                          ("expratio", E.ExpDecayFixedRatioScheme()),
+                          ("poly", E.PolynomialDecayFixedIterScheme()),
+                          ("daly", E.DalyScheme()),
+                          ("friel", E.FrielPettittScheme()),
+                          ("ess", E.EssScheme())]:
+            out[f"{name}_t{t}"] = sch(t=t, max_nr_populations=6,
+                                      prev_temperature=prev,
+                                      acceptance_rate=rate, **base)
+    # a full Temperature sequence (default schemes) over 5 generations
+    temp = E.Temperature()
+    cfg = dict(pdf_norm=pdf_norm, kernel_scale=SCALE_LOG)
+    temp.initialize(0, lambda: wd, lambda: records, 5, cfg)
+    seq = [temp(0)]
+    for t, rate in zip(range(1, 5), [0.5, 0.2, 0.1, 0.05]):
+        temp.update(t, lambda: wd, lambda: records, rate, cfg)
+        seq.append(temp(t))
+    out["temperature_seq"] = np.array(seq)
+    # pdf norms
+    out["pdfnorm_maxfound"] = pdf_norm_max_found(
+        prev_pdf_norm=-3.0, get_weighted_distances=lambda: wd)
+    sp_ = ScaledPDFNorm()
+    out["pdfnorm_scaled_hi"] = sp_(prev_pdf_norm=-30.0,
+                                   get_weighted_distances=lambda: wd,
+                                   prev_temp=5.0, acceptance_rate=0.5)
+    out["pdfnorm_scaled_lo"] = sp_(prev_pdf_norm=-30.0,
+                                   get_weighted_distances=lambda: wd,
+                                   prev_temp=5.0, acceptance_rate=0.01)
+    save("temperature", **out,
+         _ref=np.array("epsilon/temperature.py:45-742, "
+                       "acceptor/pdf_norm.py:17-110"))
+
+
+GENS["stochastic"] = gen_stochastic
+GENS["temperature"] = gen_temperature
+
+
+def gen_e2e_stochastic():
+    """Exact-inference run: noise-free linear model y = A theta, Gaussian
+    likelihood via IndependentNormalKernel(var), StochasticAcceptor,
+    Temperature (smc.py:796-1022 with acceptor/acceptor.py:309-473,
+    epsilon/temperature.py:45-345)."""
+    from pyabc.sampler import SingleCoreSampler
+    from pyabc.distance import IndependentNormalKernel
+    from pyabc.acceptor import StochasticAcceptor
+    from pyabc.epsilon import Temperature
+    d, S, var = 2, 10, 0.25
+    A = np.random.RandomState(11).randn(S, d)
+    th_true = np.array([0.8, -0.4])
+    x0v = A @ th_true + np.sqrt(var) * np.random.RandomState(12).randn(S)
+    keys = [f"y{k:02d}" for k in range(S)]
+    names = [f"p{k}" for k in range(d)]
+    x0 = dict(zip(keys, x0v))
+    res = {}
+    for r in range(3):
+        np.random.seed(300 + r)
+
+        def model(par):
+            th = np.array([par[n] for n in names])
+            return dict(zip(keys, A @ th))
+        prior = pyabc.Distribution(**{n: pyabc.RV("uniform", -5, 10)
+                                      for n in names})
+        abc = pyabc.ABCSMC(model, prior, IndependentNormalKernel(var=var),
+                           population_size=1000, eps=Temperature(),
+                           acceptor=StochasticAcceptor(),
+                           sampler=SingleCoreSampler())
+        abc.new("sqlite://", x0)
+        h = abc.run(max_nr_populations=6)
+        st, eps, nsim = _run_stats(h, names)
+        res[f"mean_{r}"] = np.array([s_[0] for s_ in st])
+        res[f"std_{r}"] = np.array([s_[1] for s_ in st])
+        res[f"ess_{r}"] = np.array([s_[2] for s_ in st])
+        res[f"temp_{r}"] = eps
+        res[f"nsim_{r}"] = nsim
+        print(f"    seed {r}: T {eps} mean {st[-1][0]} std {st[-1][1]}")
+    save("e2e_stochastic", A=A, x0=x0v, var=var, theta_true=th_true, **res,
+         _ref=np.array("pyabc/smc.py:796-1022 with StochasticAcceptor + "
+                       "Temperature + IndependentNormalKernel, "
+                       "SingleCoreSampler"))
+
+
+GENS["e2e_stochastic"] = gen_e2e_stochastic
+
+
 if __name__ == "__main__":
     _main()

@@ -60,13 +60,27 @@ def _generation(comm, n, min_batch, record):
     th, dd, ww, n_eval, _ = eng.gather_population(res)
     eps1 = float(K.weighted_quantile(dd, ww, 0.5)[0].item())
     fit1 = DeviceMVNFit(th, ww)
+    # exact-inference generation: stochastic acceptance with u keyed by the
+    # global evaluation id, acceptance weights, particle records
+    from pyabc_amd.engine import StochasticAcceptance
+    var = torch.full((S,), 0.25, dtype=torch.float64, device="cuda")
+    c = float(np.sum(np.log(2) + np.log(np.pi) + np.log(np.full(S, 0.25))))
+    acc = StochasticAcceptance(x0, var, K.KERNEL_NORMAL, c, -0.5 * c, 20.0)
+    rs = eng.sample_generation(2, n, fit1, None, None, None, keep_stats=False,
+                               record=False, acceptance=acc,
+                               record_particles=True)
     return dict(theta0=theta.cpu().numpy(), eps0=eps, theta=th.cpu().numpy(),
                 d=dd.cpu().numpy(), w=ww.cpu().numpy(),
                 logpd=res.logpd.cpu().numpy(), n_eval=int(n_eval),
                 stats=res.stats_T.cpu().numpy(),
                 rec=None if res.rec_stats_T is None
                 else res.rec_stats_T.cpu().numpy(),
-                eps1=eps1, cov1=fit1.cov)
+                eps1=eps1, cov1=fit1.cov,
+                s_theta=rs.theta.cpu().numpy(), s_d=rs.d.cpu().numpy(),
+                s_w=rs.w.cpu().numpy(), s_accw=rs.accw.cpu().numpy(),
+                s_rec_theta=rs.rec_theta.cpu().numpy(),
+                s_rec_d=rs.rec_d.cpu().numpy(),
+                s_rec_acc=rs.rec_acc.cpu().numpy(), s_n_eval=int(rs.n_eval))
 
 
 def _rank_main(rank, world, port, n, out):
@@ -90,7 +104,9 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     """Global-id sampling (engine.sample_generation): two ranks sharing
     cuda:0 over gloo produce exactly the population, distances, weights,
     evaluation count, recorded statistics, next epsilon and next fit that
-    one rank produces -- with different sampling-round sizes too."""
+    one rank produces -- with different sampling-round sizes too; and the
+    same for a stochastic-acceptance generation (acceptance weights and
+    particle records)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 6001          # odd: uneven row slices for the weight pass
@@ -103,10 +119,19 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     for r in (0, 1):
         got = res[r]
         for k in ("theta0", "theta", "d", "w", "logpd", "stats", "rec",
-                  "cov1"):
+                  "cov1", "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta",
+                  "s_rec_d", "s_rec_acc"):
             np.testing.assert_array_equal(got[k], one[k], err_msg=k)
-        for k in ("eps0", "eps1", "n_eval"):
+        for k in ("eps0", "eps1", "n_eval", "s_n_eval"):
             assert got[k] == one[k], k
+    # stochastic generation: records are every evaluation up to the n-th
+    # acceptance, the accepted ones in order are the population
+    assert one["s_rec_d"].shape[0] == one["s_n_eval"] > n
+    acc = one["s_rec_acc"] > 0
+    assert acc.sum() == n
+    np.testing.assert_array_equal(one["s_rec_theta"][acc], one["s_theta"])
+    np.testing.assert_array_equal(one["s_rec_d"][acc], one["s_d"])
+    assert np.all(one["s_accw"] >= 1.0)
     assert one["theta"].shape == (n, 4)
     assert one["rec"].shape[1] == one["n_eval"] >= n
     assert np.all(one["d"] <= one["eps0"])

@@ -108,9 +108,31 @@ def c5(N=1_000_000, gens=10):
         max_nr_populations=gens)
 
 
+def x1(N=100_000, gens=6):
+    """Exact inference: noise-free C2 model, Gaussian
+    likelihood IndependentNormalKernel(var=0.25), StochasticAcceptor,
+    Temperature() (AcceptanceRateScheme over all recorded evaluations:
+    two device KDE passes per generation)."""
+    A, th, x0, keys, names = linear_problem(4, 100, 2.0)
+    model = pa.LinearGaussianModel(A, None, 0.0, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=0.25),
+                    population_size=N, eps=pa.Temperature(),
+                    acceptor=pa.StochasticAcceptor(),
+                    sampler=pa.GPUBatchSampler(seed=6))
+    out = run("x1_exact_inference_N1e5_d4_S100", abc, dict(zip(keys, x0)),
+              names, th, max_nr_populations=gens)
+    P = A.T @ A / 0.25
+    post = np.linalg.solve(P, A.T @ x0 / 0.25)
+    print(json.dumps({"config": "x1_exact_posterior_mean",
+                      "analytic": post.tolist(),
+                      "abc": out["posterior_mean"]}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", nargs="*", default=["c1", "c2", "c4", "c5"])
+    ap.add_argument("--only", nargs="*",
+                    default=["c1", "c2", "c4", "c5", "x1"])
     args = ap.parse_args()
     torch.cuda.set_device(0)
     for c in args.only:

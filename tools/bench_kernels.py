@@ -137,6 +137,22 @@ def main():
     report("pnorm_distance_f64", t, B, "particles", 8 * S + 10, "hbm",
            {"S": S})
 
+    # ------- (f3) exact inference: kernel density + stochastic acceptance --
+    var = torch.full((S,), 0.25, dtype=F64, device="cuda")
+    c = float(np.sum(np.log(2) + np.log(np.pi) + np.log(np.full(S, 0.25))))
+    t = timed(lambda: K.stochastic_kernel(stats, x0, var, K.KERNEL_NORMAL, c,
+                                          pdf_norm=-50.0, inv_temp=0.1,
+                                          seed=1, stream=9))
+    # stats 8S + pd 8 + accept 1 + weight 8 + guard 1 (u is in-kernel Philox)
+    report("stochastic_kernel_accept_f64", t, B, "evaluations", 8 * S + 18,
+           "hbm", {"S": S})
+    pdv = dd.clone()
+    lnum = torch.randn(B, dtype=F64, device="cuda", generator=g)
+    lden = torch.randn(B, dtype=F64, device="cuda", generator=g)
+    t = timed(lambda: K.tempered_sums(pdv, 30.0, [0.5], logw_num=lnum,
+                                      logw_den=lden))
+    report("tempered_sums_f64", t, B, "records", 24, "hbm", {"K": 1})
+
     # ---------------- (a6) adaptive scales --------------------------------
     for n in (200_000, 2_000_000 // q):
         data = stats[:, :n].contiguous() if n <= B else torch.randn(

@@ -119,6 +119,33 @@ int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
                        int64_t npad, int d, const double* lw2max,
                        double log_const, double* out_logpd, void* ws,
                        size_t ws_bytes, hipStream_t stream);
+/* Same density on the matrix cores (v_mfma_f32_32x32x16_bf16): the
+ * exponent lw2_j - |y_i - y_j|^2 is expanded as a_j + b_i + 2 y_i.y_j with
+ * every operand split into bf16 pieces on a power-of-two grid so that the
+ * large part of the sum is EXACT in the fp32 accumulator.
+ * Afr: population fragments (abc_kde_mfma_prev_bytes), built with the
+ * direct P by abc_kde_pack_prev_mfma (which also writes lw2max and the grid
+ * g to gscale; ws >= 128 B).  Bfr: new-row fragments
+ * (abc_kde_mfma_new_bytes, abc_kde_mfma_new_rows padded rows) and the direct
+ * fp32 rows Ynew [M][D] (used by the exact underflow fixup), built by
+ * abc_kde_pack_new_mfma from theta.  Workspace: abc_kde_workspace_bytes.
+ *                                          multivariatenormal.py:102-125 */
+size_t abc_kde_mfma_prev_bytes(int64_t npad, int d);
+int64_t abc_kde_mfma_new_rows(int64_t M, int d);
+size_t abc_kde_mfma_new_bytes(int64_t M, int d);
+int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
+                           const double* mu, const double* Us, float* P,
+                           void* Afr, int64_t npad, double* lw2max,
+                           double* gscale, void* ws, hipStream_t stream);
+int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
+                          const double* mu, const double* Us,
+                          const double* gscale, float* Ynew, void* Bfr,
+                          hipStream_t stream);
+int abc_kde_logpdf_mfma(const void* Bfr, const float* Ynew, int64_t M,
+                        const void* Afr, const float* P, int64_t npad, int d,
+                        const double* lw2max, double log_const,
+                        double* out_logpd, void* ws, size_t ws_bytes,
+                        hipStream_t stream);
 /* w = prior_pd / exp(logpd)                          smc.py:776-792
  * prior may be NULL (then prior_const is used for every row) */
 int abc_importance_weights_f64(const double* logpd, const double* prior,

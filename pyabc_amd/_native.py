@@ -77,6 +77,17 @@ _SIGS = {
                                    c_dbl, c_ptr, c_ptr, c_size, c_ptr]),
     "abc_kde_logpdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_i64, c_int, c_ptr,
                                    c_dbl, c_ptr, c_ptr, c_size, c_ptr]),
+    "abc_kde_mfma_prev_bytes": (c_size, [c_i64, c_int]),
+    "abc_kde_mfma_new_rows": (c_i64, [c_i64, c_int]),
+    "abc_kde_mfma_new_bytes": (c_size, [c_i64, c_int]),
+    "abc_kde_pack_prev_mfma": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
+                                       c_ptr, c_ptr, c_ptr, c_i64, c_ptr,
+                                       c_ptr, c_ptr, c_ptr]),
+    "abc_kde_pack_new_mfma": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                      c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_kde_logpdf_mfma": (c_int, [c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                    c_int, c_ptr, c_dbl, c_ptr, c_ptr, c_size,
+                                    c_ptr]),
     "abc_importance_weights_f64": (c_int, [c_ptr, c_ptr, c_dbl, c_i64, c_ptr,
                                            c_ptr]),
     # (a4)

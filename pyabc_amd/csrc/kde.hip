@@ -35,6 +35,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "kde_internal.hpp"
 
 namespace abc {
 
@@ -570,6 +571,43 @@ static int pack_dispatch(const double* X, const double* w, int64_t n, int d,
   }
   ABC_LAUNCH_CHECK("pack_prev_kernel");
   return kOk;
+}
+
+// shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum,
+// underflow detection and exact fixup of the fp32 paths
+int kde_finish_f32(const double* partial, int64_t M, int nseg,
+                   const float* Ynew, const float* P, int64_t npad, int d,
+                   const double* lw2max, double log_const, double* out_logpd,
+                   int* n_fix, int* fix_rows, hipStream_t stream) {
+  hipLaunchKernelGGL((kde_finalize_kernel<float>), dim3(ceil_div(M, 256)),
+                     dim3(256), 0, stream, partial, M, nseg, lw2max,
+                     log_const, out_logpd, n_fix, fix_rows);
+  ABC_LAUNCH_CHECK("kde_finalize_kernel");
+  switch (padded_dim(d)) {
+#define CASE(DD)                                                             \
+  case DD:                                                                   \
+    hipLaunchKernelGGL((kde_fixup_kernel<float, DD>), dim3(64), dim3(256), 0, \
+                       stream, Ynew, P, npad, lw2max, log_const, n_fix,      \
+                       fix_rows, out_logpd);                                 \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default:
+      set_error("kde: unsupported dimension d=%d (max 32)", d);
+      return kUnsupported;
+  }
+  ABC_LAUNCH_CHECK("kde_fixup_kernel");
+  return kOk;
+}
+
+int kde_padded_dim(int d) { return padded_dim(d); }
+int kde_num_segments(int64_t npad) { return kde_segments(npad); }
+int kde_pack_direct_f32(const double* X, const double* w, int64_t n, int d,
+                        const double* mu, const double* Us, float* P,
+                        int64_t npad, double* lw2max, void* ws,
+                        hipStream_t st) {
+  return pack_dispatch<float>(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
 }
 
 }  // namespace abc

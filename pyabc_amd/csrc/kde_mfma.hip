@@ -1,0 +1,580 @@
+// KDE importance-weight pass on the matrix cores: exact-grid bf16 MFMA.
+// Same quantity as kde.hip (MultivariateNormalTransition.pdf, reference
+// pyabc/transition/multivariatenormal.py:102-125 via smc.py:722-733):
+//
+//   pd(theta_i) = exp(c) * sum_j 2^(e_ij),  e_ij = lw2_j - |y_i - y_j|^2
+//
+// expanded as e_ij = a_j + b_i + 2 y_i.y_j with a_j = lw2_j - |y_j|^2 and
+// b_i = -|y_i|^2.  The expansion cancels catastrophically in fp32 (a plain
+// fp32 GEMM form loses 4e-5 relative at N = 1e6, d = 8), so every operand is
+// split into bf16 pieces that make the large part of the sum EXACT:
+//
+//   y = y1 + y2 + y3   y1 = g*rint(y/g) on a fixed power-of-two grid g with
+//                      |y1/g| <= 256 (8 significant bits: exact in bf16),
+//                      y2 = bf16(y - y1), y3 = bf16(y - y1 - y2)
+//   a = aH0 + aH1 + aH2 + aL0 + aL1   (aH* bf16 multiples of G = g^2 holding
+//                      rint(a/G)*G exactly, aL* = bf16 pieces of the rest)
+//
+// hi = sum_k 2 y1_ik y1_jk + aH + bH is a sum of multiples of G below
+// 2^24 G, so the fp32 MFMA accumulation is exact in ANY order; lo (the
+// seven y1/y2/y3 cross products per dimension + aL + bL) is small (|lo| <~
+// 4) and accumulates with ~1e-7 absolute error.  e = hi + lo is rounded
+// once, so the exponent carries one fp32 rounding at |e| -- tighter than
+// the direct fp32 difference form of kde.hip (max 9e-6 vs 3e-5 relative on
+// rows far outside the population, SURVEY 8(a3) tolerance 1e-5).
+//
+// MFMA mapping (v_mfma_f32_32x32x16_bf16): A = previous population (rows =
+// j), B = new rows (columns = i), K = the piece slots.  KH chunks of 16
+// slots feed the hi accumulator, KL chunks the lo accumulator; each lane
+// owns one new row (column lane&31) and 16 j's of the 32-row tile, so per
+// pair the VALU does only  v_add (hi+lo), v_exp_f32, v_add (row sum).
+// The j-range uses kde.hip's fixed segments, each lane's values are summed in
+// register order and the two lane halves combined in a fixed order, so a
+// row's bits are independent of M, of the launch shape and of the number of
+// ranks.  Rows whose sum underflows -- and new rows outside the grid range
+// (|y| > 256 g, flagged by b = -inf) -- go through kde.hip's exact fixup.
+#include <cmath>
+
+#include "common.hpp"
+#include "kde_internal.hpp"
+
+namespace abc {
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr double kLwFloor = -160.0;  // 2^-160 is 0 in fp32: no term changes
+constexpr int kWaves = 4;            // waves per block
+
+template <int D>
+struct Mk {
+  static constexpr int KH = (D + 6 + 15) / 16;      // y1.y1, aH x3, bH x3
+  static constexpr int KL = (7 * D + 4 + 15) / 16;  // 7 cross terms, aL, bL
+  static constexpr int KT = KH + KL;
+  static constexpr int IB = D <= 8 ? 4 : (D <= 24 ? 2 : 1);  // i-tiles/wave
+};
+
+__device__ inline unsigned short bf16_rne(float x) {
+  unsigned u = __float_as_uint(x);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return static_cast<unsigned short>(u >> 16);
+}
+__device__ inline unsigned short bf16_trunc(float x) {
+  return static_cast<unsigned short>(__float_as_uint(x) >> 16);
+}
+__device__ inline float bf16_f(unsigned short b) {
+  return __uint_as_float(static_cast<unsigned>(b) << 16);
+}
+constexpr unsigned short kBf16One = 0x3F80;
+constexpr unsigned short kBf16NegInf = 0xFF80;
+
+// y -> (y1, y2, y3) bf16 bits, scaled by `side` (1 for the population, 2 for
+// new rows: exact); returns |y1 + y2 + y3|^2 (the represented point)
+template <int D>
+__device__ inline double split_row(const double* y, double g, float side,
+                                   unsigned short* y1, unsigned short* y2,
+                                   unsigned short* y3) {
+  double n2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double v1 = rint(y[k] / g) * g;
+    const double r = y[k] - v1;
+    const unsigned short b2 = bf16_rne(static_cast<float>(r));
+    const double v2 = bf16_f(b2);
+    const unsigned short b3 = bf16_rne(static_cast<float>(r - v2));
+    const double v3 = bf16_f(b3);
+    y1[k] = bf16_rne(side * static_cast<float>(v1));
+    y2[k] = bf16_rne(side * static_cast<float>(v2));
+    y3[k] = bf16_rne(side * static_cast<float>(v3));
+    const double yt = v1 + v2 + v3;
+    n2 = fma(yt, yt, n2);
+  }
+  return n2;
+}
+
+// v -> three bf16 multiples of G summing to rint(v/G)*G exactly, plus two
+// bf16 pieces of the remainder (|rem| <= G/2)
+__device__ inline void split_value(double v, double G, unsigned short* h,
+                                   unsigned short* l) {
+  double q = rint(v / G);
+  q = fmin(fmax(q, -8388607.0), 8388607.0);  // |q| < 2^23 (bounds in DESIGN)
+  const float qf = static_cast<float>(q);     // exact integer
+  const unsigned short h0 = bf16_trunc(qf);
+  const float r1 = qf - bf16_f(h0);
+  const unsigned short h1 = bf16_trunc(r1);
+  const float r2 = r1 - bf16_f(h1);
+  const unsigned short h2 = bf16_trunc(r2);  // r2 - h2 == 0
+  const float Gf = static_cast<float>(G);
+  h[0] = bf16_rne(bf16_f(h0) * Gf);
+  h[1] = bf16_rne(bf16_f(h1) * Gf);
+  h[2] = bf16_rne(bf16_f(h2) * Gf);
+  const double lo = v - q * G;  // exact (Sterbenz / q == 0)
+  const unsigned short l0 = bf16_rne(static_cast<float>(lo));
+  l[0] = l0;
+  l[1] = bf16_rne(static_cast<float>(lo - static_cast<double>(bf16_f(l0))));
+}
+
+// Slot k of the population (A) and new-row (B) operands.
+//  hi  k < D: y1 | 2y1        k = D..D+2: aH | 1     k = D+3..D+5: 1 | bH
+//  lo  k' = 7m + q (m < D):   q: 0 y2|2y1  1 y3|2y1  2 y1|2y2  3 y1|2y3
+//                                4 y2|2y2  5 y3|2y2  6 y2|2y3
+//      k' = 7D, 7D+1: aL | 1  k' = 7D+2, 7D+3: 1 | bL
+template <int D, bool kA>
+__device__ inline unsigned short slot(int k, const unsigned short* y1,
+                                      const unsigned short* y2,
+                                      const unsigned short* y3,
+                                      const unsigned short* h,
+                                      const unsigned short* l) {
+  constexpr int KH = Mk<D>::KH;
+  if (k < 16 * KH) {
+    if (k < D) return y1[k];
+    if (k < D + 3) return kA ? h[k - D] : kBf16One;
+    if (k < D + 6) return kA ? kBf16One : h[k - D - 3];
+    return 0;
+  }
+  const int kk = k - 16 * KH;
+  if (kk < 7 * D) {
+    const int m = kk / 7, q = kk % 7;
+    if (kA) {
+      switch (q) {
+        case 0: case 4: case 6: return y2[m];
+        case 1: case 5: return y3[m];
+        default: return y1[m];
+      }
+    } else {
+      switch (q) {
+        case 0: case 1: return y1[m];
+        case 2: case 4: case 5: return y2[m];
+        default: return y3[m];
+      }
+    }
+  }
+  if (kk < 7 * D + 2) return kA ? l[kk - 7 * D] : kBf16One;
+  if (kk < 7 * D + 4) return kA ? kBf16One : l[kk - 7 * D - 2];
+  return 0;
+}
+
+// fragment layout [tile][chunk c][lane][8]: lane = 32h + (particle % 32),
+// element e = slot 16c + 8h + e
+template <int D, bool kA>
+__device__ inline void store_frags(bf16x8* __restrict__ F, int64_t p,
+                                   const unsigned short* y1,
+                                   const unsigned short* y2,
+                                   const unsigned short* y3,
+                                   const unsigned short* h,
+                                   const unsigned short* l) {
+  constexpr int KT = Mk<D>::KT;
+  const int64_t tile = p >> 5;
+  const int r = static_cast<int>(p & 31);
+#pragma unroll
+  for (int c = 0; c < KT; ++c) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = static_cast<short>(slot<D, kA>(16 * c + 8 * hh + e, y1, y2, y3, h, l));
+      F[(tile * KT + c) * 64 + 32 * hh + r] = v;
+    }
+  }
+}
+
+template <int D>
+__device__ inline void whiten_row(const double* __restrict__ X, int64_t i,
+                                  int d, const double* __restrict__ mu,
+                                  const double* __restrict__ Us, double* y) {
+  double xc[D];
+#pragma unroll
+  for (int l = 0; l < D; ++l) xc[l] = l < d ? X[i * d + l] - mu[l] : 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < D; ++l)
+      if (l < d && k < d) acc = fma(xc[l], Us[l * d + k], acc);
+    y[k] = acc;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ymax_kernel(
+    const double* __restrict__ X, int64_t n, int d,
+    const double* __restrict__ mu, const double* __restrict__ Us,
+    unsigned long long* __restrict__ key) {
+  double m = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    double y[D];
+    whiten_row<D>(X, i, d, mu, Us, y);
+#pragma unroll
+    for (int k = 0; k < D; ++k) m = fmax(m, fabs(y[k]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(key, static_cast<unsigned long long>(f64_key(m)));
+}
+
+__device__ inline double grid_from_key(const unsigned long long* key) {
+  const double m = key_f64(*key);
+  int E = 0;
+  if (m > 0.0) frexp(m, &E);  // m < 2^E
+  return fmax(ldexp(1.0, E - 7), 0.015625);  // 256 g = 2^(E+1) >= 2 max|y|
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pack_prev_frag_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    int d, const double* __restrict__ mu, const double* __restrict__ Us,
+    int64_t npad, const double* __restrict__ lw2max,
+    const unsigned long long* __restrict__ ykey, double* __restrict__ gscale,
+    bf16x8* __restrict__ A) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const double g = grid_from_key(ykey);
+  if (j == 0) *gscale = g;
+  if (j >= npad) return;
+  double y[D];
+  double lw = kLwFloor;
+  if (j < n) {
+    whiten_row<D>(X, j, d, mu, Us, y);
+    const double wj = w[j];
+    if (wj > 0.0) lw = fmax(log2(wj) - *lw2max, kLwFloor);
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) y[k] = 0.0;
+  }
+  unsigned short y1[D], y2[D], y3[D], h[3], l[2];
+  const double n2 = split_row<D>(y, g, 1.0f, y1, y2, y3);
+  split_value(lw - n2, g * g, h, l);
+  store_frags<D, true>(A, j, y1, y2, y3, h, l);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pack_new_frag_kernel(
+    const double* __restrict__ theta, int64_t M, int64_t mpad, int d,
+    const double* __restrict__ mu, const double* __restrict__ Us,
+    const double* __restrict__ gscale, float* __restrict__ Ydir,
+    bf16x8* __restrict__ B) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= mpad) return;
+  const double g = *gscale;
+  double y[D];
+  bool ok = i < M;
+  if (ok) {
+    whiten_row<D>(theta, i, d, mu, Us, y);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      Ydir[i * D + k] = static_cast<float>(y[k]);
+      ok = ok && fabs(y[k]) <= 256.0 * g;  // NaN -> not ok
+    }
+  }
+  unsigned short y1[D], y2[D], y3[D], h[3], l[2];
+  if (ok) {
+    const double n2 = split_row<D>(y, g, 2.0f, y1, y2, y3);
+    split_value(-n2, g * g, h, l);
+  } else {  // padding / out-of-grid row: e = -inf, exact fixup if i < M
+#pragma unroll
+    for (int k = 0; k < D; ++k) y1[k] = y2[k] = y3[k] = 0;
+    h[0] = kBf16NegInf;
+    h[1] = h[2] = l[0] = l[1] = 0;
+  }
+  store_frags<D, false>(B, i, y1, y2, y3, h, l);
+}
+
+// one (32-row tile, i-tile) product: hi (exact) and lo accumulators
+template <int KH, int KL>
+__device__ __forceinline__ void mfma_step(const bf16x8* a, const bf16x8* b,
+                                          f32x16& hi, f32x16& lo) {
+  hi = f32x16{};
+  lo = f32x16{};
+#pragma unroll
+  for (int c = 0; c < KH; ++c)
+    hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
+#pragma unroll
+  for (int c = 0; c < KL; ++c)
+    lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0, 0, 0);
+}
+
+// sum of 2^(hi+lo) over the lane's 16 values: 16 independent exps, then a
+// fixed pairwise tree (v, v+8), (v, v+4), (v, v+2), (v, v+1)
+__device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
+  float e[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v] + lo[v]);
+#pragma unroll
+  for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+    for (int v = 0; v < w; ++v) e[v] += e[v + w];
+  return e[0];
+}
+
+// main pass.  Block (rb, s): wave w owns i-tiles (rb*kWaves + w)*IB + t and
+// walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
+// per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
+// into fp64.
+template <int KH, int KL, int IB>
+__global__ __launch_bounds__(256) void kde_mfma_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64 + lane;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    for (int jc = 0; jc < nj; jc += 64) {
+      // both 32-row tiles of the 64-row chunk: 2*IB (tile, i-tile) steps,
+      // software-pipelined -- the MFMAs of step q+1 issue before the VALU
+      // of step q, on a second accumulator pair
+      const bf16x8* __restrict__ ap = Aseg + (jc >> 5) * KT * 64;
+      bf16x8 a[2][KT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < KT; ++c) a[h][c] = ap[(h * KT + c) * 64];
+      float sacc[IB];
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+      f32x16 hi[2], lo[2];
+      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+#pragma unroll
+      for (int q = 0; q < 2 * IB; ++q) {
+        if (q + 1 < 2 * IB)
+          mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB], hi[(q + 1) & 1],
+                            lo[(q + 1) & 1]);
+        sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
+template <int D>
+int64_t mpad_rows(int64_t M) {
+  constexpr int rows = 32 * kWaves * Mk<D>::IB;
+  return ceil_div(M, rows) * rows;
+}
+
+int64_t mpad_for(int d, int64_t M) {
+  switch (kde_padded_dim(d)) {
+#define CASE(DD) \
+  case DD: return mpad_rows<DD>(M);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default: return -1;
+  }
+}
+
+int kt_for(int d) {
+  switch (kde_padded_dim(d)) {
+#define CASE(DD) \
+  case DD: return Mk<DD>::KT;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default: return -1;
+  }
+}
+
+struct MPlan {
+  int split, nseg, spb, jseg;
+  int64_t row_blocks;
+};
+
+template <int D>
+MPlan make_mplan(int64_t M, int64_t npad, int ib) {
+  constexpr int64_t target_blocks = 4096;
+  MPlan p;
+  p.nseg = kde_num_segments(npad);
+  p.jseg = static_cast<int>(ceil_div(ceil_div(npad, p.nseg), 64) * 64);
+  p.row_blocks = mpad_rows<D>(M) / (32 * kWaves * ib);
+  int split = 1;
+  while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
+  if (const char* env = getenv("ABC_KDE_MFMA_SPLIT")) {  // tuning override
+    const int v = atoi(env);
+    if (v >= 1 && v <= p.nseg && (p.nseg % v) == 0) split = v;
+  }
+  p.split = split;
+  p.spb = p.nseg / split;
+  return p;
+}
+
+template <int D, int IB>
+void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
+                 const bf16x8* Afr, int64_t npad, double* partial,
+                 hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
+  hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB>), dim3(grid),
+                     dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,
+                     p.spb, p.jseg, partial);
+}
+
+template <int D>
+int logpdf_mfma_impl(const bf16x8* Bfr, const float* Ynew, int64_t M,
+                     const bf16x8* Afr, const float* P, int64_t npad, int d,
+                     const double* lw2max, double log_const, double* out,
+                     void* ws, size_t ws_bytes, hipStream_t st) {
+  // i-tiles per wave: Mk<D>::IB (the row padding unit) or half of it
+  // (tuning override ABC_KDE_MFMA_IB); a row's arithmetic is the same
+  constexpr int IBF = Mk<D>::IB;
+  constexpr int IBH = IBF > 1 ? IBF / 2 : 1;
+  int ib = IBF;
+  if (const char* env = getenv("ABC_KDE_MFMA_IB")) {
+    if (atoi(env) == IBH) ib = IBH;
+  }
+  const MPlan p = make_mplan<D>(M, npad, ib);
+  const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
+                      static_cast<size_t>(M) * 4;
+  ABC_REQUIRE(ws_bytes >= need, "kde_mfma: workspace too small (%zu < %zu)",
+              ws_bytes, need);
+  char* base = static_cast<char*>(ws);
+  double* partial = reinterpret_cast<double*>(base);
+  int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.nseg * M) * 8);
+  int* fix_rows = n_fix + 4;
+  ABC_HIP(hipMemsetAsync(n_fix, 0, 16, st));
+  if (ib == IBF)
+    launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, st);
+  else
+    launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, st);
+  ABC_LAUNCH_CHECK("kde_mfma_kernel");
+  return kde_finish_f32(partial, M, p.nseg, Ynew, P, npad, d, lw2max,
+                        log_const, out, n_fix, fix_rows, st);
+}
+
+}  // namespace
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" {
+
+size_t abc_kde_mfma_prev_bytes(int64_t npad, int d) {
+  const int kt = kt_for(d);
+  if (kt < 0 || npad < 0) return 0;
+  return static_cast<size_t>(ceil_div(npad, 32)) * kt * 64 * 16;
+}
+
+int64_t abc_kde_mfma_new_rows(int64_t M, int d) { return mpad_for(d, M); }
+
+size_t abc_kde_mfma_new_bytes(int64_t M, int d) {
+  const int kt = kt_for(d);
+  const int64_t mp = mpad_for(d, M);
+  if (kt < 0 || mp < 0) return 0;
+  return static_cast<size_t>(mp / 32) * kt * 64 * 16;
+}
+
+int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
+                           const double* mu, const double* Us, float* P,
+                           void* Afr, int64_t npad, double* lw2max,
+                           double* gscale, void* ws, hipStream_t st) {
+  ABC_REQUIRE(Afr && gscale && ws, "pack_prev_mfma: null pointer");
+  const int D = kde_padded_dim(d);
+  if (D < 0) {
+    set_error("pack_prev_mfma: unsupported dimension d=%d (max 32)", d);
+    return kUnsupported;
+  }
+  const int rc = kde_pack_direct_f32(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
+  if (rc != kOk) return rc;
+  unsigned long long* ykey =
+      reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + 64);
+  ABC_HIP(hipMemsetAsync(ykey, 0, 8, st));
+  const unsigned gr = static_cast<unsigned>(ceil_div(npad, 256));
+  switch (D) {
+#define CASE(DD)                                                               \
+  case DD:                                                                     \
+    hipLaunchKernelGGL((ymax_kernel<DD>), dim3(stream_grid(n, 256, 1024)),     \
+                       dim3(256), 0, st, X, n, d, mu, Us, ykey);               \
+    hipLaunchKernelGGL((pack_prev_frag_kernel<DD>), dim3(gr), dim3(256), 0, st, \
+                       X, w, n, d, mu, Us, npad, lw2max, ykey, gscale,         \
+                       static_cast<bf16x8*>(Afr));                             \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+  }
+  ABC_LAUNCH_CHECK("pack_prev_frag_kernel");
+  return kOk;
+}
+
+int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
+                          const double* mu, const double* Us,
+                          const double* gscale, float* Ynew, void* Bfr,
+                          hipStream_t st) {
+  ABC_REQUIRE(M >= 0, "pack_new_mfma: negative M");
+  const int D = kde_padded_dim(d);
+  if (D < 0) {
+    set_error("pack_new_mfma: unsupported dimension d=%d (max 32)", d);
+    return kUnsupported;
+  }
+  if (M == 0) return kOk;
+  ABC_REQUIRE(theta && mu && Us && gscale && Ynew && Bfr,
+              "pack_new_mfma: null pointer");
+  const int64_t mp = mpad_for(d, M);
+  const unsigned gr = static_cast<unsigned>(ceil_div(mp, 256));
+  switch (D) {
+#define CASE(DD)                                                              \
+  case DD:                                                                    \
+    hipLaunchKernelGGL((pack_new_frag_kernel<DD>), dim3(gr), dim3(256), 0, st, \
+                       theta, M, mp, d, mu, Us, gscale, Ynew,                 \
+                       static_cast<bf16x8*>(Bfr));                            \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+  }
+  ABC_LAUNCH_CHECK("pack_new_frag_kernel");
+  return kOk;
+}
+
+int abc_kde_logpdf_mfma(const void* Bfr, const float* Ynew, int64_t M,
+                        const void* Afr, const float* P, int64_t npad, int d,
+                        const double* lw2max, double log_const,
+                        double* out_logpd, void* ws, size_t ws_bytes,
+                        hipStream_t st) {
+  ABC_REQUIRE(M >= 0 && npad >= 0, "kde_mfma: negative size");
+  ABC_REQUIRE(npad % kKdeRowPad == 0, "kde_mfma: npad must be a multiple of %d",
+              kKdeRowPad);
+  if (M == 0) return kOk;
+  ABC_REQUIRE(npad > 0, "kde_mfma: empty previous population");
+  ABC_REQUIRE(Bfr && Ynew && Afr && P && lw2max && out_logpd && ws,
+              "kde_mfma: null pointer");
+  const bf16x8* B = static_cast<const bf16x8*>(Bfr);
+  const bf16x8* A = static_cast<const bf16x8*>(Afr);
+  switch (kde_padded_dim(d)) {
+#define CASE(DD)                                                          \
+  case DD:                                                                \
+    return logpdf_mfma_impl<DD>(B, Ynew, M, A, P, npad, d, lw2max,        \
+                                log_const, out_logpd, ws, ws_bytes, st);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default:
+      set_error("kde_mfma: unsupported dimension d=%d (max 32)", d);
+      return kUnsupported;
+  }
+}
+
+}  // extern "C"

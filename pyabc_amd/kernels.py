@@ -176,32 +176,63 @@ def psd_whitening(cov):
     return U, int(keep.sum()), float(np.sum(np.log(s[keep])))
 
 
-class PackedPopulation:
-    """The previous population packed for the KDE pass (built once per fit)."""
+class WhitenedRows:
+    """New rows prepared for the MFMA KDE pass: direct fp32 rows (exact
+    underflow fixup) plus the bf16 piece fragments of the B operand."""
 
-    def __init__(self, X, w, mu, Us, rank, log_pdet, precision="f32"):
+    def __init__(self, Y, frags, M):
+        self.Y, self.frags, self.M = Y, frags, M
+        self.shape = (M, Y.shape[1])
+
+
+class PackedPopulation:
+    """The previous population packed for the KDE pass (built once per fit).
+
+    precision: "mfma" (default: exact-grid bf16 pieces on the matrix cores,
+    kde_mfma.hip), "f32" (direct fp32 VALU pass) or "f64" (fp64 VALU pass).
+    """
+
+    def __init__(self, X, w, mu, Us, rank, log_pdet, precision="mfma"):
         X = _contig(X, F64)
         n, d = X.shape
         self.n, self.d = n, d
         self.D = padded_dim(d)
         rp = row_pad()
         self.npad = ((n + rp - 1) // rp) * rp
+        if precision not in ("mfma", "f32", "f64"):
+            raise ValueError(f"unknown KDE precision {precision!r}")
         self.precision = precision
-        dt = F32 if precision == "f32" else F64
+        dt = F64 if precision == "f64" else F32
         self.P = torch.empty((self.npad, self.D + 1), dtype=dt, device=_dev())
         self.lw2max = torch.empty(1, dtype=F64, device=_dev())
         self.mu = mu
         self.Us = Us
         self.log_const = -0.5 * (rank * LOG_2PI + log_pdet)
         ws = WS.get(256, "pack")
+        w = _contig(w, F64)
+        if precision == "mfma":
+            nb = nat.lib().abc_kde_mfma_prev_bytes(self.npad, d)
+            self.A = torch.empty(nb, dtype=torch.uint8, device=_dev())
+            self.gscale = torch.empty(1, dtype=F64, device=_dev())
+            call("abc_kde_pack_prev_mfma", ptr(X), ptr(w), n, d, ptr(mu),
+                 ptr(Us), ptr(self.P), ptr(self.A), self.npad,
+                 ptr(self.lw2max), ptr(self.gscale), ptr(ws), nat.stream())
+            return
         fn = "abc_kde_pack_prev_f32" if precision == "f32" else \
             "abc_kde_pack_prev_f64"
-        call(fn, ptr(X), ptr(_contig(w, F64)), n, d, ptr(mu), ptr(Us),
+        call(fn, ptr(X), ptr(w), n, d, ptr(mu), ptr(Us),
              ptr(self.P), self.npad, ptr(self.lw2max), ptr(ws), nat.stream())
 
     def whiten(self, theta):
         theta = _contig(theta, F64)
         M = theta.shape[0]
+        if self.precision == "mfma":
+            Y = torch.zeros((M, self.D), dtype=F32, device=_dev())
+            nb = nat.lib().abc_kde_mfma_new_bytes(M, self.d)
+            B = torch.empty(max(nb, 16), dtype=torch.uint8, device=_dev())
+            call("abc_kde_pack_new_mfma", ptr(theta), M, self.d, ptr(self.mu),
+                 ptr(self.Us), ptr(self.gscale), ptr(Y), ptr(B), nat.stream())
+            return WhitenedRows(Y, B, M)
         dt = F32 if self.precision == "f32" else F64
         Y = torch.zeros((M, self.D), dtype=dt, device=_dev())
         fn = "abc_whiten_f32" if self.precision == "f32" else "abc_whiten_f64"
@@ -217,6 +248,13 @@ class PackedPopulation:
             return out
         wsb = nat.lib().abc_kde_workspace_bytes(M, self.npad, self.d)
         ws = WS.get(wsb, "kde")
+        if self.precision == "mfma":
+            if not isinstance(Y, WhitenedRows):
+                raise TypeError("mfma KDE pass takes rows from whiten()")
+            call("abc_kde_logpdf_mfma", ptr(Y.frags), ptr(Y.Y), M, ptr(self.A),
+                 ptr(self.P), self.npad, self.d, ptr(self.lw2max),
+                 self.log_const, ptr(out), ptr(ws), wsb, nat.stream())
+            return out
         fn = "abc_kde_logpdf_f32" if self.precision == "f32" else \
             "abc_kde_logpdf_f64"
         call(fn, ptr(Y), M, ptr(self.P), self.npad, self.d, ptr(self.lw2max),

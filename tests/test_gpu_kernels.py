@@ -42,7 +42,8 @@ def _packed(K, X, w, cov, precision):
                               log_pdet, precision)
 
 
-@pytest.mark.parametrize("precision,rtol", [("f32", 1e-5), ("f64", 1e-12)])
+@pytest.mark.parametrize("precision,rtol", [("mfma", 1e-5), ("f32", 1e-5),
+                                            ("f64", 1e-12)])
 @pytest.mark.parametrize("name", golden_names("kde_"))
 def test_kde_density_vs_reference(K, name, precision, rtol):
     g = load_golden(name)
@@ -63,7 +64,8 @@ def test_kde_density_vs_reference(K, name, precision, rtol):
         np.testing.assert_allclose(host(wt), g["weight_norm"], rtol=rtol)
 
 
-def test_kde_underflow_rows_fixup(K):
+@pytest.mark.parametrize("precision", ["mfma", "f32"])
+def test_kde_underflow_rows_fixup(K, precision):
     """Rows far from every previous particle underflow the fixed offset;
     the fixup pass must still return the exact log density."""
     rng = np.random.default_rng(7)
@@ -72,7 +74,7 @@ def test_kde_underflow_rows_fixup(K):
     w /= w.sum()
     cov = ref.mvn_fit_cov(X, w)
     theta = np.concatenate([X[:50] + 0.01, X[:20] + 6.0])   # far rows
-    pp = _packed(K, X, w, cov, "f32")
+    pp = _packed(K, X, w, cov, precision)
     lp = host(pp.logpdf(dev(theta)))
     U, rank, log_pdet = ref.psd_whitening(cov)
     ls = ref.kde_logsum(theta @ U, X @ U, np.log(w))
@@ -89,10 +91,60 @@ def test_kde_large_random_vs_oracle(K):
     cov = ref.mvn_fit_cov(X, w)
     theta = X[rng.integers(0, N, M)] + rng.normal(size=(M, d)) * 0.3
     expect = ref.kde_transition_pd(theta, X, w, cov)
-    for prec, rtol in [("f32", 1e-5), ("f64", 1e-12)]:
+    for prec, rtol in [("mfma", 1e-5), ("f32", 1e-5), ("f64", 1e-12)]:
         pp = _packed(K, X, w, cov, prec)
         got = np.exp(host(pp.logpdf(dev(theta))))
         np.testing.assert_allclose(got, expect, rtol=rtol)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 5, 8, 12, 20, 32])
+def test_kde_mfma_all_dims_vs_oracle(K, d):
+    """Exact-grid bf16 MFMA pass at every padded-dimension instance,
+    including ragged N / M (tails of 32-row tiles and 64-row chunks)."""
+    rng = np.random.default_rng(100 + d)
+    N, M = 3001 + 7 * d, 517
+    X = rng.normal(size=(N, d)) * rng.uniform(0.5, 3, d) + 1.0
+    w = rng.uniform(0.1, 2, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = X[rng.integers(0, N, M)] + rng.normal(size=(M, d)) * 0.2
+    expect = ref.kde_transition_pd(theta, X, w, cov)
+    pp = _packed(K, X, w, cov, "mfma")
+    got = np.exp(host(pp.logpdf(dev(theta))))
+    np.testing.assert_allclose(got, expect, rtol=1e-5)
+
+
+def test_kde_mfma_out_of_grid_rows(K):
+    """New rows beyond the population's grid range (|y| > 256 g) are flagged
+    by the packer and evaluated by the exact fixup."""
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(2000, 3))
+    w = np.full(2000, 1 / 2000)
+    cov = ref.mvn_fit_cov(X, w)
+    theta = np.concatenate([X[:10] + 0.05, X[:5] * 40.0, X[:5] + 3.0])
+    pp = _packed(K, X, w, cov, "mfma")
+    lp = host(pp.logpdf(dev(theta)))
+    U, rank, log_pdet = ref.psd_whitening(cov)
+    ls = ref.kde_logsum(theta @ U, X @ U, np.log(w))
+    expect = ls - 0.5 * (rank * ref.LOG_2PI + log_pdet)
+    np.testing.assert_allclose(lp, expect, rtol=2e-6, atol=1e-5)
+
+
+def test_kde_mfma_rows_independent_of_launch(K):
+    """A row's bits do not depend on M or on which rows share its tiles
+    (the multi-GPU row split relies on it)."""
+    rng = np.random.default_rng(9)
+    N, M, d = 70000, 3000, 8
+    X = rng.normal(size=(N, d))
+    w = rng.uniform(0.5, 1.5, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = X[rng.integers(0, N, M)] + 0.1 * rng.normal(size=(M, d))
+    pp = _packed(K, X, w, cov, "mfma")
+    full = host(pp.logpdf(dev(theta)))
+    for lo, hi in [(0, 1), (17, 1234), (1500, 3000), (2999, 3000)]:
+        part = host(pp.logpdf(dev(theta[lo:hi])))
+        np.testing.assert_array_equal(part, full[lo:hi])
 
 
 # ------------------------------------------------------------ (a1) fit

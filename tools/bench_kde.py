@@ -59,6 +59,19 @@ if __name__ == "__main__":
                 print(f"tier {tier}:", end=" ")
                 run(100000, M, 4, "f32", reps=3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "mfma":
+        for (N, M, d) in [(1000000, 1000000, 8), (262144, 262144, 8),
+                          (1000000, 500000, 8), (1000000, 125000, 8),
+                          (262144, 262144, 20), (100000, 100000, 4)]:
+            run(N, M, d, "mfma")
+            if len(sys.argv) > 2:
+                run(N, M, d, "f32")
+        if len(sys.argv) > 2 and sys.argv[2] == "split":
+            for sp in ["1", "2", "4", "8", "16"]:
+                os.environ["ABC_KDE_MFMA_SPLIT"] = sp
+                print(f"split {sp}:", end=" ")
+                run(1000000, 1000000, 8, "mfma", reps=2)
+        sys.exit(0)
     for (N, M, d, p) in [(262144, 262144, 8, "f32"), (1000000, 1000000, 8, "f32"),
                          (262144, 262144, 4, "f32"), (262144, 262144, 20, "f32"),
                          (65536, 65536, 8, "f64")]:

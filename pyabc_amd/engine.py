@@ -52,7 +52,7 @@ class DeviceMVNFit:
     previous population for the KDE pass (scipy _PSD whitening)."""
 
     def __init__(self, X, w, scaling=1.0, bandwidth_selector=None,
-                 precision="f32", moments=None):
+                 precision="mfma", moments=None):
         self.X = X
         self.w = w
         n, d = X.shape
@@ -201,7 +201,7 @@ class GenerationEngine:
 
     def __init__(self, model, prior_lo, prior_scale, distance_p=2.0,
                  comm=None, seed=0, min_batch=1 << 16, max_batch=1 << 22,
-                 kde_precision="f32", record_stats=False):
+                 kde_precision="mfma", record_stats=False):
         self.model = model
         self.dev = torch.device("cuda", torch.cuda.current_device())
         self.lo = torch.as_tensor(np.asarray(prior_lo, dtype=np.float64),

@@ -124,12 +124,12 @@ class GPUBatchSampler(Sampler):
 
     Parameters: ``seed`` (Philox seed; default drawn from numpy's global
     state), ``min_batch`` / ``max_batch`` proposals per round,
-    ``kde_precision`` ("f32" or "f64" KDE kernel), ``comm`` (multi-GPU
+    ``kde_precision`` ("mfma" default, "f32" or "f64" KDE kernel), ``comm`` (multi-GPU
     sharding, default from the torchrun environment).
     """
 
     def __init__(self, seed=None, min_batch=1 << 14, max_batch=1 << 22,
-                 kde_precision="f32", comm=None):
+                 kde_precision="mfma", comm=None):
         super().__init__()
         self.seed = seed
         self.min_batch = min_batch

@@ -151,12 +151,13 @@ class MultivariateNormalTransition(Transition):
 
     fit: weighted moments kernel + host d x d finish (smart_cov * bw^2 *
     scaling, multivariatenormal.py:67-85).  rvs: device resampling +
-    perturbation (Philox).  pdf: device KDE pass (fp32 by default;
+    perturbation (Philox).  pdf: device KDE pass (exact-grid bf16 MFMA by
+    default; ``kde_precision="f32"`` for the direct fp32 kernel,
     ``kde_precision="f64"`` for the fp64 kernel).
     """
 
     def __init__(self, scaling=1, bandwidth_selector=silverman_rule_of_thumb,
-                 kde_precision="f32"):
+                 kde_precision="mfma"):
         self.scaling = scaling
         self.bandwidth_selector = bandwidth_selector
         self.kde_precision = kde_precision

@@ -77,8 +77,9 @@ def main():
     q = 4 if args.quick else 1
 
     # ---------------- (a3) KDE weight pass -------------------------------
-    for (N, d, prec) in [(1_000_000 // q, 8, "f32"), (1_000_000 // q, 20, "f32"),
-                         (100_000, 4, "f32"), (200_000 // q, 8, "f64")]:
+    for (N, d, prec) in [(1_000_000 // q, 8, "mfma"), (1_000_000 // q, 8, "f32"),
+                         (1_000_000 // q, 20, "mfma"), (100_000, 4, "mfma"),
+                         (200_000 // q, 8, "f64")]:
         X = torch.randn((N, d), dtype=F64, device="cuda", generator=g)
         w = torch.rand(N, dtype=F64, device="cuda", generator=g) + 0.5
         w /= w.sum()
@@ -89,7 +90,7 @@ def main():
         t = timed(lambda: fit.packed.logpdf_whitened(Y), reps=3)
         pairs = N * fit.packed.npad
         report(f"kde_logpdf_{prec}", t, pairs, "pairs", 3 * d + 4,
-               "valu_f32" if prec == "f32" else "valu_f64",
+               "valu_f64" if prec == "f64" else "valu_f32",
                {"N": N, "M": N, "d": d})
 
     # ---------------- (a1) fit: weighted moments -------------------------

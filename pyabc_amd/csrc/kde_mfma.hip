@@ -312,7 +312,7 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB>
+template <int KH, int KL, int IB, bool PIPE>
 __global__ __launch_bounds__(256) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -350,14 +350,23 @@ __global__ __launch_bounds__(256) void kde_mfma_kernel(
       float sacc[IB];
 #pragma unroll
       for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
-      f32x16 hi[2], lo[2];
-      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+      if constexpr (PIPE) {
+        f32x16 hi[2], lo[2];
+        mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
-      for (int q = 0; q < 2 * IB; ++q) {
-        if (q + 1 < 2 * IB)
-          mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB], hi[(q + 1) & 1],
-                            lo[(q + 1) & 1]);
-        sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+        for (int q = 0; q < 2 * IB; ++q) {
+          if (q + 1 < 2 * IB)
+            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+                              hi[(q + 1) & 1], lo[(q + 1) & 1]);
+          sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2 * IB; ++q) {
+          f32x16 hi, lo;
+          mfma_step<KH, KL>(a[q / IB], bq[q % IB], hi, lo);
+          sacc[q % IB] += tile_sum(hi, lo);
+        }
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
@@ -427,9 +436,18 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
                  const bf16x8* Afr, int64_t npad, double* partial,
                  hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
-  hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB>), dim3(grid),
-                     dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,
-                     p.spb, p.jseg, partial);
+  // software pipelining pays at D <= 8 (VALU-bound); at larger D the
+  // MFMA chain dominates and the lower register count wins (bench_kde sweep)
+  bool pipe = D <= 8;
+  if (const char* env = getenv("ABC_KDE_MFMA_PIPE")) pipe = atoi(env) != 0;
+  if (pipe)
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
+                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                       p.split, p.spb, p.jseg, partial);
+  else
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
+                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                       p.split, p.spb, p.jseg, partial);
 }
 
 template <int D>

@@ -52,7 +52,7 @@ struct Mk {
   static constexpr int KH = (D + 6 + 15) / 16;      // y1.y1, aH x3, bH x3
   static constexpr int KL = (7 * D + 4 + 15) / 16;  // 7 cross terms, aL, bL
   static constexpr int KT = KH + KL;
-  static constexpr int IB = D <= 8 ? 4 : (D <= 24 ? 2 : 1);  // i-tiles/wave
+  static constexpr int IB = D <= 8 ? 3 : (D <= 24 ? 2 : 1);  // i-tiles/wave
 };
 
 __device__ inline unsigned short bf16_rne(float x) {
@@ -337,20 +337,28 @@ __global__ __launch_bounds__(256) void kde_mfma_kernel(
     double S[IB];
 #pragma unroll
     for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    // a[0] / a[1]: the two 32-row tiles of the current 64-row chunk.  Each
+    // tile's fragments are requested one half-chunk before their first MFMA
+    // (tile 1 while tile 0 computes, the next chunk's tile 0 while tile 1
+    // computes), so the L2 latency runs under the VALU work.
+    bf16x8 a[2][KT];
+    if (nj > 0) {
+#pragma unroll
+      for (int c = 0; c < KT; ++c) a[0][c] = Aseg[c * 64];
+    }
     for (int jc = 0; jc < nj; jc += 64) {
-      // both 32-row tiles of the 64-row chunk: 2*IB (tile, i-tile) steps,
-      // software-pipelined -- the MFMAs of step q+1 issue before the VALU
-      // of step q, on a second accumulator pair
       const bf16x8* __restrict__ ap = Aseg + (jc >> 5) * KT * 64;
-      bf16x8 a[2][KT];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int c = 0; c < KT; ++c) a[h][c] = ap[(h * KT + c) * 64];
+      // next chunk's first tile (re-read of this one on the last chunk)
+      const bf16x8* __restrict__ an =
+          Aseg + (((jc + 64 < nj) ? jc + 64 : jc) >> 5) * KT * 64;
       float sacc[IB];
 #pragma unroll
       for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
       if constexpr (PIPE) {
+        // 2*IB (tile, i-tile) steps; the MFMAs of step q+1 issue before the
+        // VALU of step q, on a second accumulator pair
+#pragma unroll
+        for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
         f32x16 hi[2], lo[2];
         mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
@@ -358,14 +366,24 @@ __global__ __launch_bounds__(256) void kde_mfma_kernel(
           if (q + 1 < 2 * IB)
             mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
                               hi[(q + 1) & 1], lo[(q + 1) & 1]);
+          if (q + 1 == IB) {  // last MFMA reading tile 0 is issued
+#pragma unroll
+            for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
+          }
           sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
         }
       } else {
+#pragma unroll
+        for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
           mfma_step<KH, KL>(a[q / IB], bq[q % IB], hi, lo);
           sacc[q % IB] += tile_sum(hi, lo);
+          if (q + 1 == IB) {
+#pragma unroll
+            for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
+          }
         }
       }
 #pragma unroll
@@ -415,7 +433,10 @@ struct MPlan {
 
 template <int D>
 MPlan make_mplan(int64_t M, int64_t npad, int ib) {
-  constexpr int64_t target_blocks = 4096;
+  // many short blocks: at N = M = 1e6 split 1 -> 32 is 181 -> 163 ms
+  // (tools/bench_kde.py msplit); split % 8 == 0 pins each j-segment set to
+  // one XCD's L2 (blocks go round-robin over the 8 XCDs)
+  constexpr int64_t target_blocks = 65536;
   MPlan p;
   p.nseg = kde_num_segments(npad);
   p.jseg = static_cast<int>(ceil_div(ceil_div(npad, p.nseg), 64) * 64);

@@ -59,6 +59,17 @@ if __name__ == "__main__":
                 print(f"tier {tier}:", end=" ")
                 run(100000, M, 4, "f32", reps=3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "msplit":
+        for sp in ["1", "2", "4", "8", "16", "32"]:
+            os.environ["ABC_KDE_MFMA_SPLIT"] = sp
+            print(f"split {sp}:", end=" ")
+            run(1000000, 1000000, 8, "mfma", reps=2)
+        os.environ.pop("ABC_KDE_MFMA_SPLIT")
+        for ib in ["3", "1"]:
+            os.environ["ABC_KDE_MFMA_IB"] = ib
+            print(f"ib {ib}:", end=" ")
+            run(100000, 100000, 4, "mfma", reps=3)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "mfma":
         for (N, M, d) in [(1000000, 1000000, 8), (262144, 262144, 8),
                           (1000000, 500000, 8), (1000000, 125000, 8),

@@ -46,7 +46,8 @@ from .model import (Model, SimpleModel, ModelResult,  # noqa: E402
                     GaussianMeanModel)
 from .population import Particle, Population, ColumnarPopulation  # noqa: E402
 from .populationstrategy import (PopulationStrategy,  # noqa: E402
-                                 ConstantPopulationSize, ListPopulationSize)
+                                 ConstantPopulationSize, ListPopulationSize,
+                                 AdaptivePopulationSize)
 from .sampler import (Sample, SampleFactory, Sampler,  # noqa: E402
                       SingleCoreSampler, GPUBatchSampler)
 from .storage import History, create_sqlite_db_id  # noqa: E402

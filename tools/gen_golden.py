@@ -562,5 +562,67 @@ def gen_e2e_stochastic():
 GENS["e2e_stochastic"] = gen_e2e_stochastic
 
 
+def gen_cv():
+    """AdaptivePopulationSize pieces (populationstrategy.py:318-345):
+    bootstrap KDE fit (fit_cov, multivariatenormal.py:67-73) + pdf_static
+    (:114-126) at the test points, cv/bootstrap.py calc_variation (:12-32)
+    and cv/powerlaw.py fitpowerlaw (:13-18)."""
+    from pyabc.cv.bootstrap import calc_variation
+    from pyabc.cv.powerlaw import fitpowerlaw
+    rng = np.random.default_rng(41)
+    d, N, n, B = 3, 500, 200, 5
+    test_X = np.asarray(make_population(rng, N, d)[0])
+    test_w = rng.uniform(0.5, 1.5, N)
+    test_w /= test_w.sum()
+    tr = MultivariateNormalTransition(scaling=1)
+    boots = np.stack([test_X[rng.integers(0, N, n)]
+                      + 0.3 * rng.normal(size=(n, d)) for _ in range(B)])
+    w0 = np.ones(n) / n
+    dens, covs = [], []
+    for b in range(B):
+        cov = tr.fit_cov(boots[b], w0)
+        covs.append(cov)
+        dens.append(tr.pdf_static(test_X, boots[b], cov, w0))
+    dens = np.stack(dens)
+    cv = calc_variation([dens], np.array([n]), test_w[None, :])
+    # a second model with a different share
+    dens2 = dens[::-1] * rng.uniform(0.9, 1.1, dens.shape)
+    cv2 = calc_variation([dens, dens2], np.array([n, 3 * n]),
+                         np.vstack([test_w, test_w[::-1]]))
+    xs = np.arange(100, 2000, 190)
+    ys = 0.8 * xs ** -0.45 * (1 + 0.01 * np.sin(xs))
+    popt, _, finv = fitpowerlaw(xs, ys)
+    save("cv_bootstrap", test_X=test_X, test_w=test_w, boots=boots,
+         covs=np.stack(covs), dens=dens, cv=np.float64(cv), dens2=dens2,
+         cv2=np.float64(cv2), xs=xs, ys=ys, popt=popt,
+         n_at_005=np.float64(finv(0.05)),
+         _ref="pyabc/populationstrategy.py:318-345, "
+              "transition/multivariatenormal.py:67-73,114-126, "
+              "cv/bootstrap.py:12-32, cv/powerlaw.py:13-18")
+
+
+GENS["cv"] = gen_cv
+
+
+def gen_vis():
+    """visualization/kde.py:19-75 kde_1d and :173-247 kde_2d."""
+    from pyabc.visualization.kde import kde_1d, kde_2d
+    rng = np.random.default_rng(43)
+    N = 800
+    df = pd.DataFrame({"a": rng.normal(1, 0.5, N),
+                       "b": rng.gamma(2.0, 1.0, N)})
+    w = rng.uniform(0.2, 1.0, N)
+    w /= w.sum()
+    x1, pdf1 = kde_1d(df, w, "a", numx=40)
+    x1l, pdf1l = kde_1d(df, w, "b", xmin=-1, xmax=9, numx=33)
+    X, Y, PDF = kde_2d(df, w, "a", "b", numx=20, numy=15)
+    save("vis_kde", a=df["a"].values, b=df["b"].values, w=w, x1=x1,
+         pdf1=pdf1, x1l=x1l, pdf1l=pdf1l, X=X, Y=Y, PDF=PDF,
+         _ref="pyabc/visualization/kde.py:19-75, 173-247")
+
+
+GENS["vis"] = gen_vis
+
+
 if __name__ == "__main__":
     _main()

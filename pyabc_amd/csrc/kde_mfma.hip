@@ -313,7 +313,7 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
 template <int KH, int KL, int IB, bool PIPE>
-__global__ __launch_bounds__(256) void kde_mfma_kernel(
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;

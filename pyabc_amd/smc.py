@@ -124,10 +124,16 @@ class ABCSMC:
         return self.history
 
     def load(self, db, abc_id=1, observed_sum_stat=None):
-        """Continue a run held in this process (smc.py:348-382)."""
+        """Continue a run (smc.py:348-382): one held in this process, or one
+        stored in a ``sqlite:///file.db`` History (this package's or the
+        reference's; the next fit then reads the last population from the
+        file)."""
         h = History.lookup(db)
-        if h is None:
-            raise ValueError(f"no in-memory history {db!r} in this process")
+        if h is None or h.id != abc_id:
+            if not db.startswith("sqlite:///"):
+                raise ValueError(f"no in-memory history {db!r} in this "
+                                 "process")
+            h = History(db, _id=abc_id, create=False)
         self.history = h
         self.history.id = abc_id
         self.x_0 = observed_sum_stat if observed_sum_stat is not None \

@@ -19,6 +19,13 @@ def pa():
     return pyabc_amd
 
 
+def _eps(h):
+    """Epsilons of t >= 0 (the table's first row is the PRE_TIME one,
+    history.py:344-370)."""
+    pops = h.get_all_populations()
+    return pops[pops.t >= 0].epsilon.values
+
+
 def _post_stats(h, names):
     out = []
     for t in range(h.max_t + 1):
@@ -61,7 +68,7 @@ def test_config1_quickstart_batch_path(pa):
     abc.new("mem://c1", {"data": 2.5})
     h = abc.run(minimum_epsilon=0.1, max_nr_populations=4)
     assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
-    eps = h.get_all_populations().epsilon.values
+    eps = _eps(h)
     _check_against_reference(g, "c1", 5, eps, _post_stats(h, ["mean"]), 1)
 
 
@@ -84,7 +91,7 @@ def test_config2_adaptive_mad_batch_path(pa):
     abc.new("mem://c2", dict(zip(keys, x0v)))
     h = abc.run(max_nr_populations=4)
     assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
-    eps = h.get_all_populations().epsilon.values
+    eps = _eps(h)
     _check_against_reference(g, "c2", 3, eps, _post_stats(h, names), d)
 
 
@@ -245,7 +252,51 @@ def test_local_transition_batch_path(pa):
         df, w = h.distribution_numpy(0, h.max_t)
         w = w / w.sum()
         means[kind] = (df[names].values * w[:, None]).sum(0)
-        eps = h.get_all_populations().epsilon.values
+        eps = _eps(h)
         assert np.all(np.diff(eps[1:]) <= 0)
     np.testing.assert_allclose(means["local"], means["mvn"], atol=0.15)
     np.testing.assert_allclose(means["local"], theta_true, atol=0.5)
+
+
+def test_file_history_roundtrip_and_load(pa, tmp_path):
+    """SURVEY 8(f) rank 1: a batch-path run stored in a ``sqlite:///`` file
+    (the reference's schema, bulk writer thread).  Reopened from the file,
+    every generation's distribution equals the device population bit for
+    bit; ``ABCSMC.load`` continues the run from the file (the next fit reads
+    the stored population) like smc.py:348-382."""
+    db = pa.create_sqlite_db_id(str(tmp_path), "run.db")
+    prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
+
+    def make(seed):
+        return pa.ABCSMC(pa.GaussianMeanModel(), prior, pa.PNormDistance(p=2),
+                         population_size=500, eps=pa.MedianEpsilon(),
+                         sampler=pa.GPUBatchSampler(seed=seed))
+    abc = make(21)
+    abc.new(db, {"data": 2.5})
+    h = abc.run(minimum_epsilon=0.05, max_nr_populations=3)
+    assert all(e["batch"] for e in abc.generation_log)
+    assert h.max_t == 2
+    disk = pa.History(db, create=False)
+    assert disk.id == h.id and disk.max_t == 2
+    for t in range(3):
+        df_dev, w_dev = h.distribution_numpy(0, t)
+        df, w = disk.get_distribution(0, t)
+        np.testing.assert_array_equal(df["mean"].values, df_dev["mean"].values)
+        np.testing.assert_array_equal(w, w_dev)
+        wd = disk.get_weighted_distances(t)
+        np.testing.assert_array_equal(
+            wd.distance.values, h.get_weighted_distances(t).distance.values)
+    pops = disk.get_all_populations()
+    assert list(pops.t) == [-1, 0, 1, 2]
+    assert list(pops.particles) == [1, 500, 500, 500]
+    assert disk.total_nr_simulations == h.total_nr_simulations
+    assert disk.observed_sum_stat() == {"data": 2.5}
+    # continue from the file in a fresh ABCSMC (no in-process populations)
+    pa.storage._REGISTRY.pop(db, None)
+    abc2 = make(22)
+    abc2.load(db, h.id)
+    h2 = abc2.run(minimum_epsilon=0.05, max_nr_populations=1)
+    assert h2.max_t == 3
+    assert pa.History(db, create=False).get_all_populations().t.max() == 3
+    eps = _eps(pa.History(db, create=False))
+    assert len(eps) == 4 and np.all(np.diff(eps) <= 0)

@@ -314,6 +314,7 @@ def test_e2e_stochastic_batch_path(K):
     h = abc.run(max_nr_populations=6)
     assert sampler.fallback_reason is None
     pops = h.get_all_populations()
+    pops = pops[pops.t >= 0]
     temps = pops.epsilon.values
     assert temps[-1] == 1.0
     assert np.all(np.diff(temps) <= 0)

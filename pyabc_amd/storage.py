@@ -359,6 +359,7 @@ class History:
         self._pre_nr_samples = 0
         self._meta = {}
         self._sql = _SQLStore(path) if path else None
+        self._max_t = None
         self._id = self._find_latest_id() if _id is None else _id
         if self._id is None:
             self._id = 1
@@ -410,6 +411,7 @@ class History:
                 r[0] for r in self._sql.q("SELECT id FROM abc_smc")]:
             raise ValueError(f"Specified id {val} does not exist in database.")
         self._id = val
+        self._max_t = None
 
     # --- writing ----------------------------------------------------------
     def store_initial_data(self, ground_truth_model, options,
@@ -449,6 +451,7 @@ class History:
                    if m != ground_truth_model]
         s.write_population(self._id, History.PRE_TIME, np.inf, 0, models,
                            True)
+        self._max_t = History.PRE_TIME
 
     def update_nr_samples(self, t=PRE_TIME, nr_samples=0):
         if t == History.PRE_TIME:
@@ -489,6 +492,8 @@ class History:
                     distances=[list(p.accepted_distances) for p in plist],
                     stats=[s for p in plist for s in p.accepted_sum_stats])
                 models.append((int(m), model_names[m], mp[m], blk))
+        self._max_t = max(int(t), self.max_t if self.max_t is not None
+                          else int(t))
         # host copies are taken above; the SQL write runs on the writer
         # thread (readers and done() wait for it)
         self._sql.submit(
@@ -516,8 +521,12 @@ class History:
     def max_t(self):
         if self._sql is None:
             return max(self._pops) if self._pops else -1
-        return self._q("SELECT MAX(t) FROM populations WHERE abc_smc_id=?",
-                       (self._id,))[0][0]
+        if self._max_t is None:
+            # cached, so the generation loop's reads do not wait for the
+            # writer thread (append_population keeps it current)
+            self._max_t = self._q("SELECT MAX(t) FROM populations WHERE "
+                                  "abc_smc_id=?", (self._id,))[0][0]
+        return self._max_t
 
     @property
     def n_populations(self):

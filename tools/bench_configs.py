@@ -33,13 +33,22 @@ def linear_problem(d, S, A_scale):
     return A, theta_true, x0, keys, names
 
 
-def run(name, abc, x0, names, theta_true=None, **run_kw):
+def run(name, abc, x0, names, theta_true=None, db=None, **run_kw):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    abc.new(f"mem://{name}", x0)
+    abc.new(db or f"mem://{name}", x0)
+    if db is not None:
+        # the reference's timing runs store no statistics
+        abc.history.stores_sum_stats = False
     h = abc.run(**run_kw)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    store_s = None
+    if db is not None:
+        t1 = time.perf_counter()
+        h._sql.flush()          # writes still queued after the last one
+        store_s = time.perf_counter() - t1
+        wall += store_s
     log = abc.generation_log
     N = abc.population_size(0) if callable(getattr(abc, "population_size",
                                                    None)) else None
@@ -56,6 +65,9 @@ def run(name, abc, x0, names, theta_true=None, **run_kw):
                if rates else None,
                all_batch=all(g["batch"] for g in gens), gens=gens,
                posterior_mean=mean.tolist())
+    if db is not None:
+        out["db"] = db
+        out["store_wait_after_run_s"] = store_s
     if theta_true is not None:
         out["theta_true"] = list(map(float, theta_true))
     print(json.dumps(out), flush=True)
@@ -82,6 +94,22 @@ def c2(N=100_000, gens=6):
         sampler=pa.GPUBatchSampler(seed=2))
     run("c2_adaptive_mad_N1e5_d4_S100", abc, dict(zip(keys, x0)), names, th,
         max_nr_populations=gens)
+
+
+def c2_file(N=100_000, gens=6):
+    """C2 with its History in a sqlite file (the reference's schema,
+    SURVEY 8(f) rank 1): the population writes overlap the generations."""
+    import tempfile
+    A, th, x0, keys, names = linear_problem(4, 100, 2.0)
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.AdaptivePNormDistance(
+        p=2, scale_function=pa.median_absolute_deviation),
+        population_size=N, eps=pa.QuantileEpsilon(alpha=0.5),
+        sampler=pa.GPUBatchSampler(seed=2))
+    db = pa.create_sqlite_db_id(tempfile.mkdtemp(), "c2.db")
+    run("c2_file_history_N1e5_d4_S100", abc, dict(zip(keys, x0)), names, th,
+        db=db, max_nr_populations=gens)
 
 
 def c4(N=200_000, gens=4):

@@ -175,7 +175,11 @@ def _flat_parameter_items(parameter):
 
 
 def _db_path(db):
-    """history.py:165-167 (``sqlite:///rel`` / ``sqlite:////abs``)."""
+    """history.py:165-167: ``sqlite:///rel`` / ``sqlite:////abs`` files,
+    ``sqlite://`` an in-memory SQLite database; any other id is a
+    device-only History (no SQL at all)."""
+    if db == "sqlite://":
+        return ":memory:"
     if not db.startswith("sqlite:///"):
         return None
     return db[len("sqlite:///"):]
@@ -255,8 +259,20 @@ class _SQLStore:
         distances [n], stats (keys, [S, n] float64) or per-particle dicts).
         Ids follow the reference's insertion order (history.py:632-687)."""
         with self.lock:
-            self._write_population(abc_id, t, eps, nr_samples, models,
-                                   stores_sum_stats, end_time)
+            self.begin()
+            try:
+                self._write_population(abc_id, t, eps, nr_samples, models,
+                                       stores_sum_stats, end_time)
+            except BaseException:
+                self.conn.rollback()
+                raise
+            self.conn.commit()
+
+    def begin(self):
+        """Take the write lock before reading the next ids, so Histories on
+        other connections to the same file cannot race for them."""
+        if not self.conn.in_transaction:
+            self.conn.execute("BEGIN IMMEDIATE")
 
     def _write_population(self, abc_id, t, eps, nr_samples, models,
                           stores_sum_stats, end_time):
@@ -338,7 +354,6 @@ class _SQLStore:
                         rows)
             pid += n
             mid += 1
-        c.commit()
 
 
 class History:
@@ -350,7 +365,8 @@ class History:
     def __init__(self, db="sqlite://", stores_sum_stats=True, _id=None,
                  create=True):
         path = _db_path(db)
-        if not create and (path is None or not os.path.exists(path)):
+        if not create and (path in (None, ":memory:")
+                           or not os.path.exists(path)):
             raise ValueError(f"Database file {db} does not exist.")
         self.db = db
         self.stores_sum_stats = stores_sum_stats
@@ -358,12 +374,30 @@ class History:
         self._pops = {}        # t -> dict(population, eps, n_sim, names)
         self._pre_nr_samples = 0
         self._meta = {}
+        self._path = path
         self._sql = _SQLStore(path) if path else None
         self._max_t = None
+        self._dup = set()      # t appended more than once: SQL readers only
         self._id = self._find_latest_id() if _id is None else _id
-        if self._id is None:
+        if self._id is None and self._sql is None:
             self._id = 1
         _REGISTRY[db] = self
+
+    def __getstate__(self):
+        """history.py:595-600: connections do not pickle; a file History
+        reconnects on unpickling (device populations are not carried)."""
+        if self._sql is not None:
+            self._sql.flush()
+        dct = self.__dict__.copy()
+        dct["_sql"] = None
+        dct["_pops"] = {}
+        return dct
+
+    def __setstate__(self, dct):
+        self.__dict__.update(dct)
+        if self._path not in (None, ":memory:"):
+            self._sql = _SQLStore(self._path)
+            self._max_t = None
 
     @staticmethod
     def lookup(db):
@@ -375,7 +409,7 @@ class History:
 
     @property
     def in_memory(self):
-        return self._sql is None
+        return self._path in (None, ":memory:")
 
     @property
     def db_size(self):
@@ -433,6 +467,7 @@ class History:
         s = self._sql
         s.flush()
         with s.lock:
+            s.begin()
             self._id = s.next_id("abc_smc")
             s.conn.execute("INSERT INTO abc_smc VALUES (?,?,?,?,?,?,?,?)",
                            (self._id, _now(), None, str(options),
@@ -467,6 +502,8 @@ class History:
     def append_population(self, t, current_epsilon, population, nr_simulations,
                           model_names):
         """history.py:696-729 (+ _save_to_population_db :616-693)."""
+        if t in self._pops:
+            self._dup.add(t)
         self._pops[t] = dict(population=population, eps=current_epsilon,
                              n_sim=nr_simulations, names=model_names,
                              end=datetime.datetime.now())
@@ -509,7 +546,18 @@ class History:
 
     # --- reading ----------------------------------------------------------
     def _mem(self, t):
-        return self._pops.get(t)
+        """This process's population at t, when readers may use it: every
+        population of a device-only History; with SQL, device populations
+        appended once (host particle lists are read back through SQL, as
+        the reference does, e.g. without their statistics when
+        stores_sum_stats is off)."""
+        e = self._pops.get(t)
+        if self._sql is None or e is None:
+            return e
+        if t in self._dup or not isinstance(e["population"],
+                                            ColumnarPopulation):
+            return None
+        return e
 
     def _q(self, sql, args=()):
         return self._sql.q(sql, args)

@@ -10,6 +10,7 @@ import sqlite3
 import sys
 
 import numpy as np
+import pandas as pd
 import pytest
 import torch
 
@@ -151,3 +152,221 @@ def test_open_errors_and_ids(tmp_path):
 def test_in_memory_id_keeps_device_populations():
     h = pa.History("sqlite://")
     assert h.in_memory and h.all_runs() == []
+
+
+# --- the reference's storage contract (test/test_storage.py), file and
+# in-memory SQL databases; R data frames (rpy2) are not available here ----
+def _example_df():
+    return pd.DataFrame({"col_a": [1, 2], "col_b": [1.1, 2.2],
+                         "col_c": ["foo", "bar"]},
+                        index=["ind_first", "ind_second"])
+
+
+def _one(w=.2):
+    return [pa.Particle(0, pa.Parameter({"a": 23, "b": 12}), w,
+                        [{"ss": .1}], [.1])]
+
+
+def _rand_pop_list(m, rng):
+    return [pa.Particle(m, pa.Parameter({"a": int(rng.integers(10)),
+                                         "b": float(rng.normal())}),
+                        float(rng.uniform()) * 42,
+                        [{"ss_float": 0.1, "ss_int": 42,
+                          "ss_str": "foo bar string",
+                          "ss_np": rng.uniform(size=(13, 42)),
+                          "ss_df": _example_df()}],
+                        [float(rng.uniform())])
+            for _ in range(int(rng.integers(10)) + 3)]
+
+
+@pytest.fixture(params=["file", "memory"])
+def history(request, tmp_path):
+    db = ("sqlite:///" + str(tmp_path / "history_test.db")
+          if request.param == "file" else "sqlite://")
+    h = pa.History(db)
+    h.store_initial_data(0, {}, {}, {},
+                         [f"fake_name_{k}" for k in range(50)], "", "",
+                         '{"name": "pop_strategy_str_test"}')
+    return h
+
+
+def test_ref_single_particle_np_int64_indexing(history):
+    history.append_population(0, 42, pa.Population(_one()), 2, [""])
+    for m in (0, np.int64(0)):
+        for t in (0, np.int64(0)):
+            df, w = history.get_distribution(m, t)
+            assert w[0] == 1 and df.a.iloc[0] == 23 and df.b.iloc[0] == 12
+
+
+def test_ref_save_no_sum_stats(history):
+    rng = np.random.default_rng(0)
+    plist = [pa.Particle(0, pa.Parameter({"th0": float(rng.uniform())}), .2,
+                         [{"ss0": float(rng.uniform()),
+                           "ss1": float(rng.uniform())}],
+                         [float(rng.uniform())]) for _ in range(6)]
+    pop = pa.Population(plist)
+    history.stores_sum_stats = False
+    history.append_population(t=0, current_epsilon=42.97, population=pop,
+                              nr_simulations=10, model_names=[""])
+    history.get_distribution(0, 0)
+    wd_h = history.get_weighted_distances()
+    wd = pop.get_weighted_distances()
+    assert (wd_h[["distance", "w"]] == wd[["distance", "w"]]).all().all()
+    weights, sum_stats = history.get_weighted_sum_stats(t=0)
+    assert len(weights) == len(plist)
+    assert all(not s for s in sum_stats)
+    history.get_population_extended()
+
+
+def test_ref_get_population(history):
+    rng = np.random.default_rng(1)
+    pop = pa.Population(_rand_pop_list(0, rng))
+    history.append_population(t=0, current_epsilon=7.0, population=pop,
+                              nr_simulations=200, model_names=["m0"])
+    pop_h = history.get_population(t=0)
+    assert len(pop) == len(pop_h)
+    np.testing.assert_allclose(
+        sum((p.accepted_distances for p in pop.get_list()), []),
+        sum((p.accepted_distances for p in pop_h.get_list()), []))
+    np.testing.assert_allclose([p.weight for p in pop.get_list()],
+                               [p.weight for p in pop_h.get_list()])
+
+
+def test_ref_sum_stats_save_load(history):
+    rng = np.random.default_rng(2)
+    arr, arr2 = rng.uniform(size=10), rng.uniform(size=(10, 2))
+    plist = [pa.Particle(0, pa.Parameter({"a": 23, "b": 12}), .2,
+                         [{"ss1": .1, "ss2": arr2, "ss3": _example_df()}],
+                         [.1]),
+             pa.Particle(0, pa.Parameter({"a": 23, "b": 12}), .2,
+                         [{"ss12": .11, "ss22": arr, "ss33": _example_df()}],
+                         [.1])]
+    history.append_population(0, 42, pa.Population(plist), 2, ["m1", "m2"])
+    weights, ss = history.get_weighted_sum_stats_for_model(0, 0)
+    assert (weights == 0.5).all()
+    assert ss[0]["ss1"] == .1 and (ss[0]["ss2"] == arr2).all()
+    assert (ss[0]["ss3"] == _example_df()).all().all()
+    assert ss[1]["ss12"] == .11 and (ss[1]["ss22"] == arr).all()
+    assert (ss[1]["ss33"] == _example_df()).all().all()
+
+
+def test_ref_total_nr_samples_and_t_count(history):
+    pop = pa.Population(_one())
+    history.append_population(0, 42, pop, 4234, ["m1"])
+    history.append_population(0, 42, pop, 3, ["m1"])
+    assert history.total_nr_simulations == 4237
+    for t in range(1, 10):
+        history.append_population(t, 42, pa.Population(_one()), 2, ["m1"])
+        assert history.max_t == t
+
+
+def test_ref_population_retrieval_and_models(history):
+    rng = np.random.default_rng(3)
+    history.append_population(1, .23, pa.Population(_rand_pop_list(0, rng)),
+                              234, ["m1"])
+    history.append_population(2, .123, pa.Population(_rand_pop_list(0, rng)),
+                              345, ["m1"])
+    history.append_population(2, .1235,
+                              pa.Population(_rand_pop_list(5, rng)), 20345,
+                              ["m1"] * 6)
+    history.append_population(3, .12330,
+                              pa.Population(_rand_pop_list(30, rng)), 30345,
+                              ["m1"] * 31)
+    df = history.get_all_populations()
+    assert list(df[df.t == 2].epsilon) == [.123, .1235]
+    assert list(df[df.t == 2].samples) == [345, 20345]
+    assert df[df.t == 3].samples.iloc[0] == 30345
+    assert history.alive_models(1) == [0]
+    assert history.alive_models(2) == [0, 5]
+    assert history.alive_models(3) == [30]
+    assert history.get_population_strategy()["name"] == \
+        "pop_strategy_str_test"
+
+
+def test_ref_model_probabilities(history):
+    rng = np.random.default_rng(4)
+    history.append_population(1, .23, pa.Population(_rand_pop_list(3, rng)),
+                              234, ["m0", "m1", "m2", "m3"])
+    probs = history.get_model_probabilities(1)
+    assert probs.p[3] == 1 and probs.index.tolist() == [3]
+    assert (history.get_model_probabilities()[3].values == [1]).all()
+
+
+def test_ref_population_extended_and_update_nr_samples(history):
+    rng = np.random.default_rng(5)
+    for t in range(3):
+        for m in range(4):
+            history.append_population(t, .23,
+                                      pa.Population(_rand_pop_list(m, rng)),
+                                      234, ["m0", "m1", "m2", "m3"])
+    df = history.get_population_extended(m=0)
+    assert len(df) > 0 and "sumstat_ss_np" in df.columns
+    history.store_initial_data(None, {}, {}, {}, ["m0"], "", "", "")
+    pops = history.get_all_populations()
+    assert pops[pops.t == pa.History.PRE_TIME].samples.values == 0
+    history.update_nr_samples(pa.History.PRE_TIME, 43)
+    pops = history.get_all_populations()
+    assert pops[pops.t == pa.History.PRE_TIME].samples.values == 43
+
+
+def test_ref_pickle(history):
+    import pickle
+    history.append_population(0, 42, pa.Population(_one()), 2, [""])
+    h2 = pickle.loads(pickle.dumps(history))
+    if not history.in_memory:
+        assert h2.get_distribution(0, 0)[0].a.iloc[0] == 23
+
+
+@pytest.mark.parametrize("gt_model", [0, None])
+def test_ref_observed_sum_stats_and_names(tmp_path, gt_model):
+    db = "sqlite:///" + str(tmp_path / "h.db")
+    obs = {"s1": 1, "s2": 1.1, "s3": np.array(.1),
+           "s4": np.random.default_rng(6).uniform(size=10)}
+    pa.History(db).store_initial_data(gt_model, {}, obs, {},
+                                      ["m1", "m2", "m3"], "", "", "")
+    h2 = pa.History(db)
+    got = h2.observed_sum_stat()
+    for k in ["s1", "s2", "s3"]:
+        assert got[k] == obs[k]
+    assert type(got["s1"]) is int and type(got["s2"]) is float
+    assert (got["s4"] == obs["s4"]).all() and got["s4"] is not obs["s4"]
+    assert h2.model_names() == ["m1", "m2", "m3"]
+
+
+def test_ref_dataframe_storage_readout(tmp_path):
+    """Four Histories (four connections) on one file, five models each."""
+    db = "sqlite:///" + str(tmp_path / "h.db")
+    rng = np.random.default_rng(7)
+    names = ["fake_name"] * 5
+    hs = []
+    for _ in range(4):
+        h = pa.History(db)
+        h.store_initial_data(0, {}, {}, {}, names, "", "", "")
+        hs.append(h)
+    pops = {}
+    for k, h in enumerate(hs):
+        for t in range(4):
+            plist = []
+            for m in range(5):
+                pops[(k, m, t)] = _rand_pop_list(m, rng)
+                plist += pops[(k, m, t)]
+            h.append_population(t, .1, pa.Population(plist), 2, names)
+    for k, h in enumerate(hs):
+        for t in range(4):
+            for m in range(5):
+                df, w = h.get_distribution(m, t)
+                assert np.isclose(w.sum(), 1)
+                exp = pops[(k, m, t)]
+                np.testing.assert_array_equal(df.a.values,
+                                              [p.parameter["a"] for p in exp])
+                np.testing.assert_array_equal(df.b.values,
+                                              [p.parameter["b"] for p in exp])
+
+
+def test_ref_create_db(tmp_path):
+    import tempfile
+    f = tempfile.mkstemp(suffix=".db", dir=str(tmp_path))[1]
+    pa.History("sqlite:///" + f, create=False)
+    os.remove(f)
+    with pytest.raises(ValueError):
+        pa.History("sqlite:///" + f, create=False)

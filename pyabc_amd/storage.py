@@ -221,6 +221,9 @@ class _SQLStore:
     def submit(self, fn, *args):
         self._pending.append(self._pool.submit(fn, *args))
 
+    def busy(self):
+        return any(not f.done() for f in self._pending)
+
     def flush(self):
         """Wait for queued writes (re-raising their errors)."""
         pending, self._pending = self._pending, []
@@ -569,11 +572,14 @@ class History:
     def max_t(self):
         if self._sql is None:
             return max(self._pops) if self._pops else -1
-        if self._max_t is None:
-            # cached, so the generation loop's reads do not wait for the
-            # writer thread (append_population keeps it current)
-            self._max_t = self._q("SELECT MAX(t) FROM populations WHERE "
-                                  "abc_smc_id=?", (self._id,))[0][0]
+        if self._max_t is not None and self._sql.busy():
+            # while this History's writes are queued, the generation loop
+            # reads the value append_population keeps current instead of
+            # waiting for the writer thread
+            return self._max_t
+        # otherwise the file's value (another History may have appended)
+        self._max_t = self._q("SELECT MAX(t) FROM populations WHERE "
+                              "abc_smc_id=?", (self._id,))[0][0]
         return self._max_t
 
     @property

@@ -300,3 +300,28 @@ def test_file_history_roundtrip_and_load(pa, tmp_path):
     assert pa.History(db, create=False).get_all_populations().t.max() == 3
     eps = _eps(pa.History(db, create=False))
     assert len(eps) == 4 and np.all(np.diff(eps) <= 0)
+
+
+@pytest.mark.parametrize("gt_model", [0, None])
+def test_resume_run_from_file(pa, tmp_path, gt_model):
+    """test/test_resume_run.py: a one-generation run, continued by a new
+    ABCSMC from the same file; both History objects see two populations."""
+    db = "sqlite:///" + str(tmp_path / "resume.db")
+    np.random.seed(5)
+
+    def model(parameter):
+        return {"data": parameter["mean"] + np.random.randn()}
+
+    def distance(x, y):
+        return abs(x["data"] - y["data"])
+    prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
+    abc = pa.ABCSMC(model, prior, distance, population_size=10)
+    history = abc.new(db, {"data": 2.5}, gt_model=gt_model)
+    run_id = history.id
+    hist_new = abc.run(minimum_epsilon=0, max_nr_populations=1)
+    assert hist_new.n_populations == 1
+    abc_continued = pa.ABCSMC(model, prior, distance)
+    abc_continued.load(db, run_id)
+    hist_contd = abc_continued.run(minimum_epsilon=0, max_nr_populations=1)
+    assert hist_contd.n_populations == 2
+    assert hist_new.n_populations == 2

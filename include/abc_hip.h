@@ -181,6 +181,12 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
                               void* ws, size_t ws_bytes, hipStream_t stream);
 int abc_column_std_f64(const double* data_T, int64_t ld, int64_t n, int S,
                        double* mean_out, double* std_out, hipStream_t stream);
+/* the same over S * bps blocks (one block per column leaves most CUs idle
+ * at S = 100): fixed-order partials in ws; mean_out may be NULL */
+size_t abc_column_std_workspace_bytes(int64_t n, int S);
+int abc_column_std_ws_f64(const double* data_T, int64_t ld, int64_t n, int S,
+                          double* mean_out, double* std_out, void* ws,
+                          size_t ws_bytes, hipStream_t stream);
 
 /* ---------------- (a7) weighted-quantile epsilon -------------------------
  * Replaces weighted_quantile                        weighted_statistics.py:26-43

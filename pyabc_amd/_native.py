@@ -104,6 +104,9 @@ _SIGS = {
                                           c_ptr, c_ptr, c_size, c_ptr]),
     "abc_column_std_f64": (c_int, [c_ptr, c_i64, c_i64, c_int, c_ptr, c_ptr,
                                    c_ptr]),
+    "abc_column_std_workspace_bytes": (c_size, [c_i64, c_int]),
+    "abc_column_std_ws_f64": (c_int, [c_ptr, c_i64, c_i64, c_int, c_ptr,
+                                      c_ptr, c_ptr, c_size, c_ptr]),
     # (a7)
     "abc_wquantile_workspace_bytes": (c_size, []),
     "abc_wquantile_f64": (c_int, [c_ptr, c_ptr, c_i64, c_dbl, c_ptr, c_ptr,

@@ -281,10 +281,41 @@ __global__ __launch_bounds__(256) void seg_hist_kernel(
   const unsigned long long prefix = st[s].prefix;
   const double c = MODE == 1 ? center[s] : 0.0;
   const double* col = data + static_cast<int64_t>(s) * ld;
-  for (int64_t i = static_cast<int64_t>(part) * 256 + threadIdx.x; i < n;
-       i += static_cast<int64_t>(bps) * 256) {
-    const uint64_t k = seg_key<MODE>(col[i], c);
-    if (((k ^ prefix) & mask) == 0) atomicAdd(&hc[(k >> shift) & 0xff], 1u);
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = static_cast<int64_t>(bps) * 256;
+  // every lane runs the same trip count (ballots need the whole wave); four
+  // independent loads per trip keep more bytes in flight per wave
+  for (int64_t i0 = static_cast<int64_t>(part) * 256; i0 < n; i0 += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      v[u] = i < n ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      bool in = false;
+      unsigned bin = 0;
+      if (i < n) {
+        const uint64_t k = seg_key<MODE>(v[u], c);
+        in = ((k ^ prefix) & mask) == 0;
+        bin = static_cast<unsigned>(k >> shift) & 0xffu;
+      }
+      // wave-aggregated count: in the leading passes most keys of a column
+      // share one bin (sign + exponent), and 64 same-address LDS atomics
+      // serialise; one add of the wave's count replaces them
+      const unsigned long long act = __ballot(in);
+      if (act == 0ull) continue;
+      const int leader = __ffsll(static_cast<long long>(act)) - 1;
+      const unsigned lb = __shfl(bin, leader, 64);
+      const unsigned long long same = __ballot(in && bin == lb);
+      if (same == act) {
+        if (lane == leader) atomicAdd(&hc[lb], static_cast<unsigned>(__popcll(act)));
+      } else if (in) {
+        atomicAdd(&hc[bin], 1u);
+      }
+    }
   }
   __syncthreads();
   if (hc[threadIdx.x]) atomicAdd(&hist[s * kBins + threadIdx.x], hc[threadIdx.x]);
@@ -335,10 +366,20 @@ __global__ __launch_bounds__(256) void seg_next_kernel(
   const double c = MODE == 1 ? center[s] : 0.0;
   const double* col = data + static_cast<int64_t>(s) * ld;
   unsigned long long kn = ~0ull;
-  for (int64_t i = static_cast<int64_t>(part) * 256 + threadIdx.x; i < n;
-       i += static_cast<int64_t>(bps) * 256) {
-    const uint64_t k = seg_key<MODE>(col[i], c);
-    if (k > key && k < kn) kn = k;
+  const int64_t stride = static_cast<int64_t>(bps) * 256;
+  for (int64_t i0 = static_cast<int64_t>(part) * 256 + threadIdx.x; i0 < n;
+       i0 += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      v[u] = i < n ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t k = seg_key<MODE>(v[u], c);
+      if (i0 + u * stride < n && k > key && k < kn) kn = k;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -646,6 +687,79 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
                        st, sst, S, n, out);
   }
   ABC_LAUNCH_CHECK("column median/mad kernels");
+  return kOk;
+}
+
+}  // extern "C"
+
+// column mean / std over S * bps blocks: fixed per-block partials, reduced
+// in a fixed order (bit-identical run to run; np.std's pairwise order is
+// matched to 1e-12, not bitwise)
+template <int PASS>  // 0: sum x, 1: sum (x - mean)^2
+__global__ __launch_bounds__(256) void col_part_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t n, int bps,
+    const double* __restrict__ mean, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int s = blockIdx.x / bps, b = blockIdx.x % bps;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  const double m = PASS == 1 ? mean[s] : 0.0;
+  double acc = 0.0;
+  for (int64_t i = static_cast<int64_t>(b) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(bps) * 256) {
+    const double x = col[i] - m;
+    acc += PASS == 1 ? x * x : x;
+  }
+  acc = block_sum<double, 256>(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(64) void col_fin_kernel(const double* __restrict__ part,
+                                                     int S, int bps, int64_t n,
+                                                     double* __restrict__ mean,
+                                                     double* __restrict__ std_out) {
+  const int s = blockIdx.x;
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < bps; b += 64) acc += part[s * bps + b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (threadIdx.x == 0) {
+    if (PASS == 0) mean[s] = acc / static_cast<double>(n);
+    else std_out[s] = sqrt(acc / static_cast<double>(n));
+  }
+}
+
+static int col_std_bps(int64_t n, int S) {
+  int bps = static_cast<int>(ceil_div(4096, S));
+  const int64_t maxb = ceil_div(n, 1024);   // >= 4 values per thread
+  if (bps > maxb) bps = static_cast<int>(maxb);
+  return bps < 1 ? 1 : bps;
+}
+
+extern "C" {
+
+size_t abc_column_std_workspace_bytes(int64_t n, int S) {
+  return static_cast<size_t>(S) * (col_std_bps(n, S) + 1) * 8 + 256;
+}
+
+int abc_column_std_ws_f64(const double* data_T, int64_t ld, int64_t n, int S,
+                          double* mean_out, double* std_out, void* ws,
+                          size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && S > 0 && ld >= n && std_out && ws, "std: bad args");
+  ABC_REQUIRE(ws_bytes >= abc_column_std_workspace_bytes(n, S),
+              "std: workspace too small");
+  const int bps = col_std_bps(n, S);
+  double* part = static_cast<double*>(ws);
+  double* mean = mean_out ? mean_out : part + static_cast<size_t>(S) * bps;
+  hipLaunchKernelGGL(col_part_kernel<0>, dim3(S * bps), dim3(256), 0, st, data_T,
+                     ld, n, bps, mean, part);
+  hipLaunchKernelGGL(col_fin_kernel<0>, dim3(S), dim3(64), 0, st, part, S, bps, n,
+                     mean, std_out);
+  hipLaunchKernelGGL(col_part_kernel<1>, dim3(S * bps), dim3(256), 0, st, data_T,
+                     ld, n, bps, mean, part);
+  hipLaunchKernelGGL(col_fin_kernel<1>, dim3(S), dim3(64), 0, st, part, S, bps, n,
+                     mean, std_out);
+  ABC_LAUNCH_CHECK("column std kernels");
   return kOk;
 }
 

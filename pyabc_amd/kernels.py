@@ -326,8 +326,10 @@ def column_std(data_T, n=None):
     n = ld if n is None else n
     mean = torch.empty(S, dtype=F64, device=_dev())
     std = torch.empty(S, dtype=F64, device=_dev())
-    call("abc_column_std_f64", ptr(data_T), ld, n, S, ptr(mean), ptr(std),
-         nat.stream())
+    wsb = nat.lib().abc_column_std_workspace_bytes(n, S)
+    ws = WS.get(wsb, "colstd")
+    call("abc_column_std_ws_f64", ptr(data_T), ld, n, S, ptr(mean), ptr(std),
+         ptr(ws), wsb, nat.stream())
     return mean, std
 
 

@@ -437,3 +437,41 @@ def test_local_logpdf_underflow_fixup(K):
     want = (mx[:, 0] + np.log(np.exp(e - mx).sum(axis=1))) - np.log(w.sum())
     assert np.all(np.isfinite(got))
     np.testing.assert_allclose(got, want, rtol=1e-11)
+
+
+@pytest.mark.parametrize("n", [1, 2, 1023, 300_001])
+def test_column_std_block_split(K, n):
+    """abc_column_std_ws_f64: S * bps fixed-order partials; np.std to 1e-12
+    and bit-identical run to run."""
+    rng = np.random.default_rng(n)
+    data = rng.normal(3.0, 2.0, size=(n, 7)) * np.array([1, 1e-3, 1e3, 1, 1,
+                                                           1, 0])[None, :]
+    data[:, 4] = 5.0                      # constant column: std exactly 0
+    mean, std = K.column_std(dev(data.T))
+    np.testing.assert_allclose(host(mean), data.mean(0), rtol=1e-12,
+                               atol=1e-300)
+    np.testing.assert_allclose(host(std), np.std(data, axis=0), rtol=1e-12,
+                               atol=1e-300)
+    assert host(std)[4] == 0.0
+    _, std2 = K.column_std(dev(data.T))
+    np.testing.assert_array_equal(host(std2), host(std))
+
+
+@pytest.mark.parametrize("n", [200_000, 200_001])
+def test_column_median_mad_skewed(K, n):
+    """Wave-aggregated histogram counts: columns where most keys share one
+    bin (ties, one dominant value, a tail of distinct values), and ragged
+    tails (n not a multiple of 64) -- bit-exact np.median / MAD."""
+    rng = np.random.default_rng(n)
+    S = 5
+    data = np.empty((n, S))
+    data[:, 0] = 1.0
+    data[:, 1] = np.where(rng.uniform(size=n) < 0.9, 2.5, rng.normal(size=n))
+    data[:, 2] = rng.integers(0, 3, size=n).astype(float)
+    data[:, 3] = rng.normal(size=n)
+    data[:, 4] = np.where(rng.uniform(size=n) < 0.5, -0.0, 1e-300)
+    med, mad = K.column_median_mad(dev(data.T))
+    np.testing.assert_array_equal(host(med), np.median(data, axis=0))
+    mad_ref = np.array([np.median(np.abs(data[:, k] - np.median(data[:, k])))
+                        for k in range(S)])
+    np.testing.assert_array_equal(host(mad), mad_ref)

@@ -262,7 +262,19 @@ struct SegState {
   long long less;       // count of keys < prefix
   long long eq;         // count == final key
   unsigned long long knext;
+  long long cand;       // keys in the selected bin of the last pass
+  unsigned long long ccount;  // keys compacted into the candidate buffer
+  int compacted;        // the remaining passes read the candidate buffer
+  int pad;
 };
+
+// After kCompactPass + 1 passes (24 key bits) a column's candidates are
+// usually a few hundred keys: they are compacted (one more read) and the
+// remaining passes histogram the buffer instead of re-reading the column.
+// A column with more than kCandCap candidates (ties, one dominant value)
+// keeps reading its full column.
+constexpr int kCompactPass = 2;
+constexpr int kCandCap = 4096;
 
 template <int MODE>  // 0: key(x), 1: key(|x - center|)
 __device__ inline uint64_t seg_key(double x, double c) {
@@ -276,6 +288,7 @@ __global__ __launch_bounds__(256) void seg_hist_kernel(
     int shift, unsigned long long mask, unsigned* __restrict__ hist) {
   __shared__ unsigned hc[kBins];
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  if (st[s].compacted) return;   // block-uniform: seg_hist_cand_kernel's
   hc[threadIdx.x] = 0;
   __syncthreads();
   const unsigned long long prefix = st[s].prefix;
@@ -342,6 +355,7 @@ __global__ __launch_bounds__(256) void seg_select_kernel(SegState* st, int shift
     st[s].prefix |= static_cast<unsigned long long>(t) << shift;
     st[s].rank = rank - excl;
     st[s].less += excl;
+    st[s].cand = v;
     if (last) st[s].eq = v;
   }
   hist[s * kBins + t] = 0;
@@ -355,6 +369,78 @@ __global__ void seg_init_kernel(SegState* st, int S, long long rank) {
   st[s].less = 0;
   st[s].eq = 0;
   st[s].knext = ~0ull;
+  st[s].cand = 0;
+  st[s].ccount = 0;
+  st[s].compacted = 0;
+}
+
+__global__ void seg_mark_kernel(SegState* st, int S) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  st[s].compacted = st[s].cand <= kCandCap ? 1 : 0;
+}
+
+// keys of the selected 24-bit bucket -> cbuf[s][kCandCap] (any order: an
+// order statistic does not depend on it)
+template <int MODE>
+__global__ __launch_bounds__(256) void seg_compact_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t n, int bps,
+    const double* __restrict__ center, SegState* st, unsigned long long mask,
+    unsigned long long* __restrict__ cbuf) {
+  const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  if (!st[s].compacted) return;
+  const unsigned long long prefix = st[s].prefix;
+  const double c = MODE == 1 ? center[s] : 0.0;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  unsigned long long* out = cbuf + static_cast<int64_t>(s) * kCandCap;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = static_cast<int64_t>(bps) * 256;
+  for (int64_t i0 = static_cast<int64_t>(part) * 256; i0 < n; i0 += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      v[u] = i < n ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      const uint64_t k = seg_key<MODE>(v[u], c);
+      const bool in = i < n && ((k ^ prefix) & mask) == 0;
+      const unsigned long long m = __ballot(in);
+      if (m == 0ull) continue;
+      const int leader = __ffsll(static_cast<long long>(m)) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(&st[s].ccount,
+                                           static_cast<unsigned long long>(__popcll(m)));
+      base = __shfl(base, leader, 64);
+      if (in) {
+        const unsigned long long slot =
+            base + __popcll(m & ((1ull << lane) - 1ull));
+        if (slot < kCandCap) out[slot] = k;   // cand <= cap: always true
+      }
+    }
+  }
+}
+
+// histogram pass over a compacted column's candidate keys (one block each)
+__global__ __launch_bounds__(256) void seg_hist_cand_kernel(
+    const SegState* __restrict__ st, const unsigned long long* __restrict__ cbuf,
+    int shift, unsigned long long mask, unsigned* __restrict__ hist) {
+  __shared__ unsigned hc[kBins];
+  const int s = blockIdx.x;
+  if (!st[s].compacted) return;
+  hc[threadIdx.x] = 0;
+  __syncthreads();
+  const unsigned long long prefix = st[s].prefix;
+  const long long cnt = static_cast<long long>(st[s].ccount);
+  const unsigned long long* keys = cbuf + static_cast<int64_t>(s) * kCandCap;
+  for (long long i = threadIdx.x; i < cnt; i += 256) {
+    const uint64_t k = keys[i];
+    if (((k ^ prefix) & mask) == 0) atomicAdd(&hc[(k >> shift) & 0xff], 1u);
+  }
+  __syncthreads();
+  if (hc[threadIdx.x]) atomicAdd(&hist[s * kBins + threadIdx.x], hc[threadIdx.x]);
 }
 
 template <int MODE>
@@ -639,7 +725,8 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
 }
 
 size_t abc_column_select_workspace_bytes(int S) {
-  return static_cast<size_t>(S) * (sizeof(SegState) + kBins * 4) + 256;
+  return static_cast<size_t>(S) * (sizeof(SegState) + kBins * 4 +
+                                   kCandCap * 8) + 256;
 }
 
 // median (and MAD when mad_out != NULL) of every column of data_T[S][ld]
@@ -652,6 +739,8 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
   SegState* sst = static_cast<SegState*>(ws);
   unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
                                                static_cast<size_t>(S) * sizeof(SegState));
+  unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
+      hist + static_cast<size_t>(S) * kBins);
   ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * kBins * 4, st));
   int bps = static_cast<int>(ceil_div(2048, S));
   const int64_t maxb = ceil_div(n, 256);
@@ -672,8 +761,22 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
       else
         hipLaunchKernelGGL(seg_hist_kernel<1>, dim3(S * bps), dim3(256), 0, st,
                            data_T, ld, n, S, bps, center, sst, shift, mask, hist);
+      if (pass > kCompactPass)
+        hipLaunchKernelGGL(seg_hist_cand_kernel, dim3(S), dim3(256), 0, st, sst,
+                           cbuf, shift, mask, hist);
       hipLaunchKernelGGL(seg_select_kernel, dim3(S), dim3(256), 0, st, sst, shift,
                          hist, pass == 7 ? 1 : 0);
+      if (pass == kCompactPass) {
+        const unsigned long long cmask = ~0ull << shift;
+        hipLaunchKernelGGL(seg_mark_kernel, dim3(ceil_div(S, 256)), dim3(256), 0,
+                           st, sst, S);
+        if (round == 0)
+          hipLaunchKernelGGL(seg_compact_kernel<0>, dim3(S * bps), dim3(256), 0, st,
+                             data_T, ld, n, bps, center, sst, cmask, cbuf);
+        else
+          hipLaunchKernelGGL(seg_compact_kernel<1>, dim3(S * bps), dim3(256), 0, st,
+                             data_T, ld, n, bps, center, sst, cmask, cbuf);
+      }
     }
     if ((n & 1) == 0) {
       if (round == 0)

@@ -265,16 +265,18 @@ struct SegState {
   long long cand;       // keys in the selected bin of the last pass
   unsigned long long ccount;  // keys compacted into the candidate buffer
   int compacted;        // the remaining passes read the candidate buffer
+  int fresh;            // compacted by the pass that just ended
+  int next_done;        // knext found among the candidates
   int pad;
 };
 
-// After kCompactPass + 1 passes (24 key bits) a column's candidates are
-// usually a few hundred keys: they are compacted (one more read) and the
-// remaining passes histogram the buffer instead of re-reading the column.
-// A column with more than kCandCap candidates (ties, one dominant value)
-// keeps reading its full column.
-constexpr int kCompactPass = 2;
-constexpr int kCandCap = 4096;
+// After 16 (or, failing that, 24) key bits a column's selected bucket is
+// usually far smaller than the column: its keys are compacted (one more
+// read) and the remaining passes histogram the buffer instead of
+// re-reading the column.  A column whose bucket exceeds kCandCap keys
+// (ties, one dominant value) keeps reading its full column.
+constexpr int kCompactFirst = 1, kCompactLast = 2;
+constexpr int kCandCap = 65536;
 
 template <int MODE>  // 0: key(x), 1: key(|x - center|)
 __device__ inline uint64_t seg_key(double x, double c) {
@@ -372,12 +374,16 @@ __global__ void seg_init_kernel(SegState* st, int S, long long rank) {
   st[s].cand = 0;
   st[s].ccount = 0;
   st[s].compacted = 0;
+  st[s].fresh = 0;
+  st[s].next_done = 0;
 }
 
 __global__ void seg_mark_kernel(SegState* st, int S) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
-  st[s].compacted = st[s].cand <= kCandCap ? 1 : 0;
+  const int now = !st[s].compacted && st[s].cand <= kCandCap;
+  st[s].fresh = now;
+  if (now) st[s].compacted = 1;
 }
 
 // keys of the selected 24-bit bucket -> cbuf[s][kCandCap] (any order: an
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(256) void seg_compact_kernel(
     const double* __restrict__ center, SegState* st, unsigned long long mask,
     unsigned long long* __restrict__ cbuf) {
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
-  if (!st[s].compacted) return;
+  if (!st[s].fresh) return;
   const unsigned long long prefix = st[s].prefix;
   const double c = MODE == 1 ? center[s] : 0.0;
   const double* col = data + static_cast<int64_t>(s) * ld;
@@ -448,6 +454,7 @@ __global__ __launch_bounds__(256) void seg_next_kernel(
     const double* __restrict__ data, int64_t ld, int64_t n, int bps,
     const double* __restrict__ center, SegState* st) {
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  if (st[s].next_done) return;
   const unsigned long long key = st[s].prefix;
   const double c = MODE == 1 ? center[s] : 0.0;
   const double* col = data + static_cast<int64_t>(s) * ld;
@@ -473,6 +480,38 @@ __global__ __launch_bounds__(256) void seg_next_kernel(
     kn = b < kn ? b : kn;
   }
   if ((threadIdx.x & 63) == 0 && kn != ~0ull) atomicMin(&st[s].knext, kn);
+}
+
+// smallest key above the selected one, from a compacted column's bucket;
+// when the bucket holds none, the full scan (seg_next_kernel) finds it
+__global__ __launch_bounds__(256) void seg_next_cand_kernel(
+    SegState* st, const unsigned long long* __restrict__ cbuf) {
+  __shared__ unsigned long long red[4];
+  const int s = blockIdx.x;
+  if (!st[s].compacted) return;
+  const unsigned long long key = st[s].prefix;
+  const long long cnt = static_cast<long long>(st[s].ccount);
+  const unsigned long long* keys = cbuf + static_cast<int64_t>(s) * kCandCap;
+  unsigned long long kn = ~0ull;
+  for (long long i = threadIdx.x; i < cnt; i += 256) {
+    const unsigned long long k = keys[i];
+    if (k > key && k < kn) kn = k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(kn, o, 64);
+    kn = b < kn ? b : kn;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kn;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) kn = red[w] < kn ? red[w] : kn;
+    kn = red[0] < kn ? red[0] : kn;
+    if (kn != ~0ull) {
+      st[s].knext = kn;
+      st[s].next_done = 1;
+    }
+  }
 }
 
 // median = a (odd n) or (a + b) / 2 (even n), np.median semantics
@@ -761,12 +800,12 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
       else
         hipLaunchKernelGGL(seg_hist_kernel<1>, dim3(S * bps), dim3(256), 0, st,
                            data_T, ld, n, S, bps, center, sst, shift, mask, hist);
-      if (pass > kCompactPass)
+      if (pass > kCompactFirst)
         hipLaunchKernelGGL(seg_hist_cand_kernel, dim3(S), dim3(256), 0, st, sst,
                            cbuf, shift, mask, hist);
       hipLaunchKernelGGL(seg_select_kernel, dim3(S), dim3(256), 0, st, sst, shift,
                          hist, pass == 7 ? 1 : 0);
-      if (pass == kCompactPass) {
+      if (pass >= kCompactFirst && pass <= kCompactLast) {
         const unsigned long long cmask = ~0ull << shift;
         hipLaunchKernelGGL(seg_mark_kernel, dim3(ceil_div(S, 256)), dim3(256), 0,
                            st, sst, S);
@@ -779,6 +818,8 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
       }
     }
     if ((n & 1) == 0) {
+      hipLaunchKernelGGL(seg_next_cand_kernel, dim3(S), dim3(256), 0, st, sst,
+                         cbuf);
       if (round == 0)
         hipLaunchKernelGGL(seg_next_kernel<0>, dim3(S * bps), dim3(256), 0, st,
                            data_T, ld, n, bps, center, sst);

@@ -214,6 +214,14 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
                          double* out_logpdf, void* ws, size_t ws_bytes,
                          hipStream_t stream);
 size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N);
+/* the same density with the pair loop in fp32 (1e-5 relative; rows whose
+ * sum falls below 2^-60 are re-evaluated exactly in fp64) */
+int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
+                         const double* w, const double* inv_covs,
+                         const double* dets, int64_t N, int d,
+                         double* out_logpdf, void* ws, size_t ws_bytes,
+                         hipStream_t stream);
+size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N);
 /* LocalTransition.rvs_single                        local_transition.py:141-145
  * (CDF index as abc_propose_philox_f64; Cholesky factor of C[idx]) */
 int abc_propose_local_philox_f64(const double* X, int64_t N, int d,

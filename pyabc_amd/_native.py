@@ -121,6 +121,10 @@ _SIGS = {
     "abc_local_logpdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
                                      c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                      c_size, c_ptr]),
+    "abc_local_logpdf_f32": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+                                     c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                     c_size, c_ptr]),
+    "abc_local_logpdf_f32_workspace_bytes": (c_size, [c_i64, c_i64]),
     "abc_propose_local_philox_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr,
                                              c_ptr, c_ptr, c_ptr, c_u64,
                                              c_u64, c_u64, c_i64, c_ptr,

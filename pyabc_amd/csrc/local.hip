@@ -492,16 +492,90 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
   if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
 }
 
+// fp32 pass (precision="f32", 1e-5 relative): the same sum with the
+// population centred on X[0] in fp64 then rounded to fp32, the packed
+// coefficients pre-scaled by log2(e)/2 and lc by log2(e), so a term is one
+// v_exp_f32 of (lc2_n - q'_n); 16 terms are added in fp32, then into fp64.
+template <int D>
+__global__ __launch_bounds__(256) void local_pack32_kernel(
+    const double* __restrict__ X, const double* __restrict__ coef,
+    const double* __restrict__ lc, const unsigned long long* __restrict__ lc_max_key,
+    int64_t N, float* __restrict__ X32, float* __restrict__ coef32,
+    float* __restrict__ lc32) {
+  constexpr int NC = D * (D + 1) / 2;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (n >= N) return;
+  const double L = key_f64(*lc_max_key);
+  constexpr double kLog2e = 1.4426950408889634;
+#pragma unroll
+  for (int q = 0; q < D; ++q) X32[n * D + q] = static_cast<float>(X[n * D + q] - X[q]);
+#pragma unroll
+  for (int t = 0; t < NC; ++t)
+    coef32[n * NC + t] = static_cast<float>(coef[n * NC + t] * (0.5 * kLog2e));
+  lc32[n] = static_cast<float>((lc[n] - L) * kLog2e);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void local_pts32_kernel(const double* __restrict__ pts,
+                                                          int64_t M,
+                                                          const double* __restrict__ X,
+                                                          float* __restrict__ pts32) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= M) return;
+#pragma unroll
+  for (int q = 0; q < D; ++q) pts32[i * D + q] = static_cast<float>(pts[i * D + q] - X[q]);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void local_pdf32_kernel(
+    const float* __restrict__ pts, int64_t M, const float* __restrict__ X,
+    const float* __restrict__ coef, const float* __restrict__ lc, int64_t N,
+    int split, int64_t nchunk, double* __restrict__ part) {
+  constexpr int NC = D * (D + 1) / 2;
+  const int s = blockIdx.x % split;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
+  const int64_t i = i0 < M ? i0 : M - 1;
+  float th[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
+  double acc = 0.0;
+  const int64_t n0 = static_cast<int64_t>(s) * nchunk;
+  int64_t n1 = n0 + nchunk;
+  if (n1 > N) n1 = N;
+  for (int64_t b = n0; b < n1; b += 16) {
+    const int64_t be = b + 16 < n1 ? b + 16 : n1;
+    float a16 = 0.0f;
+    for (int64_t n = b; n < be; ++n) {
+      float dl[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
+      const float* c = coef + n * NC;
+      float qf = 0.0f;
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+        float r = c[t++] * dl[a];
+#pragma unroll
+        for (int bb = a + 1; bb < D; ++bb) r = fmaf(c[t++], dl[bb], r);
+        qf = fmaf(dl[a], r, qf);
+      }
+      a16 += __builtin_amdgcn_exp2f(lc[n] - qf);
+    }
+    acc += static_cast<double>(a16);
+  }
+  if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
+}
+
 __global__ __launch_bounds__(256) void local_pdf_final_kernel(
     const double* __restrict__ part, int64_t M, int split,
     const unsigned long long* __restrict__ lc_max_key,
     const double* __restrict__ logsumw, double* __restrict__ out,
-    int* __restrict__ n_fix, int* __restrict__ fix_rows) {
+    int* __restrict__ n_fix, int* __restrict__ fix_rows, double thresh) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= M) return;
   double S = 0.0;
   for (int s = 0; s < split; ++s) S += part[s * M + i];
-  if (S >= 1e-280) {
+  if (S >= thresh) {
     out[i] = key_f64(*lc_max_key) + log(S) - *logsumw;
   } else {  // the fixed offset underflowed: exact two-pass evaluation
     fix_rows[atomicAdd(n_fix, 1)] = static_cast<int>(i);
@@ -775,7 +849,7 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
                      M, X, coef, lc, lc_max_key, N, split, nchunk, part);       \
   hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256), \
                      0, st, part, M, split, lc_max_key, logsumw, out_logpdf,    \
-                     n_fix, fix_rows);                                          \
+                     n_fix, fix_rows, 1e-280);                                  \
   hipLaunchKernelGGL((local_pdf_fixup_kernel<DD>), dim3(64), dim3(256), 0, st,  \
                      pts, X, coef, lc, N, logsumw, n_fix, fix_rows, out_logpdf);
   switch (d) {
@@ -790,6 +864,75 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
   }
 #undef L
   ABC_LAUNCH_CHECK("local_logpdf kernels");
+  return kOk;
+}
+
+size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N) {
+  // the fp64 layout, then X32[N][8] | coef32[N][36] | lc32[N] | pts32[M][8]
+  return abc_local_logpdf_workspace_bytes(M, N) +
+         static_cast<size_t>(N) * 4 * 45 + static_cast<size_t>(M) * 4 * 8 + 512;
+}
+
+int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
+                         const double* w, const double* inv_covs,
+                         const double* dets, int64_t N, int d,
+                         double* out_logpdf, void* ws, size_t ws_bytes,
+                         hipStream_t st) {
+  ABC_REQUIRE(M >= 0 && N >= 1, "local_logpdf_f32: bad sizes");
+  if (M == 0) return kOk;
+  ABC_REQUIRE(d >= 1 && d <= 8, "local_logpdf_f32: unsupported d=%d (d <= 8)", d);
+  ABC_REQUIRE(pts && X && w && inv_covs && dets && out_logpdf && ws,
+              "local_logpdf_f32: null pointer");
+  ABC_REQUIRE(ws_bytes >= abc_local_logpdf_f32_workspace_bytes(M, N),
+              "local_logpdf_f32: workspace too small");
+  int split;
+  int64_t nchunk;
+  local_plan(M, N, split, nchunk);
+  char* base = static_cast<char*>(ws);
+  double* logsumw = reinterpret_cast<double*>(base);
+  unsigned long long* lc_max_key = reinterpret_cast<unsigned long long*>(base + 8);
+  int* n_fix = reinterpret_cast<int*>(base + 16);
+  double* lc = reinterpret_cast<double*>(base + 64);
+  double* coef = lc + N;
+  double* part = coef + N * 36;
+  int* fix_rows = reinterpret_cast<int*>(part + static_cast<int64_t>(split) * M);
+  float* X32 = reinterpret_cast<float*>(
+      base + ((abc_local_logpdf_workspace_bytes(M, N) + 255) / 256) * 256);
+  float* coef32 = X32 + N * 8;
+  float* lc32 = coef32 + N * 36;
+  float* pts32 = lc32 + N;
+  ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
+  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
+  hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
+                     st, w, dets, inv_covs, N, d, lc, coef, lc_max_key);
+  const unsigned grid = static_cast<unsigned>(ceil_div(M, 256) * split);
+  // rows whose fp32 sum is below 2^-60 take the exact fp64 fixup: the terms
+  // lost to fp32 underflow (< 2^-126 each) are then < 2^-40 of the sum
+  const double thresh = 8.673617379884035e-19;
+#define L(DD)                                                                    \
+  hipLaunchKernelGGL((local_pack32_kernel<DD>), dim3(ceil_div(N, 256)), dim3(256), \
+                     0, st, X, coef, lc, lc_max_key, N, X32, coef32, lc32);      \
+  hipLaunchKernelGGL((local_pts32_kernel<DD>), dim3(ceil_div(M, 256)), dim3(256),  \
+                     0, st, pts, M, X, pts32);                                   \
+  hipLaunchKernelGGL((local_pdf32_kernel<DD>), dim3(grid), dim3(256), 0, st,       \
+                     pts32, M, X32, coef32, lc32, N, split, nchunk, part);       \
+  hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),  \
+                     0, st, part, M, split, lc_max_key, logsumw, out_logpdf,     \
+                     n_fix, fix_rows, thresh);                                   \
+  hipLaunchKernelGGL((local_pdf_fixup_kernel<DD>), dim3(64), dim3(256), 0, st,   \
+                     pts, X, coef, lc, N, logsumw, n_fix, fix_rows, out_logpdf);
+  switch (d) {
+    case 1: L(1) break;
+    case 2: L(2) break;
+    case 3: L(3) break;
+    case 4: L(4) break;
+    case 5: L(5) break;
+    case 6: L(6) break;
+    case 7: L(7) break;
+    case 8: L(8) break;
+  }
+#undef L
+  ABC_LAUNCH_CHECK("local_logpdf_f32 kernels");
   return kOk;
 }
 

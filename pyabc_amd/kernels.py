@@ -373,14 +373,19 @@ def local_cov(X, w, nbr, scaling=1.0):
     return covs, invs, dets
 
 
-def local_logpdf(pts, X, w, invs, dets):
+def local_logpdf(pts, X, w, invs, dets, precision="f64"):
+    """log LocalTransition density; ``precision`` "f64" (1e-12) or "f32"
+    (pair loop in fp32, 1e-5 relative)."""
+    if precision not in ("f64", "f32"):
+        raise ValueError(f"unknown LocalTransition precision {precision!r}")
     pts = _contig(pts, F64)
     M, d = pts.shape
     N = X.shape[0]
     out = torch.empty(M, dtype=F64, device=_dev())
-    wsb = nat.lib().abc_local_logpdf_workspace_bytes(M, N)
+    wsb = getattr(nat.lib(), f"abc_local_logpdf{'_f32' if precision == 'f32' else ''}"
+                  "_workspace_bytes")(M, N)
     ws = WS.get(wsb, "localpdf")
-    call("abc_local_logpdf_f64", ptr(pts), M, ptr(_contig(X, F64)),
+    call(f"abc_local_logpdf_{precision}", ptr(pts), M, ptr(_contig(X, F64)),
          ptr(_contig(w, F64)), ptr(invs), ptr(dets), N, d, ptr(out), ptr(ws),
          wsb, nat.stream())
     return out

@@ -215,7 +215,13 @@ class LocalTransition(Transition):
     EPS = 1e-3
     MIN_K = 10
 
-    def __init__(self, k=None, k_fraction=1 / 4, scaling=1):
+    def __init__(self, k=None, k_fraction=1 / 4, scaling=1,
+                 kde_precision="f32"):
+        # kde_precision: the density pass's pair loop in "f32" (1e-5
+        # relative, the default, as for the MVN transition) or "f64" (1e-12)
+        if kde_precision not in ("f32", "f64"):
+            raise ValueError(f"unknown kde_precision {kde_precision!r}")
+        self.kde_precision = kde_precision
         if k_fraction is not None:
             self.k_fraction = k_fraction
             self._k = None
@@ -306,7 +312,7 @@ class LocalTransition(Transition):
 
     def logpdf_device(self, theta):
         return K.local_logpdf(theta, self._Xd, self._wd, self._invs,
-                              self._dets)
+                              self._dets, self.kde_precision)
 
     def rvs_single(self):
         return self._draw(1, True)
@@ -334,10 +340,12 @@ class _LocalDeviceFit:
         self.n = self.X.shape[0]
         self.cdf = tr._cdf
         self._covs, self._invs, self._dets = tr._covs, tr._invs, tr._dets
+        self.kde_precision = tr.kde_precision
 
     def propose(self, lo, scale, seed, sid, offset, B):
         return K.propose_local(self.X, self.cdf, self._covs, seed, sid,
                                offset, B, lo, scale)
 
     def logpdf(self, theta):
-        return K.local_logpdf(theta, self.X, self.w, self._invs, self._dets)
+        return K.local_logpdf(theta, self.X, self.w, self._invs, self._dets,
+                              self.kde_precision)

@@ -165,13 +165,18 @@ def test_mvn_transition_api_vs_golden(pa):
 def test_local_transition_api_vs_golden(pa):
     g = load_golden("local_N2000_d6_k50")
     cols = [f"p{k:02d}" for k in range(6)]
-    tr = pa.LocalTransition(k=50, k_fraction=None)
+    tr = pa.LocalTransition(k=50, k_fraction=None, kde_precision="f64")
     tr.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
     assert tr.k == int(g["k"])
     np.testing.assert_allclose(tr.covs, g["covs"], rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(tr.determinants, g["dets"], rtol=1e-11)
     got = tr.pdf(pd.DataFrame(g["pts"], columns=cols))
     np.testing.assert_allclose(got, g["pdf"], rtol=1e-11)
+    # the default fp32 density pass: the north-star fp32 bar
+    tr32 = pa.LocalTransition(k=50, k_fraction=None)
+    tr32.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
+    got32 = tr32.pdf(pd.DataFrame(g["pts"], columns=cols))
+    np.testing.assert_allclose(got32, g["pdf"], rtol=1e-5)
 
 
 @pytest.mark.parametrize("tag", ["even_n1000", "odd_n999"])

@@ -475,3 +475,26 @@ def test_column_median_mad_skewed(K, n):
     mad_ref = np.array([np.median(np.abs(data[:, k] - np.median(data[:, k])))
                         for k in range(S)])
     np.testing.assert_array_equal(host(mad), mad_ref)
+
+
+@pytest.mark.parametrize("d,offset", [(6, 0.0), (6, 40.0), (2, 0.0), (8, 3.0)])
+def test_local_logpdf_f32_vs_exact(K, d, offset):
+    """precision="f32" LocalTransition density (pair loop in fp32, centred on
+    X[0]): within 1e-5 relative of the exact fp64 density (north_star's fp32
+    bar), including far points (exact fixup) and an offset population."""
+    rng = np.random.default_rng(d * 7 + int(offset))
+    n, k = 4000, 50
+    X = rng.normal(size=(n, d)) @ (np.eye(d) + 0.4 * rng.normal(size=(d, d)))
+    X += offset
+    w = rng.uniform(0.1, 1.0, size=n)
+    nbr, _ = K.knn(dev(X), k)
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    pts = np.concatenate([X[rng.integers(0, n, 300)] +
+                          0.3 * rng.normal(size=(300, d)),
+                          rng.normal(size=(20, d)) * 3 + offset,
+                          np.full((3, d), 30.0 + offset)])
+    exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
+    got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets,
+                              precision="f32"))
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(np.exp(got - exact), 1.0, atol=1e-5)

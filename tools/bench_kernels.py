@@ -189,6 +189,9 @@ def main():
     t = timed(lambda: K.local_logpdf(pts, X4, w4, invs, dets), reps=2)
     report("local_logpdf_f64", t, N4 * N4, "pairs",
            3 * d4 + 2 * d4 * d4 + 4, "valu_f64", {"N": N4, "d": d4})
+    t = timed(lambda: K.local_logpdf(pts, X4, w4, invs, dets, "f32"), reps=2)
+    report("local_logpdf_f32", t, N4 * N4, "pairs",
+           3 * d4 + 2 * d4 * d4 + 4, "valu_f32", {"N": N4, "d": d4})
 
 
 if __name__ == "__main__":

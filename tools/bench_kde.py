@@ -70,6 +70,15 @@ if __name__ == "__main__":
             print(f"ib {ib}:", end=" ")
             run(100000, 100000, 4, "mfma", reps=3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "d20":
+        # launch-shape sweep of the MFMA pass at d = 20 (config 5)
+        for pipe in ["0", "1"]:
+            for ib in ["2", "1"]:
+                os.environ["ABC_KDE_MFMA_PIPE"] = pipe
+                os.environ["ABC_KDE_MFMA_IB"] = ib
+                print(f"pipe {pipe} ib {ib}:", end=" ")
+                run(262144, 262144, 20, "mfma", reps=3)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "mfma":
         for (N, M, d) in [(1000000, 1000000, 8), (262144, 262144, 8),
                           (1000000, 500000, 8), (1000000, 125000, 8),

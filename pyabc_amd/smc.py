@@ -114,7 +114,9 @@ class ABCSMC:
     # ------------------------------------------------------------------
     def new(self, db, observed_sum_stat=None, *, gt_model=None, gt_par=None,
             meta_info=None):
-        """Start a run (smc.py:248-346); ``db`` names an in-memory History."""
+        """Start a run (smc.py:248-346).  ``db``: ``"sqlite:///file.db"``
+        (the reference's SQL schema on disk), ``"sqlite://"`` (the same in
+        memory) or any other id (device populations only, no SQL)."""
         self.x_0 = {} if observed_sum_stat is None else observed_sum_stat
         self.history = History(db)
         self.history.store_initial_data(

@@ -398,6 +398,100 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
   }
 }
 
+// The same pass with the A fragments of each 64-row chunk staged once per
+// block in LDS (double-buffered) and shared by the kWaves waves, which walk
+// the same j-segments.  Where the register version needs more than 256
+// VGPRs (d > 8: one wave per SIMD, MFMA chain and VALU back to back) this
+// frees the a[2][KT] registers, and L2 serves each fragment once per block
+// instead of once per wave.  Per-lane arithmetic and order are those of
+// kde_mfma_kernel<.., PIPE = false>: the two give bit-identical rows.
+template <int KH, int KL, int IB>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT * 64;  // fragments of one 64-row chunk
+  constexpr int PER = (CH + 64 * kWaves - 1) / (64 * kWaves);
+  __shared__ bf16x8 As[2][CH];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    bf16x8 stage[PER];
+    if (nj > 0) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int idx = threadIdx.x + q * 64 * kWaves;
+        if (idx < CH) As[0][idx] = Aseg[idx];
+      }
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int jc = 0; jc < nj; jc += 64) {
+      const bool more = jc + 64 < nj;
+      if (more) {  // next chunk into registers; written after this compute
+        const bf16x8* __restrict__ an = Aseg + ((jc + 64) >> 5) * KT * 64;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const int idx = threadIdx.x + q * 64 * kWaves;
+          if (idx < CH) stage[q] = an[idx];
+        }
+      }
+      const bf16x8* __restrict__ Ab = As[buf];
+      float sacc[IB];
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 2 * IB; ++q) {
+        const int tile = q / IB, it = q % IB;
+        f32x16 hi = f32x16{}, lo = f32x16{};
+#pragma unroll
+        for (int c = 0; c < KH; ++c)
+          hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              Ab[(tile * KT + c) * 64 + lane], bq[it][c], hi, 0, 0, 0);
+#pragma unroll
+        for (int c = 0; c < KL; ++c)
+          lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              Ab[(tile * KT + KH + c) * 64 + lane], bq[it][KH + c], lo, 0, 0, 0);
+        sacc[it] += tile_sum(hi, lo);
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+      if (more) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const int idx = threadIdx.x + q * 64 * kWaves;
+          if (idx < CH) As[buf ^ 1][idx] = stage[q];
+        }
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
 template <int D>
 int64_t mpad_rows(int64_t M) {
   constexpr int rows = 32 * kWaves * Mk<D>::IB;
@@ -461,7 +555,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   // MFMA chain dominates and the lower register count wins (bench_kde sweep)
   bool pipe = D <= 8;
   if (const char* env = getenv("ABC_KDE_MFMA_PIPE")) pipe = atoi(env) != 0;
-  if (pipe)
+  bool lds = false;
+  if (const char* env = getenv("ABC_KDE_MFMA_LDS")) lds = atoi(env) != 0;
+  if (lds)
+    hipLaunchKernelGGL((kde_mfma_lds_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                       p.split, p.spb, p.jseg, partial);
+  else if (pipe)
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
                        dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
                        p.split, p.spb, p.jseg, partial);

@@ -70,6 +70,38 @@ if __name__ == "__main__":
             print(f"ib {ib}:", end=" ")
             run(100000, 100000, 4, "mfma", reps=3)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "lds":
+        # LDS-shared A fragments vs the register version: bits and time
+        def rows(N, M, d):
+            g = torch.Generator(device="cuda").manual_seed(1)
+            X = torch.randn((N, d), dtype=torch.float64, device="cuda",
+                            generator=g)
+            w = torch.rand(N, dtype=torch.float64, device="cuda",
+                           generator=g) + 0.5
+            w /= w.sum()
+            from oracle import ref_cpu as ref
+            cov = ref.mvn_fit_cov(X.cpu().numpy(), w.cpu().numpy())
+            U, rank, lpd = K.psd_whitening(cov)
+            Us = torch.as_tensor(U * math.sqrt(0.5 * K.LOG2E), device="cuda")
+            mu = torch.zeros(d, dtype=torch.float64, device="cuda")
+            pp = K.PackedPopulation(X, w, mu, Us, rank, lpd, "mfma")
+            return pp.logpdf(X[:M] + 0.05)
+        for d in (20, 8, 4):
+            outs = {}
+            for lds in ("0", "1"):
+                for ib in (["2", "1"] if d == 20 else ["3", "1"] if d <= 8
+                           else ["2"]):
+                    os.environ["ABC_KDE_MFMA_LDS"] = lds
+                    os.environ["ABC_KDE_MFMA_IB"] = ib
+                    outs[(lds, ib)] = rows(20000, 5000, d).cpu().numpy()
+                    print(f"d {d} lds {lds} ib {ib}:", end=" ")
+                    run(262144 if d != 8 else 1000000,
+                        262144 if d != 8 else 1000000, d, "mfma", reps=2)
+            ref0 = outs[("0", "2" if d == 20 else "3")]
+            for k, v in outs.items():
+                print(f"  d {d} {k} bit-identical: {np.array_equal(v, ref0)}",
+                      flush=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "d20":
         # launch-shape sweep of the MFMA pass at d = 20 (config 5)
         for pipe in ["0", "1"]:

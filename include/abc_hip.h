@@ -124,25 +124,27 @@ int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
  * every operand split into bf16 pieces on a power-of-two grid so that the
  * large part of the sum is EXACT in the fp32 accumulator.
  * Afr: population fragments (abc_kde_mfma_prev_bytes), built with the
- * direct P by abc_kde_pack_prev_mfma (which also writes lw2max and the grid
- * g to gscale; ws >= 128 B).  Bfr: new-row fragments
- * (abc_kde_mfma_new_bytes, abc_kde_mfma_new_rows padded rows) and the direct
- * fp32 rows Ynew [M][D] (used by the exact underflow fixup), built by
- * abc_kde_pack_new_mfma from theta.  Workspace: abc_kde_workspace_bytes.
+ * fp64 whitened population P [npad][D+1] by abc_kde_pack_prev_mfma (which
+ * also writes lw2max and the grid g to gscale; ws >= 128 B).  Bfr: new-row
+ * fragments (abc_kde_mfma_new_bytes, abc_kde_mfma_new_rows padded rows) and
+ * the fp64 whitened rows Ynew [M][D], built by abc_kde_pack_new_mfma from
+ * theta.  Rows whose fp32-exponent sum underflows 2^-60 and rows beyond the
+ * grid range are re-evaluated exactly in fp64 from Ynew and P.
+ * Workspace: abc_kde_workspace_bytes.
  *                                          multivariatenormal.py:102-125 */
 size_t abc_kde_mfma_prev_bytes(int64_t npad, int d);
 int64_t abc_kde_mfma_new_rows(int64_t M, int d);
 size_t abc_kde_mfma_new_bytes(int64_t M, int d);
 int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
-                           const double* mu, const double* Us, float* P,
+                           const double* mu, const double* Us, double* P,
                            void* Afr, int64_t npad, double* lw2max,
                            double* gscale, void* ws, hipStream_t stream);
 int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
                           const double* mu, const double* Us,
-                          const double* gscale, float* Ynew, void* Bfr,
+                          const double* gscale, double* Ynew, void* Bfr,
                           hipStream_t stream);
-int abc_kde_logpdf_mfma(const void* Bfr, const float* Ynew, int64_t M,
-                        const void* Afr, const float* P, int64_t npad, int d,
+int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
+                        const void* Afr, const double* P, int64_t npad, int d,
                         const double* lw2max, double log_const,
                         double* out_logpd, void* ws, size_t ws_bytes,
                         hipStream_t stream);

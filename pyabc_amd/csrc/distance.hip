@@ -10,9 +10,11 @@
 // proposal, so lane b reads x[s, b] for s = 0..S-1 with fully coalesced rows;
 // the sum over keys is sequential in key order per lane (as the reference's
 // Python sum).  Powers p = 1, 2 use t, t*t and sqrt (the reference's glibc
-// pow differs from these by at most 1 ulp); the kernel flags every particle
-// whose distance lies within 4 ulp of eps (guard band), where that ulp could
-// flip the decision; parity tests assert the band is empty.
+// pow(s, .5) differs from sqrt by at most 1 ulp, for ~1e-3 of all s); the
+// kernel flags every particle whose distance lies within 4 ulp of eps (16 for
+// a general p) -- the guard band, where that ulp could flip the decision --
+// and the engine re-decides the flagged particles on the host with libm pow
+// (engine.redecide_guard_band), so accept masks equal the reference's.
 #include "common.hpp"
 #include "philox.hpp"
 
@@ -53,7 +55,10 @@ __global__ __launch_bounds__(256) void pnorm_kernel(
     d = pow(acc, 1.0 / p);
   d_out[b] = d;
   if (accept) accept[b] = d <= eps ? 1 : 0;
-  if (guard) guard[b] = fabs(d - eps) <= 4.0 * ulp_of(eps) ? 1 : 0;
+  // band: sqrt vs libm pow(s, .5) differ by <= 1 ulp; a general p adds
+  // device-pow vs libm-pow error in every term and in the root
+  if (guard)
+    guard[b] = fabs(d - eps) <= (PMODE == 0 ? 16.0 : 4.0) * ulp_of(eps) ? 1 : 0;
 }
 
 // y[s, b] = sum_k A[s, k] theta[b, k] + c[s] + sigma * z(b, s)

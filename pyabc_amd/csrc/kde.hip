@@ -573,22 +573,27 @@ static int pack_dispatch(const double* X, const double* w, int64_t n, int d,
   return kOk;
 }
 
-// shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum,
-// underflow detection and exact fixup of the fp32 paths
-int kde_finish_f32(const double* partial, int64_t M, int nseg,
-                   const float* Ynew, const float* P, int64_t npad, int d,
-                   const double* lw2max, double log_const, double* out_logpd,
-                   int* n_fix, int* fix_rows, hipStream_t stream) {
+// shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum
+// and underflow detection of the fp32-exponent pass, then the exact fixup in
+// fp64 on fp64 rows.  An fp32 copy of a far row (|y| ~ 30 in log2 units)
+// carries ~2e-6 absolute error per coordinate, i.e. up to 5e-5 relative on
+// the density through |y_i - y_j|^2: the fixup rows are exactly the far ones,
+// so they are evaluated from the fp64 whitened rows
+// (tests/test_gpu_fullsize.py, constructed rows beyond the population).
+int kde_finish_mfma(const double* partial, int64_t M, int nseg,
+                    const double* Ynew, const double* P, int64_t npad, int d,
+                    const double* lw2max, double log_const, double* out_logpd,
+                    int* n_fix, int* fix_rows, hipStream_t stream) {
   hipLaunchKernelGGL((kde_finalize_kernel<float>), dim3(ceil_div(M, 256)),
                      dim3(256), 0, stream, partial, M, nseg, lw2max,
                      log_const, out_logpd, n_fix, fix_rows);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
   switch (padded_dim(d)) {
-#define CASE(DD)                                                             \
-  case DD:                                                                   \
-    hipLaunchKernelGGL((kde_fixup_kernel<float, DD>), dim3(64), dim3(256), 0, \
-                       stream, Ynew, P, npad, lw2max, log_const, n_fix,      \
-                       fix_rows, out_logpd);                                 \
+#define CASE(DD)                                                              \
+  case DD:                                                                    \
+    hipLaunchKernelGGL((kde_fixup_kernel<double, DD>), dim3(64), dim3(256), 0, \
+                       stream, Ynew, P, npad, lw2max, log_const, n_fix,       \
+                       fix_rows, out_logpd);                                  \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
@@ -603,11 +608,11 @@ int kde_finish_f32(const double* partial, int64_t M, int nseg,
 
 int kde_padded_dim(int d) { return padded_dim(d); }
 int kde_num_segments(int64_t npad) { return kde_segments(npad); }
-int kde_pack_direct_f32(const double* X, const double* w, int64_t n, int d,
-                        const double* mu, const double* Us, float* P,
+int kde_pack_direct_f64(const double* X, const double* w, int64_t n, int d,
+                        const double* mu, const double* Us, double* P,
                         int64_t npad, double* lw2max, void* ws,
                         hipStream_t st) {
-  return pack_dispatch<float>(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
+  return pack_dispatch<double>(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
 }
 
 }  // namespace abc

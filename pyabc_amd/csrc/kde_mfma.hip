@@ -32,7 +32,8 @@
 // register order and the two lane halves combined in a fixed order, so a
 // row's bits are independent of M, of the launch shape and of the number of
 // ranks.  Rows whose sum underflows -- and new rows outside the grid range
-// (|y| > 256 g, flagged by b = -inf) -- go through kde.hip's exact fixup.
+// (|y| > 256 g, flagged by b = -inf) -- go through kde.hip's exact fixup,
+// in fp64 on the fp64 whitened rows (Ynew [M][D], P [npad][D+1]).
 #include <cmath>
 
 #include "common.hpp"
@@ -253,7 +254,7 @@ template <int D>
 __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     const double* __restrict__ theta, int64_t M, int64_t mpad, int d,
     const double* __restrict__ mu, const double* __restrict__ Us,
-    const double* __restrict__ gscale, float* __restrict__ Ydir,
+    const double* __restrict__ gscale, double* __restrict__ Ydir,
     bf16x8* __restrict__ B) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= mpad) return;
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     whiten_row<D>(theta, i, d, mu, Us, y);
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      Ydir[i * D + k] = static_cast<float>(y[k]);
+      Ydir[i * D + k] = y[k];
       ok = ok && fabs(y[k]) <= 256.0 * g;  // NaN -> not ok
     }
   }
@@ -572,8 +573,8 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 }
 
 template <int D>
-int logpdf_mfma_impl(const bf16x8* Bfr, const float* Ynew, int64_t M,
-                     const bf16x8* Afr, const float* P, int64_t npad, int d,
+int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
+                     const bf16x8* Afr, const double* P, int64_t npad, int d,
                      const double* lw2max, double log_const, double* out,
                      void* ws, size_t ws_bytes, hipStream_t st) {
   // i-tiles per wave: Mk<D>::IB (the row padding unit) or half of it
@@ -599,8 +600,8 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const float* Ynew, int64_t M,
   else
     launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, st);
   ABC_LAUNCH_CHECK("kde_mfma_kernel");
-  return kde_finish_f32(partial, M, p.nseg, Ynew, P, npad, d, lw2max,
-                        log_const, out, n_fix, fix_rows, st);
+  return kde_finish_mfma(partial, M, p.nseg, Ynew, P, npad, d, lw2max,
+                         log_const, out, n_fix, fix_rows, st);
 }
 
 }  // namespace
@@ -626,7 +627,7 @@ size_t abc_kde_mfma_new_bytes(int64_t M, int d) {
 }
 
 int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
-                           const double* mu, const double* Us, float* P,
+                           const double* mu, const double* Us, double* P,
                            void* Afr, int64_t npad, double* lw2max,
                            double* gscale, void* ws, hipStream_t st) {
   ABC_REQUIRE(Afr && gscale && ws, "pack_prev_mfma: null pointer");
@@ -635,7 +636,7 @@ int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
     set_error("pack_prev_mfma: unsupported dimension d=%d (max 32)", d);
     return kUnsupported;
   }
-  const int rc = kde_pack_direct_f32(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
+  const int rc = kde_pack_direct_f64(X, w, n, d, mu, Us, P, npad, lw2max, ws, st);
   if (rc != kOk) return rc;
   unsigned long long* ykey =
       reinterpret_cast<unsigned long long*>(static_cast<char*>(ws) + 64);
@@ -660,7 +661,7 @@ int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
 
 int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
                           const double* mu, const double* Us,
-                          const double* gscale, float* Ynew, void* Bfr,
+                          const double* gscale, double* Ynew, void* Bfr,
                           hipStream_t st) {
   ABC_REQUIRE(M >= 0, "pack_new_mfma: negative M");
   const int D = kde_padded_dim(d);
@@ -688,8 +689,8 @@ int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
   return kOk;
 }
 
-int abc_kde_logpdf_mfma(const void* Bfr, const float* Ynew, int64_t M,
-                        const void* Afr, const float* P, int64_t npad, int d,
+int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
+                        const void* Afr, const double* P, int64_t npad, int d,
                         const double* lw2max, double log_const,
                         double* out_logpd, void* ws, size_t ws_bytes,
                         hipStream_t st) {

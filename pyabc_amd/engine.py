@@ -157,16 +157,61 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     return torch.cat(out) if out else allr[:0]
 
 
+def pnorm_host(x, x0, fw, p):
+    """One particle's distance exactly as the reference evaluates it
+    (distance/distance.py:88-100): Python floats, libm ``pow`` for every
+    term and for the root, ``sum`` sequential from int 0 in key order."""
+    if p == math.inf:
+        return max(abs(f * (a - b)) for a, b, f in zip(x, x0, fw))
+    return math.pow(sum(math.pow(abs(f * (a - b)), p)
+                        for a, b, f in zip(x, x0, fw)), 1 / p)
+
+
+def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps):
+    """Host re-decision of the guard band (acceptor.py:241-242).
+
+    The kernel squares with ``t*t`` and roots with ``sqrt``; the reference
+    calls libm ``pow`` for both.  ``t*t == pow(t, 2.)`` bit for bit, but
+    ``pow(s, .5)`` differs from ``sqrt(s)`` by one ulp for about 1e-3 of all
+    s (general p: a few ulp), so a particle whose device distance lies within
+    the flagged band around eps could be decided differently.  Those
+    columns -- normally none -- are copied to the host, re-evaluated with
+    :func:`pnorm_host`, and their distance and accept bit overwritten, so
+    the accept mask equals the reference's.  Returns the band's size."""
+    if guard is None or B == 0:
+        return 0
+    gpos, gcount = K.compact(guard[:B])
+    n = int(gcount.item())
+    if n == 0:
+        return 0
+    sel = gpos[:n]
+    cols = stats.index_select(1, sel).cpu().numpy()
+    dh = np.array([pnorm_host(cols[:, i].tolist(), x0_host, fw_host, p)
+                   for i in range(n)], dtype=np.float64)
+    d.index_copy_(0, sel, torch.as_tensor(dh, device=d.device))
+    acc.index_copy_(0, sel, torch.as_tensor((dh <= eps).astype(np.uint8),
+                                            device=acc.device))
+    return n
+
+
 class PNormAcceptance:
     """Uniform acceptance d <= eps of a p-norm distance
-    (distance/distance.py:76-102, acceptor/acceptor.py:235-244)."""
+    (distance/distance.py:76-102, acceptor/acceptor.py:235-244), with the
+    guard band re-decided on the host (:func:`redecide_guard_band`)."""
 
     def __init__(self, x0, fw, p, eps):
         self.x0, self.fw, self.p, self.eps = x0, fw, p, eps
+        self._host = None
+        self.n_redecided = 0
 
     def __call__(self, stats, nv, seed, stream, eval_off):
         d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
                                          self.eps, B=nv)
+        if self._host is None:
+            self._host = (self.x0.cpu().tolist(), self.fw.cpu().tolist())
+        self.n_redecided += redecide_guard_band(
+            stats, nv, d, acc, guard, self._host[0], self._host[1], self.p,
+            self.eps)
         return d, acc, guard, None
 
 

@@ -177,8 +177,8 @@ def psd_whitening(cov):
 
 
 class WhitenedRows:
-    """New rows prepared for the MFMA KDE pass: direct fp32 rows (exact
-    underflow fixup) plus the bf16 piece fragments of the B operand."""
+    """New rows prepared for the MFMA KDE pass: direct fp64 whitened rows
+    (exact underflow fixup) plus the bf16 piece fragments of the B operand."""
 
     def __init__(self, Y, frags, M):
         self.Y, self.frags, self.M = Y, frags, M
@@ -202,7 +202,8 @@ class PackedPopulation:
         if precision not in ("mfma", "f32", "f64"):
             raise ValueError(f"unknown KDE precision {precision!r}")
         self.precision = precision
-        dt = F64 if precision == "f64" else F32
+        # the MFMA pass keeps an fp64 direct copy for its exact fixup rows
+        dt = F32 if precision == "f32" else F64
         self.P = torch.empty((self.npad, self.D + 1), dtype=dt, device=_dev())
         self.lw2max = torch.empty(1, dtype=F64, device=_dev())
         self.mu = mu
@@ -227,7 +228,7 @@ class PackedPopulation:
         theta = _contig(theta, F64)
         M = theta.shape[0]
         if self.precision == "mfma":
-            Y = torch.zeros((M, self.D), dtype=F32, device=_dev())
+            Y = torch.zeros((M, self.D), dtype=F64, device=_dev())
             nb = nat.lib().abc_kde_mfma_new_bytes(M, self.d)
             B = torch.empty(max(nb, 16), dtype=torch.uint8, device=_dev())
             call("abc_kde_pack_new_mfma", ptr(theta), M, self.d, ptr(self.mu),

@@ -253,6 +253,77 @@ def test_pnorm_distances_and_accept(K):
             assert host(guard).sum() == 0
 
 
+def _sqrt_pow_disagree(rng, n):
+    """(t1, t2) with s = t1*t1 + t2*t2 and sqrt(s) != pow(s, .5) (libm: about
+    1e-3 of generic s; a lone square t*t is almost never such an s), both
+    ways."""
+    up, down = [], []
+    for _ in range(2_000_000):
+        t1, t2 = (float(v) for v in rng.uniform(1, 100, 2))
+        s = t1 * t1 + t2 * t2
+        a, b = math.sqrt(s), math.pow(s, 0.5)
+        if a > b and len(up) < n:
+            up.append((t1, t2))
+        elif a < b and len(down) < n:
+            down.append((t1, t2))
+        if len(up) == n and len(down) == n:
+            return up, down
+    raise AssertionError("no sqrt/pow disagreement found")
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_guard_band_redecided_on_host(K, p):
+    """A distance within 1 ulp of eps where the kernel's sqrt (or device
+    pow) and the reference's libm pow disagree: the engine's host
+    re-decision (engine.redecide_guard_band) makes the accept bit the
+    reference's (distance.py:96-100, acceptor.py:241-242)."""
+    from pyabc_amd.engine import PNormAcceptance, pnorm_host
+    rng = np.random.default_rng(17)
+    x0 = np.array([0.0, 0.0, -1.0])
+    fw = np.array([1.0, 1.0, 1.0])
+    if p == 2:
+        up, down = _sqrt_pow_disagree(rng, 4)
+        ts = up + down
+    else:
+        ts = [tuple(r) for r in rng.uniform(1, 100, (8, 2)).tolist()]
+    cols = np.array([[t1, t2, -1.0] for t1, t2 in ts]).T     # [S, B]
+    ref_d = np.array([pnorm_host(cols[:, i].tolist(), x0.tolist(),
+                                 fw.tolist(), p) for i in range(len(ts))])
+    stats = dev(cols)
+    d_dev, _, _ = K.pnorm_distance(stats, dev(x0), dev(fw), p, math.inf)
+    d_dev = host(d_dev)
+    for i in range(len(ts)):
+        # eps exactly at the reference's distance, and one ulp either side
+        for eps in (ref_d[i], np.nextafter(ref_d[i], 0),
+                    np.nextafter(ref_d[i], np.inf)):
+            acc_obj = PNormAcceptance(dev(x0), dev(fw), p, float(eps))
+            d, acc, guard, _ = acc_obj(stats, len(ts), 0, 0, 0)
+            want = (ref_d <= eps).astype(np.uint8)
+            np.testing.assert_array_equal(host(acc), want)
+            assert host(d)[i] == ref_d[i]
+            assert acc_obj.n_redecided >= 1
+    if p == 2:
+        # the kernel alone disagrees on these rows (what the guard is for)
+        assert np.count_nonzero(d_dev != ref_d) == len(ts)
+
+
+def test_guard_band_large_batch(K):
+    """Many particles, eps at the reference median: accept mask equals the
+    libm-pow decision for every particle; the band stays tiny."""
+    from pyabc_amd.engine import PNormAcceptance, pnorm_host
+    g = load_golden("pnorm_B1500_S100")
+    stats = g["stats"].T
+    x0, fw = g["x0"].tolist(), g["fw"].tolist()
+    ref_d = np.array([pnorm_host(stats[:, i].tolist(), x0, fw, 2)
+                      for i in range(stats.shape[1])])
+    for eps in np.quantile(ref_d, [0.1, 0.5, 0.9], method="lower"):
+        a = PNormAcceptance(dev(g["x0"]), dev(g["fw"]), 2, float(eps))
+        d, acc, guard, _ = a(dev(stats), stats.shape[1], 0, 0, 0)
+        np.testing.assert_array_equal(host(acc), (ref_d <= eps).astype(
+            np.uint8))
+        assert 1 <= a.n_redecided <= 8
+
+
 # ---------------------------------------------- (a6) adaptive scales
 @pytest.mark.parametrize("name", golden_names("adaptive_"))
 def test_column_mad_and_std(K, name):

@@ -624,5 +624,69 @@ def gen_vis():
 GENS["vis"] = gen_vis
 
 
+C5_D, C5_S, C5_N, C5_T, C5_R = 20, 100, 10_000, 4, 5
+
+
+def _c5_problem():
+    """y = A theta + 0.5 eps, A = RandomState(42).randn(100,
+    20)/sqrt(20), theta_true = linspace(-1, 1, 20), x0 from RandomState(7)."""
+    A = np.random.RandomState(42).randn(C5_S, C5_D) / np.sqrt(C5_D)
+    th_true = np.linspace(-1, 1, C5_D)
+    x0v = A @ th_true + 0.5 * np.random.RandomState(7).randn(C5_S)
+    return A, th_true, x0v
+
+
+def _c5_seed(r):
+    A, th_true, x0v = _c5_problem()
+    keys = [f"y{k:03d}" for k in range(C5_S)]
+    names = pnames(C5_D)
+    x0 = dict(zip(keys, x0v))
+    np.random.seed(500 + r)
+
+    def model(par):
+        th = np.array([par[n] for n in names])
+        return dict(zip(keys, A @ th + 0.5 * np.random.randn(C5_S)))
+    from pyabc.sampler import SingleCoreSampler
+    prior = pyabc.Distribution(**{n: pyabc.RV("uniform", -5, 10)
+                                  for n in names})
+    abc = pyabc.ABCSMC(model, prior, PNormDistance(p=2),
+                       population_size=C5_N,
+                       eps=pyabc.QuantileEpsilon(alpha=0.5),
+                       sampler=SingleCoreSampler())
+    abc.new("sqlite://", x0)
+    abc.history.stores_sum_stats = False      # storage only; not the algorithm
+    t0 = time.time()
+    h = abc.run(max_nr_populations=C5_T)
+    st, eps, nsim = _run_stats(h, names)
+    print(f"    c5 seed {r}: {time.time() - t0:.0f} s eps {eps}", flush=True)
+    return r, st, eps, nsim
+
+
+def gen_e2e_c5():
+    """C5 at reduced N (SURVEY 8(c) 'a d=20 variant at N=1e4'): 20-param
+    linear Gaussian, S=100, PNormDistance(p=2), QuantileEpsilon(0.5),
+    SingleCoreSampler, R seeds in parallel processes."""
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(C5_R) as pool:
+        outs = pool.map(_c5_seed, range(C5_R))
+    A, th_true, x0v = _c5_problem()
+    res = {}
+    for r, st, eps, nsim in outs:
+        res[f"c5_mean_{r}"] = np.array([s[0] for s in st])
+        res[f"c5_std_{r}"] = np.array([s[1] for s in st])
+        res[f"c5_ess_{r}"] = np.array([s[2] for s in st])
+        res[f"c5_eps_{r}"] = eps
+        res[f"c5_nsim_{r}"] = nsim
+    save("e2e_c5", A=A, x0=x0v, theta_true=th_true, N=np.array(C5_N),
+         T=np.array(C5_T), R=np.array(C5_R), **res,
+         _ref=np.array("pyabc/smc.py:796-1022 (ABCSMC.run), "
+                       "SingleCoreSampler, PNormDistance(p=2), "
+                       "QuantileEpsilon(alpha=0.5); SURVEY 8(d) C5 at "
+                       "N=1e4"))
+
+
+GENS["e2e_c5"] = gen_e2e_c5
+
+
 if __name__ == "__main__":
     _main()

@@ -66,40 +66,77 @@ def kde_traffic():
     return t.get("hbm_bytes_per_launch"), t.get("source")
 
 
-def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
-                 pairs_per_launch):
-    """Roofline of the dominant kernel (kde_mfma_kernel, DESIGN.md §4).
+def kde_pmc(d):
+    """Per-tile instruction counts of kde_mfma_kernel from the committed
+    rocprofv3 PMC passes (tools/kde_pmc.py), if they were taken at this d."""
+    path = os.path.join(ROOT, "profiles", "r02_kde_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    return t if t.get("d") == d else None
 
-    achieved = SURVEY 8(d)'s algorithmic 3d+4 FLOP per pair over the average
-    launch, priced against the FP32 vector peak (the bound of a VALU-only
-    pass).  The MFMA reformulation moves the d-dimensional part onto the
-    matrix cores, so two further ceilings are reported: the bf16 MFMA work
-    actually issued (32 FLOP per pair per 32x32x16 chunk) against the dense
-    bf16 peak, and the VALU issue ceiling of what stays on the VALU per pair
-    (v_add + v_exp_f32 + v_add = 16 issue cycles per 64 pairs, plus 8 per
-    MFMA per 1024 pairs; guide issue costs at 2.4 GHz)."""
-    D = K.padded_dim(d)
-    kt = (D + 6 + 15) // 16 + (7 * D + 4 + 15) // 16
+
+def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
+                 pairs_per_launch, tiles_per_launch):
+    """Roofline of the dominant kernel (kde_mfma_kernel, DESIGN.md §4, §6).
+
+    The pass is bound by the SIMD's instruction issue: per 32x32 tile of
+    pairs a wave issues MFMAs (the d-dimensional exponent on the matrix
+    cores) and VALU (hi+lo add, v_exp_f32, row-sum add).  The ceiling is
+    the instruction mix COUNTED by PMC (profiles/r02_kde_pmc.json: per-tile
+    SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32, SQ_INSTS_MFMA) priced at the
+    guide's per-instruction SIMD cycles (plain VALU 2, transcendental 8,
+    MFMA issue 8 / matrix pipe 32) at the 2.4 GHz peak clock on 1024 SIMDs:
+
+        t_ceiling = tiles * max(2 V + 8 T + 8 F, 32 F) / (1024 * 2.4e9)
+
+    frac = t_ceiling / t_launch (<= 1).  achieved / peak are the same ratio
+    in SURVEY 8(d)'s algorithmic unit (3d+4 FLOP per pair).  The FP32
+    vector-peak figure of a VALU-only pass is reported beside it as
+    ``valu_equiv`` (it exceeds 1: the MFMA does the d-dimensional part)."""
+    pmc = kde_pmc(d)
     pairs_per_s = pairs_per_launch / avg_launch_s
-    issue_peak = 1024 * 64 * CLOCK_HZ / (16 + kt / 2)
-    mfma_tf = 32 * kt * pairs_per_s / 1e12
+    fpp = 3 * d + 4
+    if pmc is not None:
+        pt = pmc["per_tile"]
+        V, T, F = (pt["SQ_INSTS_VALU"], pt.get("SQ_INSTS_VALU_TRANS_F32", 0.0),
+                   pt["SQ_INSTS_MFMA"])
+        src = "profiles/r02_kde_pmc.json (rocprofv3 --pmc, per-tile counts)"
+    else:   # static count of the kernel's per-tile code (DESIGN.md §4)
+        D = K.padded_dim(d)
+        F = (D + 6 + 15) // 16 + (7 * D + 4 + 15) // 16
+        V, T = 48.0, 16.0
+        src = "static per-tile instruction count (no PMC file for this d)"
+    cyc = max(2 * (V - T) + 8 * T + 8 * F, 32 * F)
+    t_ceil = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
+    frac = t_ceil / avg_launch_s
+    peak_tf = achieved_tf / frac
+    mfma_tf = 32768 * F * tiles_per_launch / avg_launch_s / 1e12
     return {
         "bound": "valu",
         "kernel": "kde_mfma_kernel (exact-grid bf16 pieces: "
                   "v_mfma_f32_32x32x16_bf16 for the d-dim exponent, "
                   "v_add + v_exp_f32 + v_add per pair on the VALU)",
         "achieved": achieved_tf,
-        "peak": FP32_PEAK_TFLOPS,
+        "peak": peak_tf,
         "unit": "TFLOP/s",
-        "frac": achieved_tf / FP32_PEAK_TFLOPS,
+        "frac": frac,
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "flops_per_pair": 3 * d + 4,
+        "peak_basis": "SIMD issue ceiling of the PMC-counted instruction mix "
+                      "(VALU 2, TRANS 8, MFMA 8 issue / 32 pipe cycles per "
+                      "wave64 instruction, 1024 SIMDs at 2.4 GHz), expressed "
+                      f"in algorithmic {fpp} FLOP/pair; {src}",
+        "ceiling_cycles_per_tile": cyc,
+        "measured_cycles_per_tile": avg_launch_s * 1024 * CLOCK_HZ
+        / tiles_per_launch,
+        "flops_per_pair": fpp,
         "avg_launch_ms": avg_launch_s * 1e3,
         "pairs_per_launch": pairs_per_launch,
-        "valu_issue": {"pairs_per_s": pairs_per_s,
-                       "peak_pairs_per_s": issue_peak,
-                       "frac": pairs_per_s / issue_peak},
+        "pairs_per_s": pairs_per_s,
+        "valu_equiv": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
+                       "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS},
         "mfma_bf16": {"achieved": mfma_tf, "peak": BF16_MFMA_PEAK_TFLOPS,
                       "unit": "TFLOP/s",
                       "frac": mfma_tf / BF16_MFMA_PEAK_TFLOPS},
@@ -176,6 +213,9 @@ def main():
     elapsed = comm.all_reduce_max_float(elapsed)
     kde_ms = [e0.elapsed_time(e1) for (e0, e1, _, _) in eng.kde_events]
     kde_pairs = [M * Np for (_, _, M, Np) in eng.kde_events]
+    rp = K.row_pad()
+    kde_tiles = [(K.nat.lib().abc_kde_mfma_new_rows(M, d) // 32)
+                 * (-(-Np // rp) * rp // 32) for (_, _, M, Np) in eng.kde_events]
     kde_t = sum(kde_ms) / 1e3
     pairs_local = sum(kde_pairs)
     kde_t_max = comm.all_reduce_max_float(kde_t)
@@ -187,6 +227,7 @@ def main():
     # per-launch roofline of the dominant kernel on this rank
     avg_launch_s = kde_t / max(len(kde_ms), 1)
     pairs_per_launch = pairs_local / max(len(kde_ms), 1)
+    tiles_per_launch = sum(kde_tiles) / max(len(kde_ms), 1)
     achieved_tf = flops_per_pair * pairs_per_launch / avg_launch_s / 1e12
     log(f"[rank {comm.rank}] steps={args.steps} elapsed={elapsed:.3f}s "
         f"ms/step={ms_step:.1f} kde avg launch {avg_launch_s*1e3:.1f} ms "
@@ -220,7 +261,8 @@ def main():
                            f"population all-gathered per generation)"},
         "kde_pairs_per_s": pairs_total / kde_t_max,
         "roofline": kde_roofline(d, achieved_tf, traffic, traffic_src,
-                                 avg_launch_s, pairs_per_launch),
+                                 avg_launch_s, pairs_per_launch,
+                                 tiles_per_launch),
     }
     if R == 1 and not args.no_cpu_baseline:
         v, cores, acc, ev, wall = cpu_baseline(state["fit"], model, x0,

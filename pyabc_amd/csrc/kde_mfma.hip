@@ -313,7 +313,7 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB, bool PIPE>
+template <int KH, int KL, int IB, bool PIPE, bool SCHED = false>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -372,6 +372,20 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
           sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+          if constexpr (SCHED) {
+            // interleave: each MFMA of step q+1 followed by a share of step
+            // q's 48 VALU (16 add, 16 exp, 16 tree/row adds)
+            constexpr int VPG = (48 + KT - 1) / KT;
+            if (q + 1 < 2 * IB) {
+#pragma unroll
+              for (int m = 0; m < KT; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
+              }
+            } else {
+              __builtin_amdgcn_sched_group_barrier(0x002, 48, 0);
+            }
+          }
         }
       } else {
 #pragma unroll
@@ -389,6 +403,92 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
+// The same pass software-pipelined ACROSS 64-row chunks: the MFMAs of step
+// q+1 -- for the last step of a chunk, step 0 of the next chunk -- are
+// issued interleaved with the VALU of step q (sched_group_barrier: one MFMA,
+// then a share of the 48 VALU instructions), so no step's exp/add block
+// runs without matrix work beside it.  A row's arithmetic and summation
+// order are those of kde_mfma_kernel: the rows are bit-identical.
+template <int KH, int KL, int IB>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int NS = 2 * IB;                  // steps per 64-row chunk
+  constexpr int VPG = (48 + KT - 1) / KT;     // VALU per MFMA gap
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64 + lane;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    if (nj > 0) {
+      bf16x8 a[2][KT];
+      f32x16 hi[2], lo[2];
+#pragma unroll
+      for (int c = 0; c < KT; ++c) a[0][c] = Aseg[c * 64];
+#pragma unroll
+      for (int c = 0; c < KT; ++c) a[1][c] = Aseg[(KT + c) * 64];
+      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+      for (int jc = 0; jc < nj; jc += 64) {
+        const bool more = jc + 64 < nj;
+        // next chunk's tiles (a re-read of this chunk's on the last one)
+        const bf16x8* __restrict__ an =
+            Aseg + ((more ? jc + 64 : jc) >> 5) * KT * 64;
+        float sacc[IB];
+#pragma unroll
+        for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+          if (q + 1 < NS)
+            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+                              hi[(q + 1) & 1], lo[(q + 1) & 1]);
+          else if (more)  // step 0 of the next chunk (tile 0 loaded below)
+            mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+          if (q + 1 == IB) {  // last MFMA reading tile 0 issued
+#pragma unroll
+            for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
+          }
+          if (q + 2 == NS) {  // last MFMA reading tile 1 issued
+#pragma unroll
+            for (int c = 0; c < KT; ++c) a[1][c] = an[(KT + c) * 64];
+          }
+          sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+          if (q + 1 < NS || more) {
+#pragma unroll
+            for (int m = 0; m < KT; ++m) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
@@ -558,7 +658,22 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if (const char* env = getenv("ABC_KDE_MFMA_PIPE")) pipe = atoi(env) != 0;
   bool lds = false;
   if (const char* env = getenv("ABC_KDE_MFMA_LDS")) lds = atoi(env) != 0;
-  if (lds)
+  // sched_group_barrier interleave of step q+1's MFMAs with step q's VALU:
+  // 156.4 -> 151.2 ms at N = M = 1e6, d = 8; slower at d = 4 (1.37 -> 1.44
+  // ms) and d = 20 (21 -> 52 ms), so on at D = 8 only (tools/bench_kde.py sw)
+  bool sched = D == 8;
+  if (const char* env = getenv("ABC_KDE_MFMA_SCHED")) sched = atoi(env) != 0;
+  bool sw = false;
+  if (const char* env = getenv("ABC_KDE_MFMA_SW")) sw = atoi(env) != 0;
+  if (sw)
+    hipLaunchKernelGGL((kde_mfma_sw_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                       p.split, p.spb, p.jseg, partial);
+  else if (sched)
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, true>),
+                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                       p.split, p.spb, p.jseg, partial);
+  else if (lds)
     hipLaunchKernelGGL((kde_mfma_lds_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
                        dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
                        p.split, p.spb, p.jseg, partial);

@@ -330,3 +330,81 @@ def test_resume_run_from_file(pa, tmp_path, gt_model):
     hist_contd = abc_continued.run(minimum_epsilon=0, max_nr_populations=1)
     assert hist_contd.n_populations == 2
     assert hist_new.n_populations == 2
+
+
+def _c5_run(pa, g, N, T, seed):
+    A, x0v = g["A"], g["x0"]
+    S, d = A.shape
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k:02d}" for k in range(d)]
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    sampler = pa.GPUBatchSampler(seed=seed)
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2), population_size=N,
+                    eps=pa.QuantileEpsilon(alpha=0.5), sampler=sampler)
+    abc.new(f"mem://c5_{seed}", dict(zip(keys, x0v)))
+    h = abc.run(max_nr_populations=T)
+    assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
+    pops = h.get_all_populations()
+    nsim = pops[pops.t >= 0].samples.values
+    return h, _eps(h), _post_stats(h, names), nsim
+
+
+def test_config5_d20_vs_reference_runs(pa):
+    """C5 at the reference-feasible size (d = 20 variant at
+    N = 1e4): 20-param linear Gaussian, S = 100, PNormDistance(p=2),
+    QuantileEpsilon(0.5), 4 generations.  Five GPU seeds against five
+    reference SingleCoreSampler seeds (tests/golden/e2e_c5.npz): per
+    generation, the epsilon, every parameter's posterior mean and sd and the
+    evaluation count agree within Monte Carlo error (two-sample, 5 sigma of
+    the seed-to-seed spread; floors 1 % of eps, 0.02 in theta, 2 % of the
+    sd and of the evaluation count).  Pins the method of
+    test_nondeterministic/test_abc_smc_algorithm.py:354-394 (posterior
+    moments over multiple populations) on this problem."""
+    g = load_golden("e2e_c5")
+    R, T, N = int(g["R"]), int(g["T"]), int(g["N"])
+    ref_eps = np.array([g[f"c5_eps_{r}"] for r in range(R)])
+    ref_m = np.array([g[f"c5_mean_{r}"] for r in range(R)])     # [R, T, d]
+    ref_s = np.array([g[f"c5_std_{r}"] for r in range(R)])
+    ref_n = np.array([g[f"c5_nsim_{r}"] for r in range(R)], dtype=float)
+    runs = [_c5_run(pa, g, N, T, 1000 + r) for r in range(R)]
+    eps = np.array([r[1][:T] for r in runs])
+    m = np.array([[st[t][0] for t in range(T)] for _, _, st, _ in runs])
+    s = np.array([[st[t][1] for t in range(T)] for _, _, st, _ in runs])
+    ns = np.array([r[3][:T] for r in runs], dtype=float)
+
+    def close(a, b, floor):
+        se = np.sqrt(a.var(0, ddof=1) / len(a) + b.var(0, ddof=1) / len(b))
+        diff = np.abs(a.mean(0) - b.mean(0))
+        assert np.all(diff <= 5 * se + floor), (diff, se)
+    close(eps, ref_eps, 0.01 * ref_eps.mean(0))
+    close(m, ref_m, 0.02)
+    close(s, ref_s, 0.02 * ref_s.mean(0))
+    close(ns, ref_n, 0.02 * ref_n.mean(0))
+
+
+def test_config5_full_size_10_generations(pa):
+    """C5 as BASELINE names it, on one GPU: N = 1e6, d = 20, S = 100,
+    QuantileEpsilon(0.5), 10 generations through ABCSMC + GPUBatchSampler.
+    The first generations' epsilons agree with the reference runs at N = 1e4
+    (the quantile of the same distance distribution, to 3 %); epsilon
+    decreases every generation; weights are normalised; the posterior
+    contracts toward theta_true."""
+    g = load_golden("e2e_c5")
+    T = int(g["T"])
+    ref_eps = np.array([g[f"c5_eps_{r}"] for r in range(int(g["R"]))])
+    h, eps, st, nsim = _c5_run(pa, g, 1_000_000, 10, 77)
+    assert h.max_t == 9
+    np.testing.assert_allclose(eps[:T], ref_eps.mean(0), rtol=0.03)
+    assert np.all(np.diff(eps) < 0)
+    for t in range(10):
+        df, w = h.distribution_numpy(0, t)
+        assert df.shape == (1_000_000, 20)
+        assert abs(w.sum() - 1) < 1e-9
+    th = g["theta_true"]
+    err0 = np.abs(st[0][0] - th).mean()
+    err9 = np.abs(st[9][0] - th).mean()
+    print(f"C5 full size: eps {eps} |mean - theta_true| {err0:.3f} -> "
+          f"{err9:.3f}, sd {st[0][1].mean():.3f} -> {st[9][1].mean():.3f}")
+    assert err9 < err0, (err0, err9)
+    assert np.all(st[9][1] < st[0][1])

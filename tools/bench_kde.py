@@ -102,6 +102,43 @@ if __name__ == "__main__":
                 print(f"  d {d} {k} bit-identical: {np.array_equal(v, ref0)}",
                       flush=True)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "sw":
+        # software-pipelined / sched_group_barrier variants: bits and time
+        def rows(N, M, d):
+            g = torch.Generator(device="cuda").manual_seed(1)
+            X = torch.randn((N, d), dtype=torch.float64, device="cuda",
+                            generator=g)
+            w = torch.rand(N, dtype=torch.float64, device="cuda",
+                           generator=g) + 0.5
+            w /= w.sum()
+            from oracle import ref_cpu as ref
+            cov = ref.mvn_fit_cov(X.cpu().numpy(), w.cpu().numpy())
+            U, rank, lpd = K.psd_whitening(cov)
+            Us = torch.as_tensor(U * math.sqrt(0.5 * K.LOG2E), device="cuda")
+            mu = torch.zeros(d, dtype=torch.float64, device="cuda")
+            pp = K.PackedPopulation(X, w, mu, Us, rank, lpd, "mfma")
+            return pp.logpdf(X[:M] + 0.05)
+        variants = [("base", {}), ("sched", {"ABC_KDE_MFMA_SCHED": "1"}),
+                    ("sw", {"ABC_KDE_MFMA_SW": "1"}),
+                    ("sw-ibh", {"ABC_KDE_MFMA_SW": "1", "ABC_KDE_MFMA_IB": "h"})]
+        dims = [int(x) for x in sys.argv[2:]] or [8, 20, 4]
+        for d in dims:
+            ib = {8: "1", 20: "1", 4: "1"}.get(d, "1")
+            outs = {}
+            for name, env in variants:
+                for k in ("ABC_KDE_MFMA_SCHED", "ABC_KDE_MFMA_SW",
+                          "ABC_KDE_MFMA_IB"):
+                    os.environ.pop(k, None)
+                for k, v in env.items():
+                    os.environ[k] = ib if v == "h" else v
+                outs[name] = rows(20000, 5000, d).cpu().numpy()
+                print(f"d {d} {name}:", end=" ")
+                N = {8: 1000000, 20: 262144, 4: 100000}.get(d, 262144)
+                run(N, N, d, "mfma", reps=3)
+            for k, v in outs.items():
+                print(f"  d {d} {k} bit-identical: "
+                      f"{np.array_equal(v, outs['base'])}", flush=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "d20":
         # launch-shape sweep of the MFMA pass at d = 20 (config 5)
         for pipe in ["0", "1"]:

@@ -232,6 +232,17 @@ int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
                                  uint64_t seed, uint64_t sid, uint64_t offset,
                                  int64_t B, double* theta, int64_t* idx,
                                  uint8_t* in_support, hipStream_t stream);
+/* Parity form of the same draw with the caller's uniforms u[B] and normals
+ * z[B*d] and the reference's own factor: A[N][d][d] = sqrt(s)[:,None] * V
+ * from numpy svd(C_n) (legacy multivariate_normal), theta = X[idx] +
+ * z @ A[idx], idx = searchsorted(cdf, u, 'right').
+ *                                                   local_transition.py:141-145 */
+int abc_resample_perturb_local_f64(const double* X, int64_t N, int d,
+                                   const double* cdf, const double* u,
+                                   const double* z, const double* A,
+                                   const double* lo, const double* scale,
+                                   int64_t B, double* theta, int64_t* idx,
+                                   uint8_t* in_support, hipStream_t stream);
 
 /* ---------------- synthetic batch simulators (benchmark models) ----------
  * linear-Gaussian y = A theta + c + sigma eps (SURVEY configs C2/C5) and the

@@ -353,6 +353,19 @@ def local_covs(X, w, nbr, scaling=1.0, eps=1e-3):
     return covs, invs, dets
 
 
+def local_rvs(X, w, covs, u, z):
+    """``LocalTransition.rvs_single`` per draw (local_transition.py:141-145):
+    ``choice(N, p=w)`` = searchsorted(cumsum(w)/sum, u, 'right'), then legacy
+    ``multivariate_normal(X[idx], C[idx])`` = X[idx] + z @ (sqrt(s)[:, None]
+    * V) with (U, s, V) = svd(C[idx])."""
+    idx = resample_indices(resample_cdf(w), np.asarray(u))
+    theta = np.empty((len(idx), X.shape[1]))
+    for b, i in enumerate(idx):
+        _, s, v = np.linalg.svd(covs[i])
+        theta[b] = np.asarray(z[b]) @ (np.sqrt(s)[:, None] * v) + X[i]
+    return idx, theta
+
+
 def local_pdf(pts, X, w, invs, dets):
     """LocalTransition._pdf_single (local_transition.py:103-110):
     sum_n w_n exp(-1/2 q_n) / sqrt((2 pi)^d det_n) / sum w."""

@@ -129,6 +129,10 @@ _SIGS = {
                                              c_ptr, c_ptr, c_ptr, c_u64,
                                              c_u64, c_u64, c_i64, c_ptr,
                                              c_ptr, c_ptr, c_ptr]),
+    "abc_resample_perturb_local_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr,
+                                               c_ptr, c_ptr, c_ptr, c_ptr,
+                                               c_ptr, c_i64, c_ptr, c_ptr,
+                                               c_ptr, c_ptr]),
     # (f3) exact inference: stochastic kernels / acceptor / temperatures
     "abc_stochastic_kernel_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_int,
                                           c_int, c_dbl, c_i64, c_ptr, c_dbl,

@@ -493,22 +493,32 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
 }
 
 // fp32 pass (precision="f32", 1e-5 relative): the same sum with the
-// population centred on X[0] in fp64 then rounded to fp32, the packed
-// coefficients pre-scaled by log2(e)/2 and lc by log2(e), so a term is one
-// v_exp_f32 of (lc2_n - q'_n); 16 terms are added in fp32, then into fp64.
+// population centred on X[0] in fp64, the packed coefficients pre-scaled by
+// log2(e)/2 and lc by log2(e), so a term is one v_exp_f32 of (lc2_n - q'_n);
+// 16 terms are added in fp32, then into fp64.  Centred coordinates are kept
+// as an fp32 (hi, lo) pair, x - X[0] = hi + lo, and the pair difference is
+// (th_hi - X_hi) + (th_lo - X_lo): its error is ~2^-24 of the difference
+// itself, not of the distance R to X[0], so the density's accuracy does not
+// degrade with the population's extent over the local bandwidth (a single
+// fp32 rounding of x - X[0] costs ~ sqrt(q) (R / sigma) 2^-23 relative).
 template <int D>
 __global__ __launch_bounds__(256) void local_pack32_kernel(
     const double* __restrict__ X, const double* __restrict__ coef,
     const double* __restrict__ lc, const unsigned long long* __restrict__ lc_max_key,
-    int64_t N, float* __restrict__ X32, float* __restrict__ coef32,
-    float* __restrict__ lc32) {
+    int64_t N, float* __restrict__ X32, float* __restrict__ X32lo,
+    float* __restrict__ coef32, float* __restrict__ lc32) {
   constexpr int NC = D * (D + 1) / 2;
   const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (n >= N) return;
   const double L = key_f64(*lc_max_key);
   constexpr double kLog2e = 1.4426950408889634;
 #pragma unroll
-  for (int q = 0; q < D; ++q) X32[n * D + q] = static_cast<float>(X[n * D + q] - X[q]);
+  for (int q = 0; q < D; ++q) {
+    const double c = X[n * D + q] - X[q];
+    const float h = static_cast<float>(c);
+    X32[n * D + q] = h;
+    X32lo[n * D + q] = static_cast<float>(c - static_cast<double>(h));
+  }
 #pragma unroll
   for (int t = 0; t < NC; ++t)
     coef32[n * NC + t] = static_cast<float>(coef[n * NC + t] * (0.5 * kLog2e));
@@ -519,25 +529,35 @@ template <int D>
 __global__ __launch_bounds__(256) void local_pts32_kernel(const double* __restrict__ pts,
                                                           int64_t M,
                                                           const double* __restrict__ X,
-                                                          float* __restrict__ pts32) {
+                                                          float* __restrict__ pts32,
+                                                          float* __restrict__ pts32lo) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= M) return;
 #pragma unroll
-  for (int q = 0; q < D; ++q) pts32[i * D + q] = static_cast<float>(pts[i * D + q] - X[q]);
+  for (int q = 0; q < D; ++q) {
+    const double c = pts[i * D + q] - X[q];
+    const float h = static_cast<float>(c);
+    pts32[i * D + q] = h;
+    pts32lo[i * D + q] = static_cast<float>(c - static_cast<double>(h));
+  }
 }
 
 template <int D>
 __global__ __launch_bounds__(256) void local_pdf32_kernel(
-    const float* __restrict__ pts, int64_t M, const float* __restrict__ X,
+    const float* __restrict__ pts, const float* __restrict__ ptslo, int64_t M,
+    const float* __restrict__ X, const float* __restrict__ Xlo,
     const float* __restrict__ coef, const float* __restrict__ lc, int64_t N,
     int split, int64_t nchunk, double* __restrict__ part) {
   constexpr int NC = D * (D + 1) / 2;
   const int s = blockIdx.x % split;
   const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
   const int64_t i = i0 < M ? i0 : M - 1;
-  float th[D];
+  float th[D], tl[D];
 #pragma unroll
-  for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
+  for (int q = 0; q < D; ++q) {
+    th[q] = pts[i * D + q];
+    tl[q] = ptslo[i * D + q];
+  }
   double acc = 0.0;
   const int64_t n0 = static_cast<int64_t>(s) * nchunk;
   int64_t n1 = n0 + nchunk;
@@ -548,7 +568,8 @@ __global__ __launch_bounds__(256) void local_pdf32_kernel(
     for (int64_t n = b; n < be; ++n) {
       float dl[D];
 #pragma unroll
-      for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
+      for (int q = 0; q < D; ++q)
+        dl[q] = (th[q] - X[n * D + q]) + (tl[q] - Xlo[n * D + q]);
       const float* c = coef + n * NC;
       float qf = 0.0f;
       int t = 0;
@@ -868,9 +889,10 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
 }
 
 size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N) {
-  // the fp64 layout, then X32[N][8] | coef32[N][36] | lc32[N] | pts32[M][8]
+  // the fp64 layout, then X32[N][8] | X32lo[N][8] | coef32[N][36] | lc32[N]
+  // | pts32[M][8] | pts32lo[M][8]
   return abc_local_logpdf_workspace_bytes(M, N) +
-         static_cast<size_t>(N) * 4 * 45 + static_cast<size_t>(M) * 4 * 8 + 512;
+         static_cast<size_t>(N) * 4 * 53 + static_cast<size_t>(M) * 4 * 16 + 512;
 }
 
 int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
@@ -898,9 +920,11 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   int* fix_rows = reinterpret_cast<int*>(part + static_cast<int64_t>(split) * M);
   float* X32 = reinterpret_cast<float*>(
       base + ((abc_local_logpdf_workspace_bytes(M, N) + 255) / 256) * 256);
-  float* coef32 = X32 + N * 8;
+  float* X32lo = X32 + N * 8;
+  float* coef32 = X32lo + N * 8;
   float* lc32 = coef32 + N * 36;
   float* pts32 = lc32 + N;
+  float* pts32lo = pts32 + M * 8;
   ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
   hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
   hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
@@ -911,11 +935,13 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   const double thresh = 8.673617379884035e-19;
 #define L(DD)                                                                    \
   hipLaunchKernelGGL((local_pack32_kernel<DD>), dim3(ceil_div(N, 256)), dim3(256), \
-                     0, st, X, coef, lc, lc_max_key, N, X32, coef32, lc32);      \
+                     0, st, X, coef, lc, lc_max_key, N, X32, X32lo, coef32,    \
+                     lc32);                                                      \
   hipLaunchKernelGGL((local_pts32_kernel<DD>), dim3(ceil_div(M, 256)), dim3(256),  \
-                     0, st, pts, M, X, pts32);                                   \
+                     0, st, pts, M, X, pts32, pts32lo);                          \
   hipLaunchKernelGGL((local_pdf32_kernel<DD>), dim3(grid), dim3(256), 0, st,       \
-                     pts32, M, X32, coef32, lc32, N, split, nchunk, part);       \
+                     pts32, pts32lo, M, X32, X32lo, coef32, lc32, N, split,      \
+                     nchunk, part);                                              \
   hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),  \
                      0, st, part, M, split, lc_max_key, logsumw, out_logpdf,     \
                      n_fix, fix_rows, thresh);                                   \

@@ -447,9 +447,11 @@ __device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
                                    const double* __restrict__ lo,
                                    const double* __restrict__ scale,
                                    double* __restrict__ theta_row,
-                                   int64_t* idx_out, uint8_t* sup_out) {
+                                   int64_t* idx_out, uint8_t* sup_out,
+                                   int64_t a_stride = 0) {
   int64_t idx = search_right(cdf, N, u);
   const int64_t idx_c = idx < N ? idx : N - 1;  // numpy would raise; u<1 always
+  A += idx_c * a_stride;  // per-particle factor (LocalTransition) or shared
   bool ok = true;
 #pragma unroll
   for (int l = 0; l < D; ++l) {
@@ -470,6 +472,8 @@ __device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
   *sup_out = ok ? 1 : 0;
 }
 
+// a_stride = 0: one factor A for every draw (MultivariateNormalTransition);
+// a_stride = d*d: A[idx] per resampled particle (LocalTransition)
 template <int D>
 __global__ __launch_bounds__(256) void resample_perturb_kernel(
     const double* __restrict__ X, int64_t N, int d,
@@ -477,14 +481,14 @@ __global__ __launch_bounds__(256) void resample_perturb_kernel(
     const double* __restrict__ z, const double* __restrict__ A,
     const double* __restrict__ lo, const double* __restrict__ scale,
     int64_t B, double* __restrict__ theta, int64_t* __restrict__ idx,
-    uint8_t* __restrict__ sup) {
+    uint8_t* __restrict__ sup, int64_t a_stride) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double zz[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) zz[k] = k < d ? z[b * d + k] : 0.0;
   perturb_one<D>(X, N, d, cdf, u[b], zz, A, lo, scale, theta + b * d, idx + b,
-                 sup + b);
+                 sup + b, a_stride);
 }
 
 // Production proposals: u from stream (2*sid), z from stream (2*sid+1).
@@ -711,7 +715,32 @@ int abc_resample_perturb_f64(const double* X, int64_t N, int d,
 #define L(DD)                                                                \
   hipLaunchKernelGGL((resample_perturb_kernel<DD>), dim3(g), dim3(256), 0, st, \
                      X, N, d, cdf, u, z, A, lo, scale, B, theta, idx,         \
-                     in_support);
+                     in_support, int64_t{0});
+  DISPATCH_D(d, L)
+#undef L
+  ABC_LAUNCH_CHECK("resample_perturb_kernel");
+  return kOk;
+}
+
+int abc_resample_perturb_local_f64(const double* X, int64_t N, int d,
+                                   const double* cdf, const double* u,
+                                   const double* z, const double* A,
+                                   const double* lo, const double* scale,
+                                   int64_t B, double* theta, int64_t* idx,
+                                   uint8_t* in_support, hipStream_t st) {
+  ABC_REQUIRE(check_dim(d), "resample_perturb_local: unsupported d=%d", d);
+  ABC_REQUIRE(N > 0 && B >= 0, "resample_perturb_local: bad sizes");
+  if (B == 0) return kOk;
+  ABC_REQUIRE(X && cdf && u && z && A && theta && idx && in_support,
+              "resample_perturb_local: null pointer");
+  ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
+              "resample_perturb_local: lo and scale must both be given or NULL");
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+  const int64_t stride = static_cast<int64_t>(d) * d;
+#define L(DD)                                                                \
+  hipLaunchKernelGGL((resample_perturb_kernel<DD>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, u, z, A, lo, scale, B, theta, idx,         \
+                     in_support, stride);
   DISPATCH_D(d, L)
 #undef L
   ABC_LAUNCH_CHECK("resample_perturb_kernel");

@@ -45,6 +45,22 @@ class Comm:
             dist.init_process_group(backend=backend)
         return Comm(dist.get_rank(), dist.get_world_size(), None)
 
+    @staticmethod
+    def current():
+        """The already-initialised process group (or a single rank)."""
+        if dist.is_available() and dist.is_initialized() and \
+                dist.get_world_size() > 1:
+            return Comm(dist.get_rank(), dist.get_world_size(), None)
+        return Comm.single()
+
+    def broadcast_int(self, v, src=0):
+        """Rank ``src``'s int on every rank."""
+        if not self.active:
+            return int(v)
+        x = torch.tensor([int(v)], dtype=torch.int64, device=self._int_dev())
+        dist.broadcast(x, src)
+        return int(x.item())
+
     @property
     def _host_staged(self):
         # gloo's all_gather takes host tensors only
@@ -131,3 +147,23 @@ class Comm:
         x = torch.tensor([float(v)], dtype=torch.float64, device=dev)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         return float(x.item())
+
+
+def env_rank():
+    """This process's rank from the torchrun environment (before or without
+    an initialised process group)."""
+    return int(os.environ.get("RANK", "0"))
+
+
+def env_world():
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def agree_int(v):
+    """Rank 0's value of a host decision on every rank (seeds, adapted
+    population sizes: anything the ranks' collectives depend on).  A single
+    process returns ``v``; under torchrun the process group is initialised
+    on first use."""
+    if env_world() == 1:
+        return int(v)
+    return Comm.from_env().broadcast_int(v)

@@ -311,7 +311,7 @@ class GenerationEngine:
 
     def sample_generation(self, t, n, fit, x0, fw, eps, keep_stats=None,
                           record=None, stream_base=0, acceptance=None,
-                          record_particles=False):
+                          record_particles=False, max_eval=math.inf):
         """Proposals until n are accepted (over all ranks), then KDE weights.
 
         Global-id semantics (SingleCoreSampler, singlecore.py:19-38): raw
@@ -333,7 +333,10 @@ class GenerationEngine:
         returns acceptance weights that enter the importance weights.
         ``record_particles`` keeps parameters, distances and accept flags of
         the recorded evaluations (the temperature schemes' records,
-        smc.py:990-1017)."""
+        smc.py:990-1017).  ``max_eval`` (SingleCoreSampler's
+        check_max_eval, singlecore.py:24-35): no round starts once that
+        many evaluations are done; if fewer than n were accepted by then the
+        result has ``ok = False`` and no population."""
         keep_stats = self.record_stats if keep_stats is None else keep_stats
         record = self.record_stats if record is None else record
         if acceptance is None and x0 is not None:
@@ -347,6 +350,11 @@ class GenerationEngine:
         raw_off = 0
         eval_off = 0
         while n_acc < n:
+            if eval_off >= max_eval:
+                tm["propose_sim_dist"] = time.perf_counter() - t0
+                self.timers = tm
+                return GenerationResult(ok=False, n_eval=int(min(eval_off,
+                                                                max_eval)))
             need = n - n_acc
             B_glob = int(min(self.max_batch * R, max(
                 self.min_batch,
@@ -499,7 +507,7 @@ class GenerationEngine:
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm
         return GenerationResult(
-            theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
+            ok=True, theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
             n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec,
             accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc)
 

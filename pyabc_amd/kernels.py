@@ -392,6 +392,22 @@ def local_logpdf(pts, X, w, invs, dets, precision="f64"):
     return out
 
 
+def resample_perturb_local(X, cdf, u, z, A, lo=None, scale=None):
+    """LocalTransition draws from given uniforms / normals with the per-
+    particle factors A [N, d, d] (parity form, local_transition.py:141-145)."""
+    X = _contig(X, F64)
+    N, d = X.shape
+    B = u.numel()
+    theta = torch.empty((B, d), dtype=F64, device=_dev())
+    idx = torch.empty(B, dtype=torch.int64, device=_dev())
+    sup = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_resample_perturb_local_f64", ptr(X), N, d,
+         ptr(_contig(cdf, F64)), ptr(_contig(u, F64)), ptr(_contig(z, F64)),
+         ptr(_contig(A, F64)), ptr(lo), ptr(scale), B, ptr(theta), ptr(idx),
+         ptr(sup), nat.stream())
+    return theta, idx, sup
+
+
 def propose_local(X, cdf, covs, seed, sid, offset, B, lo=None, scale=None):
     X = _contig(X, F64)
     N, d = X.shape

@@ -156,6 +156,15 @@ class ColumnarPopulation:
     def __len__(self):
         return self.theta.shape[0]
 
+    def to_host(self):
+        """Move the columns to host memory (History keeps only the newest
+        population on the device); readers work on either."""
+        for name in ("theta", "w", "d", "stats_T"):
+            t = getattr(self, name)
+            if t is not None and t.is_cuda:
+                setattr(self, name, t.cpu())
+        return self
+
     def get_model_probabilities(self):
         return self._model_probabilities
 

@@ -13,6 +13,8 @@ from typing import Callable, List, NamedTuple
 
 import numpy as np
 
+from .distributed import agree_int
+
 logger = logging.getLogger("Adaptation")
 
 
@@ -186,6 +188,10 @@ class AdaptivePopulationSize(PopulationStrategy):
             self.nr_particles = max(min(int(est.n_estimated),
                                         self.max_population_size),
                                     self.min_population_size)
+        # the estimate draws from numpy's global state (multinomial split,
+        # bootstrap seeds); under torchrun every rank takes rank 0's size,
+        # since the generation's collectives assume one n
+        self.nr_particles = agree_int(self.nr_particles)
         logger.info(f"Change nr particles {ref} -> {self.nr_particles}")
 
     def __call__(self, t=None):

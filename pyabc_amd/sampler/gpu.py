@@ -97,7 +97,7 @@ class BatchSample(Sample):
 
     @property
     def n_accepted(self):
-        return len(self.population)
+        return 0 if self.population is None else len(self.population)
 
     def get_accepted_population(self):
         return self.population
@@ -123,14 +123,18 @@ class GPUBatchSampler(Sampler):
     """Runs each generation as batched HIP kernels on the current device.
 
     Parameters: ``seed`` (Philox seed; default drawn from numpy's global
-    state), ``min_batch`` / ``max_batch`` proposals per round,
-    ``kde_precision`` ("mfma" default, "f32" or "f64" KDE kernel), ``comm`` (multi-GPU
-    sharding, default from the torchrun environment).
+    state, rank 0's under torchrun), ``min_batch`` / ``max_batch``
+    proposals per round, ``kde_precision`` ("mfma" default, "f32" or "f64"
+    KDE kernel), ``comm`` (multi-GPU sharding, default from the torchrun
+    environment), ``check_max_eval`` (as SingleCoreSampler's,
+    singlecore.py:15-17: stop a generation at ``max_eval`` evaluations,
+    off by default).
     """
 
     def __init__(self, seed=None, min_batch=1 << 14, max_batch=1 << 22,
-                 kde_precision="mfma", comm=None):
+                 kde_precision="mfma", comm=None, check_max_eval=False):
         super().__init__()
+        self.check_max_eval = check_max_eval
         self.seed = seed
         self.min_batch = min_batch
         self.max_batch = max_batch
@@ -146,10 +150,14 @@ class GPUBatchSampler(Sampler):
         key = (id(model), tuple(lo), tuple(sc))
         eng = self._engines.get(key)
         if eng is None:
+            comm = self.comm or Comm.from_env()
             seed = self.seed if self.seed is not None else int(
                 np.random.randint(0, 2 ** 62, dtype=np.int64))
+            # every rank must draw from the same Philox streams (global-id
+            # sampling): rank 0's seed, whatever each rank's numpy state
+            seed = comm.broadcast_int(seed)
             eng = GenerationEngine(
-                model, lo, sc, comm=self.comm or Comm.from_env(),
+                model, lo, sc, comm=comm,
                 seed=seed, min_batch=self.min_batch,
                 max_batch=self.max_batch, kde_precision=self.kde_precision)
             eng.max_rounds = 100000
@@ -164,13 +172,16 @@ class GPUBatchSampler(Sampler):
         if reason is not None:
             return self._closure_path(n, simulate_one, max_eval)
         eng, names = self._engine(spec)
+        cap = max_eval if self.check_max_eval else np.inf
         model = spec.models[0]
         keys = list(model.keys)
         record = self.sample_factory.record_rejected
         if spec.kind == "calibration":
             res = eng.sample_generation(spec.t, n, None, None, None, np.inf,
                                         keep_stats=True, record=False,
-                                        stream_base=2)
+                                        stream_base=2, max_eval=cap)
+            if not res.ok:
+                return self._not_ok(res, record)
             # calibration distances are computed later (smc.py:516-534)
             res.d = torch.full_like(res.w, np.inf)
         else:
@@ -197,8 +208,11 @@ class GPUBatchSampler(Sampler):
                                         keep_stats=True, record=record,
                                         acceptance=acceptance,
                                         record_particles=record and
-                                        acceptance is not None)
+                                        acceptance is not None,
+                                        max_eval=cap)
             eng.model = spec.models[0]
+            if not res.ok:
+                return self._not_ok(res, record)
             keys = keys_d
         # the engine returns the global population, identical on every rank
         rec = None
@@ -213,12 +227,19 @@ class GPUBatchSampler(Sampler):
             recp = (res.rec_theta, res.rec_d, res.rec_acc)
         return BatchSample(pop, rec, record, rec_particles=recp)
 
+    def _not_ok(self, res, record):
+        """max_eval reached before n acceptances (singlecore.py:35-38):
+        ABCSMC.run stops on ``ok = False`` without reading a population."""
+        self.nr_evaluations_ = int(res.n_eval)
+        return BatchSample(None, None, record, ok=False)
+
     def _closure_path(self, n, simulate_one, max_eval):
+        """SingleCoreSampler.sample_until_n_accepted (singlecore.py:19-38)."""
         nr = 0
         sample = self._create_empty_sample()
         for _ in range(n):
             while True:
-                if nr >= max_eval:
+                if self.check_max_eval and nr >= max_eval:
                     break
                 p = simulate_one()
                 sample.append(p)

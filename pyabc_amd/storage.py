@@ -28,6 +28,7 @@ import json
 import os
 import sqlite3
 import threading
+import weakref
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -35,9 +36,12 @@ import pandas as pd
 
 from .population import ColumnarPopulation, Particle, Population
 from .parameters import Parameter
+from .distributed import agree_int, env_rank, env_world
 from .acceptor import save_dict_to_json, load_dict_from_json  # noqa: F401
 
-_REGISTRY = {}
+# History objects by db id, held weakly (a finished run's device and host
+# populations are freed with its last reference)
+_REGISTRY = weakref.WeakValueDictionary()
 
 # CREATE TABLE statements as SQLAlchemy emits them for db_model.py:35-127
 _DDL = [
@@ -378,7 +382,14 @@ class History:
         self._pre_nr_samples = 0
         self._meta = {}
         self._path = path
-        self._sql = _SQLStore(path) if path else None
+        # under torchrun every rank holds the same (global) populations; only
+        # rank 0 writes SQL.  Other ranks keep them on the device and open a
+        # file only to read a run they continue (create=False).
+        self._writer = env_rank() == 0
+        self._sql = _SQLStore(path) if path and (
+            self._writer or (not create and path != ":memory:")) else None
+        self._readonly = self._sql is not None and not self._writer
+        self._file_max_t = None
         self._max_t = None
         self._dup = set()      # t appended more than once: SQL readers only
         self._id = self._find_latest_id() if _id is None else _id
@@ -465,7 +476,9 @@ class History:
                           eps=eps_function_json_str,
                           population_strategy=population_strategy_json_str)
         self._pops = {}
-        if self._sql is None:
+        if self._sql is None or self._readonly:
+            if env_world() > 1 and self._path:
+                self._id = agree_int(0)   # the run id rank 0 creates below
             return
         s = self._sql
         s.flush()
@@ -490,13 +503,15 @@ class History:
         s.write_population(self._id, History.PRE_TIME, np.inf, 0, models,
                            True)
         self._max_t = History.PRE_TIME
+        if env_world() > 1:
+            agree_int(self._id)
 
     def update_nr_samples(self, t=PRE_TIME, nr_samples=0):
         if t == History.PRE_TIME:
             self._pre_nr_samples = nr_samples
         elif t in self._pops:
             self._pops[t]["n_sim"] = nr_samples
-        if self._sql is not None:
+        if self._sql is not None and not self._readonly:
             pid = self._sql.population_id(self._id, t)
             self._sql.execute(
                 "UPDATE populations SET nr_samples=? WHERE id=?",
@@ -510,7 +525,13 @@ class History:
         self._pops[t] = dict(population=population, eps=current_epsilon,
                              n_sim=nr_simulations, names=model_names,
                              end=datetime.datetime.now())
-        if self._sql is None:
+        # only the newest population stays on the device (the next fit and
+        # the loop read it); earlier ones move to host memory, where every
+        # reader still finds them
+        for t_old, e in self._pops.items():
+            if t_old != t and hasattr(e["population"], "to_host"):
+                e["population"].to_host()
+        if self._sql is None or self._readonly:
             return
         mp = population.get_model_probabilities()
         if isinstance(population, ColumnarPopulation):
@@ -543,7 +564,7 @@ class History:
 
     def done(self):
         self._meta["end_time"] = datetime.datetime.now()
-        if self._sql is not None:
+        if self._sql is not None and not self._readonly:
             self._sql.execute("UPDATE abc_smc SET end_time=? WHERE id=?",
                               (_now(), self._id))
 
@@ -572,6 +593,16 @@ class History:
     def max_t(self):
         if self._sql is None:
             return max(self._pops) if self._pops else -1
+        if self._readonly:
+            # the file as opened (rank 0 appends to it asynchronously)
+            # plus this process's own populations
+            if self._file_max_t is None:
+                self._file_max_t = self._q(
+                    "SELECT MAX(t) FROM populations WHERE abc_smc_id=?",
+                    (self._id,))[0][0]
+                if self._file_max_t is None:
+                    self._file_max_t = History.PRE_TIME
+            return max([self._file_max_t] + list(self._pops))
         if self._max_t is not None and self._sql.busy():
             # while this History's writes are queued, the generation loop
             # reads the value append_population keeps current instead of

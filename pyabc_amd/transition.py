@@ -327,6 +327,27 @@ class LocalTransition(Transition):
                                       _draw_seed(), 0, 0, size)
         return _as_output(theta.cpu().numpy(), single, _columns(self.X))
 
+    def svd_factors(self):
+        """numpy's legacy ``multivariate_normal`` factor of every local
+        covariance, A_n = sqrt(s)[:, None] * V with (U, s, V) = svd(C_n),
+        as a device tensor [N, d, d] (the reference's draw,
+        local_transition.py:141-145).  The production proposal kernel uses
+        the Cholesky factor instead (the same distribution); this factor
+        makes draws from given (u, z) equal the reference's."""
+        _, s, v = np.linalg.svd(self.covs)
+        return torch.as_tensor(np.sqrt(s)[..., :, None] * v,
+                               device=self._Xd.device)
+
+    def rvs_from(self, u, z):
+        """Draws from the reference's random numbers: u[B] uniforms (the
+        ``choice``) and z[B, d] normals (the ``multivariate_normal``), in
+        the order rvs_single consumes them.  Returns (theta [B, d], idx)."""
+        dev = self._Xd.device
+        theta, idx, _ = K.resample_perturb_local(
+            self._Xd, self._cdf, torch.as_tensor(np.asarray(u), device=dev),
+            torch.as_tensor(np.asarray(z), device=dev), self.svd_factors())
+        return theta, idx
+
 
 class _LocalDeviceFit:
     """LocalTransition state as the generation engine consumes it:

@@ -179,6 +179,46 @@ def test_local_transition_api_vs_golden(pa):
     np.testing.assert_allclose(got32, g["pdf"], rtol=1e-5)
 
 
+@pytest.mark.parametrize("name", ["local_rvs_N2000_d6_k50",
+                                  "local_rvs_N300_d3_k10"])
+def test_local_transition_rvs_vs_reference(pa, name):
+    """LocalTransition.rvs_single (local_transition.py:141-145) from the
+    reference's own random numbers (tools/gen_golden.py gen_local_rvs: the
+    uniform of ``choice`` and the normals of ``multivariate_normal`` replayed
+    from its seed): resampled indices bit-exact, draws within 1e-12 -- with
+    the device-fitted covariances and with the reference's."""
+    from pyabc_amd import kernels as K
+    g = load_golden(name)
+    d = g["X"].shape[1]
+    cols = [f"p{k:02d}" for k in range(d)]
+    tr = pa.LocalTransition(k=int(g["k"]), k_fraction=None)
+    tr.fit(pd.DataFrame(g["X"], columns=cols), g["w"].copy())
+    np.testing.assert_allclose(tr.covs, g["covs"], rtol=1e-12, atol=1e-15)
+    theta, idx = tr.rvs_from(g["u"], g["z"])
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["idx"])
+    # svd factors of the device-fitted covariances (1e-15 from the
+    # reference's): LAPACK fixes each singular vector's sign from rounding-
+    # level detail, so a 1e-15 change can flip one (measured: 2 of 400
+    # draws); a flip keeps the draw's Mahalanobis length |z|, and every other
+    # draw equals the reference's
+    th = theta.cpu().numpy()
+    same = np.all(np.isclose(th, g["theta"], rtol=1e-12, atol=1e-12), axis=1)
+    assert same.mean() >= 0.98, same.mean()
+    dl = th - g["X"][g["idx"]]
+    maha = np.einsum("bi,bij,bj->b", dl, np.linalg.inv(g["covs"][g["idx"]]),
+                     dl)
+    np.testing.assert_allclose(maha, np.sum(g["z"] ** 2, axis=1), rtol=1e-9)
+    # the kernel alone on the reference's own factors
+    _, s, v = np.linalg.svd(g["covs"])
+    A = torch.as_tensor(np.sqrt(s)[..., :, None] * v, device="cuda")
+    dv = lambda a: torch.as_tensor(a, device="cuda")  # noqa: E731
+    th2, idx2, _ = K.resample_perturb_local(dv(g["X"]), K.resample_cdf(
+        dv(g["w"])), dv(g["u"]), dv(g["z"]), A)
+    np.testing.assert_array_equal(idx2.cpu().numpy(), g["idx"])
+    np.testing.assert_allclose(th2.cpu().numpy(), g["theta"], rtol=1e-13,
+                               atol=1e-13)
+
+
 @pytest.mark.parametrize("tag", ["even_n1000", "odd_n999"])
 def test_adaptive_distance_api_vs_golden(pa, tag):
     g = load_golden(f"adaptive_{tag}_S100")

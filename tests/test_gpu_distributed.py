@@ -165,3 +165,58 @@ def test_bench_two_rank_rehearsal():
     assert 0 < rl["frac"] <= 1
     assert rl["peak"] >= rl["achieved"] > 0
     assert rl["ceiling_cycles_per_tile"] <= rl["measured_cycles_per_tile"]
+
+
+def _abcsmc_rank(rank, world, port, path, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from pyabc_amd.distributed import Comm
+    Comm.from_env("gloo", device=0)
+    import pyabc_amd as pa
+    from pyabc_amd.batch_models import LinearGaussianModel
+    np.random.seed(1000 + rank)        # rank-local numpy states differ
+    d, S = 3, 20
+    model = LinearGaussianModel.benchmark(d, S)
+    names = [f"p{k}" for k in range(d)]
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2), population_size=1500,
+                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.GPUBatchSampler(min_batch=1 << 11))
+    abc.new("sqlite:///" + path, model.observed())
+    h = abc.run(max_nr_populations=3)
+    df, w = h.distribution_numpy(0, h.max_t)
+    out[rank] = dict(id=h.id, max_t=h.max_t, theta=np.asarray(df.values),
+                     w=np.asarray(w), eps=list(h.get_all_populations()
+                                               .epsilon.values))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_abcsmc_one_sql_run(tmp_path):
+    """ABCSMC + GPUBatchSampler under two ranks (one GPU, gloo) with a file
+    History and no explicit seed: the ranks agree on rank 0's Philox seed,
+    hold identical populations, and the file holds ONE run written by
+    rank 0 (rank-0-only SQL)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import sqlite3
+    path = str(tmp_path / "run.db")
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_abcsmc_rank, args=(2, port, path, out), nprocs=2, join=True)
+        res = dict(out)
+    a, b = res[0], res[1]
+    assert a["id"] == b["id"] == 1 and a["max_t"] == b["max_t"] == 2
+    np.testing.assert_array_equal(a["theta"], b["theta"])
+    np.testing.assert_array_equal(a["w"], b["w"])
+    assert a["eps"] == b["eps"]
+    c = sqlite3.connect(path)
+    assert c.execute("SELECT COUNT(*) FROM abc_smc").fetchone()[0] == 1
+    assert c.execute("SELECT COUNT(*) FROM populations").fetchone()[0] == 4
+    n_par = c.execute("SELECT COUNT(*) FROM particles").fetchone()[0]
+    c.close()
+    assert n_par == 3 * 1500 + 1

@@ -1,0 +1,79 @@
+"""Multi-rank host logic under torchrun semantics, on the CPU (gloo,
+world size 2): decisions every rank must share come from rank 0, and only
+rank 0 writes the SQL History (a run is one abc_smc row however many ranks
+drive it)."""
+import os
+import socket
+import sqlite3
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+
+
+def _history_rank(rank, world, port, path, out):
+    _init(rank, world, port)
+    import torch.distributed as dist
+    from tests.test_history import write_ours
+    from pyabc_amd.distributed import agree_int
+    # rank-local numpy states differ: the agreed value is rank 0's
+    np.random.seed(100 + rank)
+    out[f"seed{rank}"] = agree_int(int(np.random.randint(0, 2 ** 62)))
+    h = write_ours(path)
+    out[f"id{rank}"] = h.id
+    out[f"max_t{rank}"] = h.max_t
+    df, w = h.get_distribution(0, h.max_t)
+    out[f"dist{rank}"] = (df.values.tolist(), list(w))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_two_ranks_one_sql_run(tmp_path):
+    """Two ranks drive the same run into one sqlite file: one abc_smc row,
+    one row per population, the same run id and the same readers' answers
+    on both ranks (rank 1 serves them from memory)."""
+    path = str(tmp_path / "run.db")
+    # a previous run in the file: the new run's id is 2 on both ranks
+    sys.path.insert(0, ROOT)
+    from tests.test_history import write_ours
+    write_ours(path)
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_history_rank, args=(2, port, path, out), nprocs=2,
+                 join=True)
+        res = dict(out)
+    assert res["seed0"] == res["seed1"]
+    assert res["id0"] == res["id1"] == 2
+    assert res["max_t0"] == res["max_t1"]
+    assert res["dist0"] == res["dist1"]
+    c = sqlite3.connect(path)
+    runs = c.execute("SELECT id FROM abc_smc").fetchall()
+    n_pops = c.execute("SELECT COUNT(*) FROM populations WHERE abc_smc_id=2"
+                       ).fetchone()[0]
+    n_pops1 = c.execute("SELECT COUNT(*) FROM populations WHERE abc_smc_id=1"
+                        ).fetchone()[0]
+    c.close()
+    assert [r[0] for r in runs] == [1, 2]
+    assert n_pops == n_pops1 > 1

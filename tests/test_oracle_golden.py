@@ -131,7 +131,8 @@ def test_pnorm_kat():
         pow(sum([(2 * 1) ** 2, (3 * 2) ** 2]), 1 / 2)
 
 
-@pytest.mark.parametrize("name", golden_names("local_"))
+@pytest.mark.parametrize("name", [n for n in golden_names("local_")
+                                  if not n.startswith("local_rvs")])
 def test_local_transition(name):
     g = load_golden(name)
     X, w, k = g["X"], g["w"], int(g["k"])
@@ -143,6 +144,16 @@ def test_local_transition(name):
     np.testing.assert_allclose(invs, g["inv_covs"], rtol=1e-10, atol=1e-12)
     pdf = ref.local_pdf(g["pts"], X, w, g["inv_covs"], g["dets"])
     np.testing.assert_allclose(pdf, g["pdf"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", golden_names("local_rvs"))
+def test_local_rvs(name):
+    """LocalTransition.rvs_single from the reference's replayed random
+    numbers: indices and draws bit-exact (local_transition.py:141-145)."""
+    g = load_golden(name)
+    idx, theta = ref.local_rvs(g["X"], g["w"], g["covs"], g["u"], g["z"])
+    np.testing.assert_array_equal(idx, g["idx"])
+    np.testing.assert_array_equal(theta, g["theta"])
 
 
 def test_philox_kat():

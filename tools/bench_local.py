@@ -1,0 +1,48 @@
+"""LocalTransition device passes at C4 (N = 2e5, d = 6, k = 50): kNN,
+local covariances, density (fp32 and fp64) -- ms per call, HIP events."""
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from pyabc_amd import kernels as K  # noqa: E402
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return min(ts)
+
+
+def main(N=200_000, d=6, k=50):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
+    w = torch.rand(N, dtype=torch.float64, device="cuda", generator=g)
+    w /= w.sum()
+    nbr, _ = K.knn(X, k)
+    covs, invs, dets = K.local_cov(X, w, nbr)
+    pts = X + 0.1
+    out = {"knn_ms": timed(lambda: K.knn(X, k)),
+           "local_cov_ms": timed(lambda: K.local_cov(X, w, nbr))}
+    for prec in ("f32", "f64"):
+        out[f"pdf_{prec}_ms"] = timed(
+            lambda: K.local_logpdf(pts, X, w, invs, dets, precision=prec))
+    a = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f32")
+    b = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f64")
+    out["max_rel_f32_vs_f64"] = float((a - b).abs().max())
+    print({k_: round(v, 4) if isinstance(v, float) else v
+           for k_, v in out.items()}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

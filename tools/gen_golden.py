@@ -258,8 +258,45 @@ def gen_local():
         print(f"    local fit {time.time() - t0:.2f}s")
 
 
+def gen_local_rvs():
+    """LocalTransition.rvs_single (local_transition.py:141-145): B calls
+    after np.random.seed; the uniforms and normals each call consumes
+    (choice: one random_sample; multivariate_normal: standard_normal(d)) are
+    replayed from the same seed and stored with the outputs."""
+    for N, d, k, seed, B in [(2000, 6, 50, 0, 400), (300, 3, 10, 1, 200)]:
+        rng = np.random.default_rng(700 + seed)
+        X = rng.normal(size=(N, d)) * rng.uniform(0.5, 2.0, size=d)
+        w = rng.uniform(0.0, 1.0, size=N)
+        w = w / w.sum()
+        cols = pnames(d)
+        tr = LocalTransition(k=k, k_fraction=None, scaling=1.0)
+        tr.fit(pd.DataFrame(X, columns=cols), w.copy())
+        np.random.seed(4242 + seed)
+        theta = np.array([tr.rvs_single().values for _ in range(B)])
+        rs = np.random.RandomState(4242 + seed)
+        u = np.empty(B)
+        z = np.empty((B, d))
+        for b in range(B):
+            u[b] = rs.random_sample()
+            z[b] = rs.standard_normal(d)
+        cdf = np.cumsum(tr.w)
+        cdf /= cdf[-1]
+        idx = cdf.searchsorted(u, side="right")
+        # replay check: the reference's own factor (svd of C_idx)
+        rep = np.empty_like(theta)
+        for b in range(B):
+            _, s, v = np.linalg.svd(tr.covs[idx[b]])
+            rep[b] = z[b] @ (np.sqrt(s)[:, None] * v) + X[idx[b]]
+        assert np.array_equal(rep, theta), np.abs(rep - theta).max()
+        save(f"local_rvs_N{N}_d{d}_k{k}", X=X, w=w, k=np.array(tr.k),
+             covs=tr.covs, u=u, z=z, idx=idx.astype(np.int64), theta=theta,
+             _ref=np.array("pyabc/transition/local_transition.py:141-145 "
+                           "(np.random.choice + multivariate_normal)"))
+
+
 GENS = {"kde": gen_kde, "resample": gen_resample, "distance": gen_distance,
-        "quantile": gen_quantile, "local": gen_local}
+        "quantile": gen_quantile, "local": gen_local,
+        "local_rvs": gen_local_rvs}
 
 def _main():
     ap = argparse.ArgumentParser()

@@ -210,6 +210,17 @@ int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
                       const int32_t* nbr, int k, double scaling,
                       double* covs, double* inv_covs, double* dets,
                       hipStream_t stream);
+/* The same for the particles [row0, row0 + nrows) only (one rank's share of
+ * the fit): nbr / nbr_d2 / covs / inv_covs / dets hold those
+ * rows, indexed from row0; every row's result equals the full call's.
+ *                                                   local_transition.py:77-96 */
+int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
+                     int64_t nrows, int32_t* nbr, double* nbr_d2, void* ws,
+                     size_t ws_bytes, hipStream_t stream);
+int abc_local_cov_rows_f64(const double* X, const double* w, int64_t N, int d,
+                           const int32_t* nbr, int k, int64_t row0,
+                           int64_t nrows, double scaling, double* covs,
+                           double* inv_covs, double* dets, hipStream_t stream);
 int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
                          const double* w, const double* inv_covs,
                          const double* dets, int64_t N, int d,

@@ -117,6 +117,11 @@ _SIGS = {
                             c_size, c_ptr]),
     "abc_local_cov_f64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr, c_int,
                                   c_dbl, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_knn_rows_f64": (c_int, [c_ptr, c_i64, c_int, c_int, c_i64, c_i64,
+                                 c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
+    "abc_local_cov_rows_f64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
+                                       c_int, c_i64, c_i64, c_dbl, c_ptr,
+                                       c_ptr, c_ptr, c_ptr]),
     "abc_local_logpdf_workspace_bytes": (c_size, [c_i64, c_i64]),
     "abc_local_logpdf_f64": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
                                      c_ptr, c_i64, c_int, c_ptr, c_ptr,

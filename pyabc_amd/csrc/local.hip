@@ -202,18 +202,20 @@ template <int D, int H>
 __global__ __launch_bounds__(64) void knn_kernel(
     const double* __restrict__ X, const float* __restrict__ Xf,
     const unsigned long long* __restrict__ amax, int64_t N, int k,
-    int32_t* __restrict__ nbr, double* __restrict__ nbr_d2) {
+    int64_t rlo, int64_t rhi, int32_t* __restrict__ nbr,
+    double* __restrict__ nbr_d2) {
+  // query rows [rlo, rhi) against all N; row r's output is row r - rlo
   constexpr int CAP = H * 64;
   __shared__ int buf[kKnnRows][CAP];
   const int lane = threadIdx.x;
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kKnnRows;
+  const int64_t row0 = rlo + static_cast<int64_t>(blockIdx.x) * kKnnRows;
   const double A = __longlong_as_double(static_cast<long long>(*amax));
 
   f32x2 xrf[kKnnRows / 2][D];   // rows in pairs for packed fp32 math
 #pragma unroll
   for (int p = 0; p < kKnnRows / 2; ++p) {
-    const int64_t ra = row0 + 2 * p < N ? row0 + 2 * p : N - 1;
-    const int64_t rb = row0 + 2 * p + 1 < N ? row0 + 2 * p + 1 : N - 1;
+    const int64_t ra = row0 + 2 * p < rhi ? row0 + 2 * p : rhi - 1;
+    const int64_t rb = row0 + 2 * p + 1 < rhi ? row0 + 2 * p + 1 : rhi - 1;
 #pragma unroll
     for (int q = 0; q < D; ++q) xrf[p][q] = f32x2{Xf[ra * D + q], Xf[rb * D + q]};
   }
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(64) void knn_kernel(
 #pragma unroll
     for (int r = 0; r < kKnnRows; ++r) {
       const int64_t row = row0 + r;
-      bool cand = valid && j != row && row < N &&
+      bool cand = valid && j != row && row < rhi &&
                   (d2f[r] < Tf[r] || Tf[r] == INFINITY);
       uint64_t m = __ballot(cand);
       if (!m) continue;
@@ -276,9 +278,9 @@ __global__ __launch_bounds__(64) void knn_kernel(
 #pragma unroll
   for (int r = 0; r < kKnnRows; ++r) {
     const int64_t row = row0 + r;
-    if (row < N)
-      knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane, nbr + row * k,
-                         nbr_d2 ? nbr_d2 + row * k : nullptr);
+    if (row < rhi)
+      knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane, nbr + (row - rlo) * k,
+                         nbr_d2 ? nbr_d2 + (row - rlo) * k : nullptr);
   }
 }
 
@@ -339,10 +341,15 @@ template <int D>
 __global__ __launch_bounds__(128) void local_cov_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
     int d, const int32_t* __restrict__ nbr, int k, double scaling,
-    double* __restrict__ covs, double* __restrict__ invs,
-    double* __restrict__ dets) {
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+    int64_t rlo, int64_t rhi, double* __restrict__ covs,
+    double* __restrict__ invs, double* __restrict__ dets) {
+  // particles [rlo, rhi); nbr and the outputs are indexed from rlo
+  const int64_t n = rlo + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= rhi) return;
+  nbr -= rlo * k;
+  covs -= rlo * d * d;
+  invs -= rlo * d * d;
+  dets -= rlo;
   double xn[D];
   for (int q = 0; q < d; ++q) xn[q] = X[n * d + q];
   // local weights lw = w[nbr] / sum
@@ -742,28 +749,34 @@ size_t abc_knn_workspace_bytes(int64_t N, int k) {
   return static_cast<size_t>(N > 0 ? N : 1) * 8 * 4 + 256;
 }
 
-int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
-                double* nbr_d2, void* ws, size_t ws_bytes, hipStream_t st) {
+int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
+                     int64_t nrows, int32_t* nbr, double* nbr_d2, void* ws,
+                     size_t ws_bytes, hipStream_t st) {
   ABC_REQUIRE(N > 1 && k >= 1 && k <= N - 1, "knn: need 1 <= k <= N-1");
   ABC_REQUIRE(k <= kMaxK, "knn: k=%d exceeds the one-pass limit %d", k, kMaxK);
   ABC_REQUIRE(N < (1ll << 31), "knn: N must fit int32 indices");
+  ABC_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= N,
+              "knn: rows [%lld, %lld) outside [0, %lld)", (long long)row0,
+              (long long)(row0 + nrows), (long long)N);
+  if (nrows == 0) return kOk;
   ABC_REQUIRE(X && nbr && ws, "knn: null pointer");
   ABC_REQUIRE(ws_bytes >= abc_knn_workspace_bytes(N, k), "knn: workspace too small");
   unsigned long long* amax = static_cast<unsigned long long*>(ws);
   float* Xf = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
   const unsigned pg = static_cast<unsigned>(ceil_div(N, 256));
-  const unsigned grid = static_cast<unsigned>(ceil_div(N, kKnnRows));
+  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, kKnnRows));
+  const int64_t rlo = row0, rhi = row0 + nrows;
 #define L(DD)                                                                   \
   {                                                                             \
     hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(pg), dim3(256), 0, st, X, N, \
                        Xf, amax);                                               \
     if (k <= 64)                                                                \
       hipLaunchKernelGGL((knn_kernel<DD, 2>), dim3(grid), dim3(64), 0, st, X,   \
-                         Xf, amax, N, k, nbr, nbr_d2);                          \
+                         Xf, amax, N, k, rlo, rhi, nbr, nbr_d2);                \
     else                                                                        \
       hipLaunchKernelGGL((knn_kernel<DD, 4>), dim3(grid), dim3(64), 0, st, X,   \
-                         Xf, amax, N, k, nbr, nbr_d2);                          \
+                         Xf, amax, N, k, rlo, rhi, nbr, nbr_d2);                \
   }
   switch (d) {
     case 1: L(1) break;
@@ -783,14 +796,24 @@ int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
   return kOk;
 }
 
-int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
-                      const int32_t* nbr, int k, double scaling, double* covs,
-                      double* inv_covs, double* dets, hipStream_t st) {
+int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
+                double* nbr_d2, void* ws, size_t ws_bytes, hipStream_t st) {
+  return abc_knn_rows_f64(X, N, d, k, 0, N, nbr, nbr_d2, ws, ws_bytes, st);
+}
+
+int abc_local_cov_rows_f64(const double* X, const double* w, int64_t N, int d,
+                           const int32_t* nbr, int k, int64_t row0,
+                           int64_t nrows, double scaling, double* covs,
+                           double* inv_covs, double* dets, hipStream_t st) {
   ABC_REQUIRE(N >= 1 && k >= 1, "local_cov: bad sizes");
-  const unsigned g = static_cast<unsigned>(ceil_div(N, 128));
+  ABC_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= N,
+              "local_cov: rows outside [0, N)");
+  if (nrows == 0) return kOk;
+  const unsigned g = static_cast<unsigned>(ceil_div(nrows, 128));
+  const int64_t rlo = row0, rhi = row0 + nrows;
 #define L(DD)                                                                   \
   hipLaunchKernelGGL((local_cov_kernel<DD>), dim3(g), dim3(128), 0, st, X, w, N, \
-                     d, nbr, k, scaling, covs, inv_covs, dets);
+                     d, nbr, k, scaling, rlo, rhi, covs, inv_covs, dets);
   if (d <= 4) {
     L(4)
   } else if (d <= 8) {
@@ -804,6 +827,13 @@ int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
 #undef L
   ABC_LAUNCH_CHECK("local_cov_kernel");
   return kOk;
+}
+
+int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
+                      const int32_t* nbr, int k, double scaling, double* covs,
+                      double* inv_covs, double* dets, hipStream_t st) {
+  return abc_local_cov_rows_f64(X, w, N, d, nbr, k, 0, N, scaling, covs,
+                                inv_covs, dets, st);
 }
 
 // The n-range is cut into a fixed number of chunks that depends on N only,

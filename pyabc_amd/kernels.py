@@ -361,6 +361,33 @@ def knn(X, k):
     return nbr, d2
 
 
+def knn_rows(X, k, row0, nrows):
+    """kNN of the particles [row0, row0 + nrows) against all N."""
+    X = _contig(X, F64)
+    N, d = X.shape
+    nbr = torch.empty((nrows, k), dtype=torch.int32, device=_dev())
+    d2 = torch.empty((nrows, k), dtype=F64, device=_dev())
+    wsb = nat.lib().abc_knn_workspace_bytes(N, k)
+    ws = WS.get(wsb, "knn")
+    call("abc_knn_rows_f64", ptr(X), N, d, k, row0, nrows, ptr(nbr), ptr(d2),
+         ptr(ws), wsb, nat.stream())
+    return nbr, d2
+
+
+def local_cov_rows(X, w, nbr, row0, scaling=1.0):
+    """Local covariances of the particles [row0, row0 + len(nbr))."""
+    X = _contig(X, F64)
+    N, d = X.shape
+    nrows, k = nbr.shape
+    covs = torch.empty((nrows, d, d), dtype=F64, device=_dev())
+    invs = torch.empty((nrows, d, d), dtype=F64, device=_dev())
+    dets = torch.empty(nrows, dtype=F64, device=_dev())
+    call("abc_local_cov_rows_f64", ptr(X), ptr(_contig(w, F64)), N, d,
+         ptr(nbr.contiguous()), k, row0, nrows, float(scaling), ptr(covs),
+         ptr(invs), ptr(dets), nat.stream())
+    return covs, invs, dets
+
+
 def local_cov(X, w, nbr, scaling=1.0):
     X = _contig(X, F64)
     N, d = X.shape

@@ -17,6 +17,7 @@ import pandas as pd
 import torch
 
 from . import kernels as K
+from .distributed import Comm
 from .engine import (DeviceMVNFit, silverman_rule_of_thumb,
                      scott_rule_of_thumb)
 from .frames import DeviceFrame, as_device_matrix, as_device_vector
@@ -265,9 +266,31 @@ class LocalTransition(Transition):
                                    device=self._Xd.device)
             dets = torch.as_tensor([det], device=self._Xd.device)
         else:
-            nbr, _ = K.knn(self._Xd, kk)
-            covs, invs, dets = K.local_cov(self._Xd, self._wd, nbr,
-                                           self.scaling)
+            comm = Comm.current()
+            if comm.active:
+                # each rank fits its row share, one all-gather
+                # of (covs, inverses, dets); every row equals the 1-rank fit
+                q, m = divmod(n, comm.world)
+                r = comm.rank
+                lo = r * q + min(r, m)
+                hi = lo + q + (1 if r < m else 0)
+                sizes = [q + (1 if s < m else 0) for s in range(comm.world)]
+                nbr, _ = K.knn_rows(self._Xd, kk, lo, hi - lo)
+                c, i, dt = K.local_cov_rows(self._Xd, self._wd, nbr, lo,
+                                            self.scaling)
+                packed = torch.cat([c.reshape(hi - lo, -1),
+                                    i.reshape(hi - lo, -1),
+                                    dt.view(-1, 1)], 1)
+                allp = comm.all_gather_rows(packed, sizes)
+                covs = allp[:, :d * d].reshape(n, d, d).contiguous()
+                invs = allp[:, d * d:2 * d * d].reshape(n, d, d).contiguous()
+                dets = allp[:, 2 * d * d].contiguous()
+                nbr = comm.all_gather_rows(nbr.to(torch.int64), sizes).to(
+                    torch.int32)
+            else:
+                nbr, _ = K.knn(self._Xd, kk)
+                covs, invs, dets = K.local_cov(self._Xd, self._wd, nbr,
+                                               self.scaling)
             self.nbr = nbr
         self._covs, self._invs, self._dets = covs, invs, dets
         self._cdf = K.resample_cdf(self._wd)

@@ -220,3 +220,67 @@ def test_two_rank_abcsmc_one_sql_run(tmp_path):
     n_par = c.execute("SELECT COUNT(*) FROM particles").fetchone()[0]
     c.close()
     assert n_par == 3 * 1500 + 1
+
+
+def _local_fit_data():
+    rng = np.random.default_rng(31)
+    X = rng.normal(size=(5001, 4)) * [1.0, 2.0, 0.5, 1.5]
+    w = rng.uniform(0.2, 1.0, size=5001)
+    return X, w / w.sum()
+
+
+def _local_generation(comm):
+    """LocalTransition fit (sharded over ranks when comm is active) and one
+    engine generation with it: the C4 path."""
+    import pandas as pd
+    import pyabc_amd as pa
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.engine import GenerationEngine
+    X, w = _local_fit_data()
+    tr = pa.LocalTransition(k=20, k_fraction=None)
+    tr.fit(pd.DataFrame(X, columns=[f"p{k}" for k in range(4)]), w)
+    d, S = 4, 20
+    model = LinearGaussianModel.benchmark(d, S)
+    x0 = torch.as_tensor(model._x0, device="cuda")
+    fw = torch.ones(S, dtype=torch.float64, device="cuda")
+    eng = GenerationEngine(model, np.full(d, -5.0), np.full(d, 10.0),
+                           distance_p=2.0, comm=comm, seed=3,
+                           min_batch=1 << 11)
+    eng.max_batch = 1 << 11
+    res = eng.sample_generation(1, 3001, tr.device_fit, x0, fw, 40.0)
+    return dict(covs=tr.covs, invs=tr.inv_covs, dets=tr.determinants,
+                nbr=tr.nbr.cpu().numpy(), theta=res.theta.cpu().numpy(),
+                logpd=res.logpd.cpu().numpy(), n_eval=int(res.n_eval))
+
+
+def _local_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from pyabc_amd.distributed import Comm
+    comm = Comm.from_env("gloo", device=0)
+    out[rank] = _local_generation(comm)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_ranks_local_transition_fit_sharded_bit_for_bit():
+    """each rank fits kNN + covariances for its row share and
+    the shares are all-gathered; the fit (neighbour sets, covariances,
+    inverses, determinants) and a LocalTransition generation (population,
+    log-densities, evaluation count) equal the one-rank result bit for bit
+    (local_transition.py:77-96)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_local_rank, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    from pyabc_amd.distributed import Comm
+    one = _local_generation(Comm.single())
+    for r in (0, 1):
+        for k in ("covs", "invs", "dets", "nbr", "theta", "logpd"):
+            np.testing.assert_array_equal(res[r][k], one[k], err_msg=k)
+        assert res[r]["n_eval"] == one["n_eval"]

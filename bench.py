@@ -43,15 +43,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(fit, model, x0, eps, seconds):
+def cpu_baseline(gens, model, x0, d, seconds):
     """The reference's per-particle CPU path (restated by the oracle) on the
     host cores, MulticoreEvalParallelSampler-style (oracle/cpu_baseline.py),
-    over the same previous population, model and epsilon."""
+    over the same generations (previous population, fit, epsilon) the GPU
+    timed."""
     from oracle import cpu_baseline as cb
-    d = fit.X.shape[1]
-    return cb.run(fit.X.cpu().numpy(), fit.w.cpu().numpy(), fit.cov,
-                  model.A_host, x0.cpu().numpy(), np.full(d, -5.0),
-                  np.full(d, 10.0), eps, model.sigma, 2.0, seconds=seconds)
+    return cb.run(gens, model.A_host, x0.cpu().numpy(), np.full(d, -5.0),
+                  np.full(d, 10.0), model.sigma, 2.0, seconds=seconds)
 
 
 def kde_traffic():
@@ -185,10 +184,20 @@ def main():
     eps = float(K.weighted_quantile(dist, w, 0.5)[0].item())
     fit = DeviceMVNFit(theta, w)
 
-    state = {"fit": fit, "eps": eps, "n_eval": 0, "t": 1}
+    # the CPU leg reruns up to 4 evenly spaced timed generations; their fits
+    # are kept by reference (no copy inside the timed region)
+    K_ = args.steps
+    pick = sorted({round(i * (K_ - 1) / 3) for i in range(4)}) if K_ > 4 \
+        else list(range(K_))
+    state = {"fit": fit, "eps": eps, "n_eval": 0, "t": 1, "sched": {},
+             "k": None}
 
     def step():
         t = state["t"]
+        if state["k"] is not None:
+            if state["k"] in pick:
+                state["sched"][state["k"]] = (state["fit"], state["eps"])
+            state["k"] += 1
         res = eng.sample_generation(t, N, state["fit"], x0, fw, state["eps"])
         th, dd, ww, n_eval, _ = eng.gather_population(res)
         state["eps"] = float(K.weighted_quantile(dd, ww, 0.5)[0].item())
@@ -199,6 +208,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    state["k"] = 0
     eng.kde_events = []
     comm.barrier()
     torch.cuda.synchronize()
@@ -265,15 +275,24 @@ def main():
                                  tiles_per_launch),
     }
     if R == 1 and not args.no_cpu_baseline:
-        v, cores, acc, ev, wall = cpu_baseline(state["fit"], model, x0,
-                                               state["eps"], args.cpu_seconds)
+        # the timed generations themselves, up to 4 evenly spaced ones
+        sched = state["sched"]
+        gens = [(sched[i][0].X.cpu().numpy(), sched[i][0].w.cpu().numpy(),
+                 sched[i][0].cov, sched[i][1]) for i in pick]
+        cb = cpu_baseline(gens, model, x0, d, args.cpu_seconds)
         out["cpu_baseline"] = {
-            "value": v, "unit": "accepted particles/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{acc} accepted particles ({ev} evaluations) in "
-                      f"{args.cpu_seconds:.0f} s on each of {cores} spawned "
-                      f"workers (1 BLAS thread each), same generation "
-                      f"(N_prev={N}, d={d}, S={S}, same eps): the "
+            "value": cb["rate"], "unit": "accepted particles/s",
+            "cores": cb["workers"], "kind": "port",
+            "cpu_model": cb["cpu_model"], "host_cpus": cb["host_cpus"],
+            "per_generation": cb["per_generation"],
+            "eps": [g[3] for g in gens],
+            "sample": f"the timed schedule's generations {pick} (of "
+                      f"{K_}; eps {[round(g[3], 3) for g in gens]}), "
+                      f"{cb['seconds_per_generation']:.1f} s each on "
+                      f"{cb['workers']} spawned workers (1 BLAS thread each; "
+                      f"{cb['accepted']} accepted of {cb['evaluations']} "
+                      f"evaluations); value = harmonic mean of the "
+                      f"per-generation rates (N_prev={N}, d={d}, S={S}): the "
                       f"reference's per-particle algorithm "
                       f"(MulticoreEvalParallelSampler layout; O(N) CDF per "
                       f"proposal, O(N d) KDE per acceptance) restated by "

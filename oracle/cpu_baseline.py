@@ -18,8 +18,12 @@ and per accepted particle the O(N d) KDE density ``transition_pdf``
 
 Workers are started with the ``spawn`` method (fresh interpreters that
 import numpy and this module only; they never touch the GPU) and pinned to
-one BLAS thread each.  Each runs for a fixed wall budget; the baseline is the
-sum over workers of accepted particles / that worker's busy time.
+one BLAS thread each.  They run the SAME generations the GPU timed (each
+generation's previous population, fit and epsilon), an equal wall slice per
+generation; a generation's rate is the sum over workers of accepted
+particles / busy time, and the baseline is their harmonic mean -- the rate
+of running each generation to the same population size, as the GPU's value
+is measured.
 """
 import multiprocessing as mp
 import os
@@ -28,47 +32,70 @@ import time
 import numpy as np
 
 
-def _worker(path, seconds, seed, out_q):
+def _worker(paths, seconds, seed, out_q):
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import ref_cpu as ref
-    with np.load(path, allow_pickle=False) as f:
-        X, w, cov = f["X"], f["w"], f["cov"]
-        A_model, x0, lo, sc = f["A_model"], f["x0"], f["lo"], f["sc"]
-        eps, sigma, p = float(f["eps"]), float(f["sigma"]), float(f["p"])
-    A = ref.svd_factor(cov)
-    fw = np.ones_like(x0)
-    d = X.shape[1]
     rng = np.random.default_rng(seed)
-    acc = evals = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        cdf = ref.resample_cdf(w)                      # O(N) per proposal
-        idx = ref.resample_indices(cdf, rng.random())
-        th = X[idx] + rng.standard_normal(d) @ A
-        if not ref.uniform_box_support(th[None], lo, sc)[0]:
-            continue
-        y = th @ A_model.T + sigma * rng.standard_normal(A_model.shape[0])
-        dist = ref.pnorm_distance(y[None], x0, fw, p)[0]
-        evals += 1
-        if dist <= eps:
-            acc += 1
-            ref.kde_transition_pd(th[None], X, w, cov)  # O(N d)
-    out_q.put((acc, evals, time.perf_counter() - t0))
+    res = []
+    for path in paths:     # one slice per generation of the GPU's schedule
+        with np.load(path, allow_pickle=False) as f:
+            X, w, cov = f["X"], f["w"], f["cov"]
+            A_model, x0, lo, sc = f["A_model"], f["x0"], f["lo"], f["sc"]
+            eps, sigma, p = float(f["eps"]), float(f["sigma"]), float(f["p"])
+        A = ref.svd_factor(cov)
+        fw = np.ones_like(x0)
+        d = X.shape[1]
+        acc = evals = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            cdf = ref.resample_cdf(w)                      # O(N) per proposal
+            idx = ref.resample_indices(cdf, rng.random())
+            th = X[idx] + rng.standard_normal(d) @ A
+            if not ref.uniform_box_support(th[None], lo, sc)[0]:
+                continue
+            y = th @ A_model.T + sigma * rng.standard_normal(A_model.shape[0])
+            dist = ref.pnorm_distance(y[None], x0, fw, p)[0]
+            evals += 1
+            if dist <= eps:
+                acc += 1
+                ref.kde_transition_pd(th[None], X, w, cov)  # O(N d)
+        res.append((acc, evals, time.perf_counter() - t0))
+    out_q.put(res)
 
 
-def run(X, w, cov, A_model, x0, lo, sc, eps, sigma, p=2.0, workers=None,
-        seconds=8.0, tmpdir="/tmp"):
-    """Returns (accepted/s over all workers, workers, accepted, evaluations,
-    wall seconds)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
+        tmpdir="/tmp"):
+    """The CPU path over the GPU's own generations: ``gens`` is a list of
+    (X, w, cov, eps) -- previous population, its fitted covariance and the
+    generation's epsilon -- each run for seconds / len(gens) on every
+    worker.  Returns a dict: per-generation accepted/s summed over workers,
+    their schedule rate (the harmonic mean: the rate of running every
+    generation to the same population size, as the GPU value is), workers,
+    accepted, evaluations, wall seconds."""
     if workers is None:
         workers = min(16, os.cpu_count() or 1)
-    path = os.path.join(tmpdir, f"abc_cpu_baseline_{os.getpid()}.npz")
-    np.savez(path, X=X, w=w, cov=cov, A_model=A_model, x0=x0, lo=lo, sc=sc,
-             eps=eps, sigma=sigma, p=p)
+    paths = []
+    for g, (X, w, cov, eps) in enumerate(gens):
+        path = os.path.join(tmpdir, f"abc_cpu_baseline_{os.getpid()}_{g}.npz")
+        np.savez(path, X=X, w=w, cov=cov, A_model=A_model, x0=x0, lo=lo,
+                 sc=sc, eps=eps, sigma=sigma, p=p)
+        paths.append(path)
+    per = seconds / len(gens)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(path, seconds, 1000 + i, q))
+    procs = [ctx.Process(target=_worker, args=(paths, per, 1000 + i, q))
              for i in range(workers)]
     t0 = time.perf_counter()
     for pr in procs:
@@ -77,8 +104,13 @@ def run(X, w, cov, A_model, x0, lo, sc, eps, sigma, p=2.0, workers=None,
     for pr in procs:
         pr.join()
     wall = time.perf_counter() - t0
-    os.remove(path)
-    acc = sum(r[0] for r in res)
-    ev = sum(r[1] for r in res)
-    rate = sum(r[0] / r[2] for r in res)
-    return rate, workers, acc, ev, wall
+    for path in paths:
+        os.remove(path)
+    rates = [sum(r[g][0] / r[g][2] for r in res) for g in range(len(gens))]
+    acc = [sum(r[g][0] for r in res) for g in range(len(gens))]
+    ev = [sum(r[g][1] for r in res) for g in range(len(gens))]
+    sched = len(rates) / sum(1.0 / max(r, 1e-12) for r in rates)
+    return dict(rate=sched, per_generation=rates, workers=workers,
+                accepted=acc, evaluations=ev, wall=wall,
+                seconds_per_generation=per, cpu_model=cpu_model(),
+                host_cpus=os.cpu_count())

@@ -89,6 +89,24 @@ def main():
         Y = fit.packed.whiten(theta)
         t = timed(lambda: fit.packed.logpdf_whitened(Y), reps=3)
         pairs = N * fit.packed.npad
+        if prec == "mfma":
+            # priced against its own SIMD issue ceiling (bench.py
+            # kde_roofline: PMC per-tile counts at d = 8, static otherwise)
+            import bench
+            tiles = (K.nat.lib().abc_kde_mfma_new_rows(N, d) // 32) * \
+                (fit.packed.npad // 32)
+            ach = (3 * d + 4) * pairs / t / 1e12
+            rl = bench.kde_roofline(d, ach, None, None, t, pairs, tiles)
+            print(json.dumps({
+                "kernel": "kde_logpdf_mfma", "ms": t * 1e3, "units": pairs,
+                "unit": "pairs", "per_unit": 3 * d + 4, "bound": "valu_issue",
+                "achieved": ach, "peak": rl["peak"], "ach_unit": "TFLOP/s",
+                "frac": rl["frac"], "units_per_s": pairs / t,
+                "ceiling_cycles_per_tile": rl["ceiling_cycles_per_tile"],
+                "valu_equiv_frac_fp32": rl["valu_equiv"]["frac"],
+                "mfma_bf16_frac": rl["mfma_bf16"]["frac"],
+                "N": N, "M": N, "d": d}), flush=True)
+            continue
         report(f"kde_logpdf_{prec}", t, pairs, "pairs", 3 * d + 4,
                "valu_f64" if prec == "f64" else "valu_f32",
                {"N": N, "M": N, "d": d})

@@ -66,6 +66,22 @@ int abc_propose_philox_f64(const double* X, int64_t N, int d,
                            int64_t B, double* theta, int64_t* idx,
                            uint8_t* in_support, hipStream_t stream);
 /* t = 0 prior draws, RV('uniform', lo, scale).rvs()  random_variables.py:434 */
+/* Bucket table of a CDF for the proposal search: tab[k] = searchsorted(cdf,
+ * k / 2^log2k, 'right') for k = 0 .. 2^log2k (tab has 2^log2k + 1 entries).
+ * abc_propose_philox_indexed_f64 = abc_propose_philox_f64 with the search
+ * of u bracketed by tab[floor(u 2^log2k)] .. tab[.. + 1]: identical
+ * indices, ~log2(N / 2^log2k) dependent loads instead of log2 N.
+ *                                   multivariatenormal.py:89 (choice p=w) */
+int abc_cdf_index_f64(const double* cdf, int64_t n, int log2k, int64_t* tab,
+                      hipStream_t stream);
+int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
+                                   const double* cdf, const int64_t* tab,
+                                   int log2k, const double* A,
+                                   const double* lo, const double* scale,
+                                   uint64_t seed, uint64_t sid,
+                                   uint64_t offset, int64_t B, double* theta,
+                                   int64_t* idx, uint8_t* in_support,
+                                   hipStream_t stream);
 int abc_prior_uniform_f64(const double* lo, const double* scale, int d,
                           uint64_t seed, uint64_t sid, uint64_t offset,
                           int64_t B, double* theta, hipStream_t stream);

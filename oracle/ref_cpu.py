@@ -455,6 +455,27 @@ def philox_normal(seed, stream, n):
     return np.where(odd, r * np.sin(ang), r * np.cos(ang))
 
 
+def philox_normal4_f32(seed, stream, n):
+    """The synthetic simulators' noise z[i] (library: philox.hpp
+    box_muller4_f32): block i//4, 24-bit uniforms (w >> 8) * 2^-24 of each
+    word, fp32 Box-Muller -- words (0,1) give members 0 (cos) and 1 (sin),
+    words (2,3) members 2 and 3; u1 = 1 - U.  Restated in float32 with
+    numpy's log2 / sin / cos: the device's hardware transcendentals agree to
+    a few fp32 ulps, not bit for bit."""
+    i = np.arange(n, dtype=np.uint64)
+    blk = philox_block(seed, stream, i // np.uint64(4))
+    k24 = np.float32(2.0 ** -24)
+    m = (i & np.uint64(3)).astype(np.int64)
+    w1 = np.where(m < 2, blk[:, 0], blk[:, 2])
+    w2 = np.where(m < 2, blk[:, 1], blk[:, 3])
+    u1 = np.float32(1) - (w1 >> np.uint64(8)).astype(np.float32) * k24
+    u2 = (w2 >> np.uint64(8)).astype(np.float32) * k24
+    r = np.sqrt(np.float32(-2 * LN2) * np.log2(u1).astype(np.float32))
+    ang = (np.float32(2 * np.pi) * u2).astype(np.float32)
+    z = np.where(m % 2 == 0, r * np.cos(ang), r * np.sin(ang))
+    return z.astype(np.float32).astype(np.float64)
+
+
 # ---------------------------------------------------------------------------
 # (f3) exact inference: stochastic kernels, stochastic acceptance,
 #      temperature schemes (SURVEY 8(f) rank 3)

@@ -47,6 +47,12 @@ _SIGS = {
     "abc_propose_philox_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                        c_ptr, c_ptr, c_u64, c_u64, c_u64,
                                        c_i64, c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_cdf_index_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr]),
+    "abc_propose_philox_indexed_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr,
+                                               c_ptr, c_int, c_ptr, c_ptr,
+                                               c_ptr, c_u64, c_u64, c_u64,
+                                               c_i64, c_ptr, c_ptr, c_ptr,
+                                               c_ptr]),
     "abc_prior_uniform_f64": (c_int, [c_ptr, c_ptr, c_int, c_u64, c_u64,
                                       c_u64, c_i64, c_ptr, c_ptr]),
     "abc_philox_uniform_f64": (c_int, [c_u64, c_u64, c_u64, c_i64, c_ptr,

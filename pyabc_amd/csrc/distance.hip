@@ -62,7 +62,10 @@ __global__ __launch_bounds__(256) void pnorm_kernel(
 }
 
 // y[s, b] = sum_k A[s, k] theta[b, k] + c[s] + sigma * z(b, s)
-// z(b, s) = philox_normal(seed, sid, (offset + b) * S + s)
+// z(b, s) = fast normal (offset + b) * S + s: block i / 4, member i % 4 of
+// box_muller4_f32 (philox.hpp) -- the fp64 Box-Muller of the proposal
+// streams cost 70 % of this kernel's time, for noise whose precision no
+// statistic resolves
 __global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
     const double* __restrict__ theta, int64_t B, int d,
     const double* __restrict__ A, const double* __restrict__ c, int S,
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
 #pragma unroll
   for (int k = 0; k < 32; ++k) th[k] = k < d ? theta[b * d + k] : 0.0;
   const uint64_t base = (offset + static_cast<uint64_t>(b)) * static_cast<uint64_t>(S);
-  double zpair[2] = {0.0, 0.0};
+  float z4[4] = {0.f, 0.f, 0.f, 0.f};
   uint64_t have = ~0ull;
   for (int s = 0; s < S; ++s) {
     double acc = c ? c[s] : 0.0;
@@ -82,12 +85,12 @@ __global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
     for (int k = 0; k < 32; ++k)
       if (k < d) acc = fma(A[s * d + k], th[k], acc);
     const uint64_t zi = base + s;
-    if ((zi >> 1) != have) {
-      box_muller(philox_block(seed, sid, zi >> 1), zpair[0], zpair[1]);
-      have = zi >> 1;
+    if ((zi >> 2) != have) {
+      box_muller4_f32(philox_block(seed, sid, zi >> 2), z4);
+      have = zi >> 2;
     }
-    const double z = (zi & 1) ? zpair[1] : zpair[0];
-    out_T[static_cast<int64_t>(s) * ld + b] = acc + sigma * z;
+    const double z = static_cast<double>(z4[zi & 3]);
+    out_T[static_cast<int64_t>(s) * ld + b] = fma(sigma, z, acc);
   }
 }
 

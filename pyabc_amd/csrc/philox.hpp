@@ -49,6 +49,26 @@ __host__ __device__ inline double u53(uint32_t hi, uint32_t lo) {
   return static_cast<double>(v) * (1.0 / 9007199254740992.0);
 }
 
+// four normals from one Philox block for the synthetic simulators' noise:
+// 24-bit uniforms from each word (w >> 8) * 2^-24, Box-Muller in fp32 on the
+// transcendental unit (v_log_f32 = log2, v_sin/cos_f32 of revolutions):
+// words (0,1) -> z0 = r cos, z1 = r sin; words (2,3) -> z2, z3, with
+// u1 = 1 - U in (0,1] (|z| <= 5.77).  ~1 fp32 ulp from the exact transform.
+__device__ inline void box_muller4_f32(u32x4 b, float (&z)[4]) {
+  constexpr float k24 = 5.9604644775390625e-08f;  // 2^-24
+  constexpr float kM2Ln2 = -1.3862943611198906f;  // -2 ln 2
+  const float u1a = 1.0f - static_cast<float>(b.x >> 8) * k24;
+  const float u2a = static_cast<float>(b.y >> 8) * k24;
+  const float u1b = 1.0f - static_cast<float>(b.z >> 8) * k24;
+  const float u2b = static_cast<float>(b.w >> 8) * k24;
+  const float ra = __builtin_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u1a));
+  const float rb = __builtin_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u1b));
+  z[0] = ra * __builtin_amdgcn_cosf(u2a);
+  z[1] = ra * __builtin_amdgcn_sinf(u2a);
+  z[2] = rb * __builtin_amdgcn_cosf(u2b);
+  z[3] = rb * __builtin_amdgcn_sinf(u2b);
+}
+
 // pair of normals (cos branch, sin branch) from one Philox block
 __device__ inline void box_muller(u32x4 b, double& z0, double& z1) {
   const double u1 = 1.0 - u53(b.x, b.y);

@@ -425,10 +425,21 @@ __global__ __launch_bounds__(kCdfThreads) void cdf_write_kernel(
 
 static int64_t cdf_tiles(int64_t n) { return ceil_div(n, kCdfTile); }
 
-// first index i with cdf[i] > u (numpy searchsorted side='right')
+// first index i with cdf[i] > u (numpy searchsorted side='right'); with a
+// bucket table (abc_cdf_index_f64: tab[k] = first i with cdf[i] > k / 2^L)
+// the answer lies in [tab[k], tab[k+1]] for k = floor(u 2^L) -- u 2^L is
+// exact -- so the dependent-load chain shrinks from log2 N to the log2 of
+// one bucket (about log2(N / 2^L) steps for spread weights)
 __device__ inline int64_t search_right(const double* __restrict__ cdf, int64_t n,
-                                       double u) {
+                                       double u,
+                                       const int64_t* __restrict__ tab = nullptr,
+                                       int log2k = 0) {
   int64_t lo = 0, hi = n;
+  if (tab) {
+    const int64_t k = static_cast<int64_t>(ldexp(u, log2k));
+    lo = tab[k];
+    hi = tab[k + 1];
+  }
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if (cdf[mid] <= u)
@@ -448,8 +459,10 @@ __device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
                                    const double* __restrict__ scale,
                                    double* __restrict__ theta_row,
                                    int64_t* idx_out, uint8_t* sup_out,
-                                   int64_t a_stride = 0) {
-  int64_t idx = search_right(cdf, N, u);
+                                   int64_t a_stride = 0,
+                                   const int64_t* __restrict__ tab = nullptr,
+                                   int log2k = 0) {
+  int64_t idx = search_right(cdf, N, u, tab, log2k);
   const int64_t idx_c = idx < N ? idx : N - 1;  // numpy would raise; u<1 always
   A += idx_c * a_stride;  // per-particle factor (LocalTransition) or shared
   bool ok = true;
@@ -501,7 +514,7 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
     const double* __restrict__ lo, const double* __restrict__ scale,
     uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
     double* __restrict__ theta, int64_t* __restrict__ idx,
-    uint8_t* __restrict__ sup) {
+    uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint64_t ui = offset + static_cast<uint64_t>(b);
@@ -521,7 +534,16 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
     }
   }
   perturb_one<D>(X, N, d, cdf, u, zz, A, lo, scale, theta + b * d, idx + b,
-                 sup + b);
+                 sup + b, 0, tab, log2k);
+}
+
+// bucket table of the CDF: tab[k] = searchsorted(cdf, k / 2^L, 'right')
+__global__ __launch_bounds__(256) void cdf_index_kernel(
+    const double* __restrict__ cdf, int64_t n, int log2k,
+    int64_t* __restrict__ tab) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (k > (int64_t{1} << log2k)) return;
+  tab[k] = search_right(cdf, n, ldexp(static_cast<double>(k), -log2k));
 }
 
 // prior sampling at t=0: theta = lo + scale * U  (scipy uniform.rvs)
@@ -764,7 +786,45 @@ int abc_propose_philox_f64(const double* X, int64_t N, int d,
 #define L(DD)                                                              \
   hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \
                      X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta, \
-                     idx, in_support);
+                     idx, in_support, nullptr, 0);
+  DISPATCH_D(d, L)
+#undef L
+  ABC_LAUNCH_CHECK("propose_philox_kernel");
+  return kOk;
+}
+
+int abc_cdf_index_f64(const double* cdf, int64_t n, int log2k, int64_t* tab,
+                      hipStream_t st) {
+  ABC_REQUIRE(n > 0 && log2k >= 0 && log2k <= 24, "cdf_index: bad sizes");
+  ABC_REQUIRE(cdf && tab, "cdf_index: null pointer");
+  const int64_t K1 = (int64_t{1} << log2k) + 1;
+  hipLaunchKernelGGL(cdf_index_kernel, dim3(ceil_div(K1, 256)), dim3(256), 0,
+                     st, cdf, n, log2k, tab);
+  ABC_LAUNCH_CHECK("cdf_index_kernel");
+  return kOk;
+}
+
+int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
+                                   const double* cdf, const int64_t* tab,
+                                   int log2k, const double* A,
+                                   const double* lo, const double* scale,
+                                   uint64_t seed, uint64_t sid,
+                                   uint64_t offset, int64_t B, double* theta,
+                                   int64_t* idx, uint8_t* in_support,
+                                   hipStream_t st) {
+  ABC_REQUIRE(check_dim(d), "propose: unsupported d=%d", d);
+  ABC_REQUIRE(N > 0 && B >= 0, "propose: bad sizes");
+  ABC_REQUIRE(log2k >= 0 && log2k <= 24, "propose: bad table size");
+  if (B == 0) return kOk;
+  ABC_REQUIRE(X && cdf && tab && A && theta && idx && in_support,
+              "propose: null pointer");
+  ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
+              "propose: lo and scale must both be given or NULL");
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+#define L(DD)                                                              \
+  hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta, \
+                     idx, in_support, tab, log2k);
   DISPATCH_D(d, L)
 #undef L
   ABC_LAUNCH_CHECK("propose_philox_kernel");

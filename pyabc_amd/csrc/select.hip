@@ -584,7 +584,8 @@ __global__ __launch_bounds__(256) void moments1_final_kernel(const double* __res
   __shared__ double red[4];
   const int nv = 2 + d;
   for (int v = 0; v < nv; ++v) {
-    double s = threadIdx.x < np ? part[threadIdx.x * nv + v] : 0.0;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < np; b += 256) s += part[b * nv + v];
     s = block_sum<double, 256>(s, red);
     if (threadIdx.x == 0) out[v] = s;
   }
@@ -655,6 +656,109 @@ __global__ __launch_bounds__(256) void moments2_final_kernel(const double* __res
     out[2 + d + k * d + l] = s;
     out[2 + d + l * d + k] = s;
   }
+}
+
+// Single-pass register forms for d <= 8 (the benchmark dimensions): every
+// thread walks rows (grid-stride, fixed grid) and keeps all sums in
+// registers -- one read of (X, w) per pass instead of 2 + d column passes
+// (pass 1) and 36-of-256 active threads (pass 2).  Block partials: fixed
+// wave butterfly, then the 4 waves in order; the final kernel adds the
+// kMomGrid partials in block order, so results are deterministic.
+constexpr int kMomGrid = 512;
+
+template <int D, int NV>
+__device__ inline void block_sums_to(double (&v)[NV], double* __restrict__ out,
+                                     double (*lds)[NV]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const double r = wave_sum(v[q]);
+    if (lane == 0) lds[wid][q] = r;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NV; q += blockDim.x)
+    out[q] = ((lds[0][q] + lds[1][q]) + lds[2][q]) + lds[3][q];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void moments1_reg_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    double* __restrict__ part) {
+  constexpr int NV = 2 + D;
+  __shared__ double lds[4][NV];
+  double v[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const double wi = w[i];
+    v[0] += wi;
+    v[1] = fma(wi, wi, v[1]);
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[2 + k] = fma(wi, X[i * D + k], v[2 + k]);
+  }
+  block_sums_to<D, NV>(v, part + static_cast<int64_t>(blockIdx.x) * NV, lds);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void moments2_reg_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    const double* __restrict__ mom, double* __restrict__ part) {
+  constexpr int NP = D * (D + 1) / 2;
+  __shared__ double lds[4][NP];
+  double mu[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) mu[k] = mom[2 + k];
+  double v[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) v[q] = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const double wi = w[i];
+    double xc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xc[k] = X[i * D + k] - mu[k];
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const double a = wi * xc[k];
+#pragma unroll
+      for (int l = k; l < D; ++l) {
+        v[q] = fma(a, xc[l], v[q]);
+        ++q;
+      }
+    }
+  }
+  block_sums_to<D, NP>(v, part + static_cast<int64_t>(blockIdx.x) * NP, lds);
+}
+
+// final sums of the register forms: one wave per value, lane l adds the
+// partials l, l + 64, ... in order, then the fixed butterfly.  pass 1
+// writes [sw, sw2, mu[d]] (mu divided by sw); pass 2 the symmetric C.
+__global__ __launch_bounds__(64) void moments_final_wave_kernel(
+    const double* __restrict__ part, int nb, int nv, int d, int which,
+    double* __restrict__ out) {
+  const int v = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 64) s += part[b * nv + v];
+  s = wave_sum(s);
+  if (threadIdx.x != 0) return;
+  if (which == 1) {
+    out[v] = s;
+  } else {
+    int k = 0, q = v;
+    while (q >= d - k) {
+      q -= d - k;
+      ++k;
+    }
+    const int l = k + q;
+    out[2 + d + k * d + l] = s;
+    out[2 + d + l * d + k] = s;
+  }
+}
+
+__global__ void moments_mu_kernel(double* __restrict__ out, int d) {
+  if (threadIdx.x < d) out[2 + threadIdx.x] = out[2 + threadIdx.x] / out[0];
 }
 
 // w_i = prior_i / exp(logpd_i)   (smc.py:776-792; prior may be a constant)
@@ -918,7 +1022,8 @@ int abc_column_std_f64(const double* data_T, int64_t ld, int64_t n, int S,
 
 size_t abc_moments_workspace_bytes(int d) {
   const int np = d * (d + 1) / 2;
-  return static_cast<size_t>(kRedGrid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
+  const int grid = kMomGrid > kRedGrid ? kMomGrid : kRedGrid;
+  return static_cast<size_t>(grid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
 }
 
 int abc_weighted_moments_f64(const double* X, const double* w, int64_t n, int d,
@@ -928,6 +1033,32 @@ int abc_weighted_moments_f64(const double* X, const double* w, int64_t n, int d,
   ABC_REQUIRE(ws_bytes >= abc_moments_workspace_bytes(d),
               "moments: workspace too small");
   double* part = static_cast<double*>(ws);
+  if (d <= 8) {
+#define L(DD)                                                                    \
+  hipLaunchKernelGGL((moments1_reg_kernel<DD>), dim3(kMomGrid), dim3(256), 0, st, \
+                     X, w, n, part);                                             \
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(2 + DD), dim3(64), 0, st,   \
+                     part, kMomGrid, 2 + DD, DD, 1, out);                        \
+  hipLaunchKernelGGL(moments_mu_kernel, dim3(1), dim3(64), 0, st, out, DD);      \
+  hipLaunchKernelGGL((moments2_reg_kernel<DD>), dim3(kMomGrid), dim3(256), 0, st, \
+                     X, w, n, out, part);                                        \
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(DD * (DD + 1) / 2),         \
+                     dim3(64), 0, st, part, kMomGrid, DD * (DD + 1) / 2, DD, 2,  \
+                     out);
+    switch (d) {
+      case 1: L(1) break;
+      case 2: L(2) break;
+      case 3: L(3) break;
+      case 4: L(4) break;
+      case 5: L(5) break;
+      case 6: L(6) break;
+      case 7: L(7) break;
+      case 8: L(8) break;
+    }
+#undef L
+    ABC_LAUNCH_CHECK("moments kernels");
+    return kOk;
+  }
   hipLaunchKernelGGL(moments1_kernel, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
                      d, part);
   hipLaunchKernelGGL(moments1_final_kernel, dim3(1), dim3(256), 0, st, part,

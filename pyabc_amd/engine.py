@@ -88,20 +88,24 @@ class DeviceMVNFit:
         self.packed = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
                                          precision)
         self._cdf = None
+        self._tab = None
 
     @property
     def cdf(self):
         if self._cdf is None:
             self._cdf = K.resample_cdf(self.w)
+            self._tab = K.cdf_index(self._cdf)
         return self._cdf
 
     def logpdf(self, theta):
         return self.packed.logpdf(theta)
 
     def propose(self, lo, scale, seed, sid, offset, B):
-        """B draws of resample + perturb + support flag (Philox)."""
-        return K.propose_philox(self.X, self.cdf, self.A, lo, scale, seed,
-                                sid, offset, B)
+        """B draws of resample + perturb + support flag (Philox); the CDF
+        search is bracketed by the bucket table (same indices)."""
+        cdf = self.cdf
+        return K.propose_philox(self.X, cdf, self.A, lo, scale, seed, sid,
+                                offset, B, tab=self._tab)
 
 
 def selection_plan(nvs, nas, n):

@@ -86,7 +86,21 @@ def resample_perturb(X, cdf, u, z, A, lo=None, scale=None):
     return theta, idx, sup
 
 
-def propose_philox(X, cdf, A, lo, scale, seed, sid, offset, B, out=None):
+CDF_INDEX_LOG2 = 16
+
+
+def cdf_index(cdf, log2k=CDF_INDEX_LOG2):
+    """Bucket table tab[k] = searchsorted(cdf, k / 2^log2k, 'right')."""
+    tab = torch.empty((1 << log2k) + 1, dtype=torch.int64, device=_dev())
+    call("abc_cdf_index_f64", ptr(_contig(cdf, F64)), cdf.numel(), log2k,
+         ptr(tab), nat.stream())
+    return tab
+
+
+def propose_philox(X, cdf, A, lo, scale, seed, sid, offset, B, out=None,
+                   tab=None):
+    """Resample + perturb + support flag for B Philox proposals; ``tab``
+    (:func:`cdf_index`) brackets the CDF search (same indices)."""
     X = _contig(X, F64)
     N, d = X.shape
     if out is None:
@@ -95,6 +109,12 @@ def propose_philox(X, cdf, A, lo, scale, seed, sid, offset, B, out=None):
         sup = torch.empty(B, dtype=torch.uint8, device=_dev())
     else:
         theta, idx, sup = out
+    if tab is not None:
+        log2k = (tab.numel() - 1).bit_length() - 1
+        call("abc_propose_philox_indexed_f64", ptr(X), N, d, ptr(cdf),
+             ptr(tab), log2k, ptr(A), ptr(lo), ptr(scale), seed, sid, offset,
+             B, ptr(theta), ptr(idx), ptr(sup), nat.stream())
+        return theta, idx, sup
     call("abc_propose_philox_f64", ptr(X), N, d, ptr(cdf), ptr(A), ptr(lo),
          ptr(scale), seed, sid, offset, B, ptr(theta), ptr(idx), ptr(sup),
          nat.stream())

@@ -95,6 +95,44 @@ def test_config2_adaptive_mad_batch_path(pa):
     _check_against_reference(g, "c2", 3, eps, _post_stats(h, names), d)
 
 
+def test_config2_full_size_N1e5(pa):
+    """C2 at its BASELINE size (N = 1e5, one MI355X): AdaptivePNormDistance
+    (MAD), QuantileEpsilon(0.5), 4 generations.  The reference cannot run
+    N = 1e5 here; the pins are its N = 1000 runs (tests/golden/e2e_stats.npz),
+    whose epsilon and acceptance sequence depend on N only through Monte
+    Carlo error: per generation the epsilon within 2 % and the evaluations
+    per particle within 10 % of the reference mean, the final posterior mean
+    within 0.1 and sd within 10 % of the reference's."""
+    g = load_golden("e2e_stats")
+    A, x0v = g["A2"], g["x0_2"]
+    S, d = A.shape
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k}" for k in range(d)]
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    sampler = pa.GPUBatchSampler(seed=21)
+    abc = pa.ABCSMC(model, prior,
+                    pa.AdaptivePNormDistance(
+                        p=2, scale_function=pa.median_absolute_deviation),
+                    population_size=100_000,
+                    eps=pa.QuantileEpsilon(alpha=0.5), sampler=sampler)
+    abc.new("mem://c2_full", dict(zip(keys, x0v)))
+    h = abc.run(max_nr_populations=4)
+    assert all(e["batch"] for e in abc.generation_log), sampler.fallback_reason
+    eps = _eps(h)
+    ref_eps = np.array([g[f"c2_eps_{r}"] for r in range(3)]).mean(0)
+    np.testing.assert_allclose(eps[:4], ref_eps, rtol=0.02)
+    pops = h.get_all_populations()
+    per = pops[pops.t >= 0].samples.values / 100_000
+    ref_per = np.array([g[f"c2_nsim_{r}"] for r in range(3)]).mean(0) / 1000
+    np.testing.assert_allclose(per[:4], ref_per, rtol=0.1)
+    m, s = _post_stats(h, names)[3]
+    ref_m = np.array([g[f"c2_mean_{r}"][-1] for r in range(3)]).mean(0)
+    ref_s = np.array([g[f"c2_std_{r}"][-1] for r in range(3)]).mean(0)
+    np.testing.assert_array_less(np.abs(m - ref_m), 0.1)
+    np.testing.assert_allclose(s, ref_s, rtol=0.1)
+
+
 def test_closure_path_python_model(pa):
     """A plain Python model cannot be batched: the sampler calls the closure
     per proposal; transitions / distances still compute on the device."""

@@ -178,3 +178,14 @@ def test_philox_streams_statistics():
     assert abs(u.mean() - 0.5) < 5e-3
     z = ref.philox_normal(1234, 7, 200000)
     assert abs(z.mean()) < 1e-2 and abs(z.std() - 1) < 1e-2
+
+
+def test_philox_normal4_f32_distribution():
+    """The synthetic simulators' fp32 Box-Muller stream is standard normal
+    (moments, tails, pairwise independence of the members of one block)."""
+    z = ref.philox_normal4_f32(99, 4, 400_000)
+    assert abs(z.mean()) < 0.005 and abs(z.std() - 1) < 0.005
+    assert np.abs(z).max() <= 5.8
+    q = z.reshape(-1, 4)
+    c = np.corrcoef(q.T)
+    assert np.all(np.abs(c - np.eye(4)) < 0.01)

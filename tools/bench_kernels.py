@@ -135,6 +135,11 @@ def main():
     # in-kernel Philox: cdf hit 8 + X[idx] 8d + theta 8d + idx 8 + flag 1
     report("propose_philox_f64", t, B, "proposals", 16 * d + 17, "hbm",
            {"N": N, "d": d})
+    tab = K.cdf_index(cdf)
+    t = timed(lambda: K.propose_philox(fit.X, cdf, fit.A, lo, sc, 1, 2, 0, B,
+                                       out=out, tab=tab))
+    report("propose_philox_indexed_f64", t, B, "proposals", 16 * d + 17,
+           "hbm", {"N": N, "d": d, "log2k": K.CDF_INDEX_LOG2})
     vpos, _ = K.compact(out[2])
     t = timed(lambda: K.compact(out[2], vpos))
     report("compact_flags", t, B, "flags", 1 + 8, "hbm")

@@ -118,22 +118,23 @@ if __name__ == "__main__":
             mu = torch.zeros(d, dtype=torch.float64, device="cuda")
             pp = K.PackedPopulation(X, w, mu, Us, rank, lpd, "mfma")
             return pp.logpdf(X[:M] + 0.05)
-        variants = [("base", {}), ("sched", {"ABC_KDE_MFMA_SCHED": "1"}),
-                    ("sw", {"ABC_KDE_MFMA_SW": "1"}),
-                    ("sw-ibh", {"ABC_KDE_MFMA_SW": "1", "ABC_KDE_MFMA_IB": "h"})]
+        variants = [("base", {}), ("nosched", {"ABC_KDE_MFMA_SCHED": "0"}),
+                    ("dma", {"ABC_KDE_MFMA_DMA": "1"})]
         dims = [int(x) for x in sys.argv[2:]] or [8, 20, 4]
         for d in dims:
             ib = {8: "1", 20: "1", 4: "1"}.get(d, "1")
             outs = {}
             for name, env in variants:
                 for k in ("ABC_KDE_MFMA_SCHED", "ABC_KDE_MFMA_SW",
-                          "ABC_KDE_MFMA_IB"):
+                          "ABC_KDE_MFMA_IB", "ABC_KDE_MFMA_DMA"):
                     os.environ.pop(k, None)
                 for k, v in env.items():
                     os.environ[k] = ib if v == "h" else v
                 outs[name] = rows(20000, 5000, d).cpu().numpy()
                 print(f"d {d} {name}:", end=" ")
                 N = {8: 1000000, 20: 262144, 4: 100000}.get(d, 262144)
+                if os.environ.get("KDE_QUICK"):
+                    N = min(N, 262144)
                 run(N, N, d, "mfma", reps=3)
             for k, v in outs.items():
                 print(f"  d {d} {k} bit-identical: "

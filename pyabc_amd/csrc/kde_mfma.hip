@@ -499,6 +499,85 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
   }
 }
 
+// Occupancy form for large d (MFMA-bound): one i-tile per wave, the A
+// fragments of each 64-row chunk copied once per block into LDS by LDS-DMA
+// (global_load_lds_dwordx4, no staging registers; double-buffered, one
+// barrier per chunk) and read back one fragment ahead of its MFMA (sched
+// groups DS_READ 1 / MFMA 1), so a wave holds only its B fragments, one
+// accumulator pair and the exp block: three waves per SIMD at d = 20
+// instead of one, and the MFMA chain of one wave runs beside the VALU of
+// another.  Per-lane arithmetic and order are those of kde_mfma_kernel at
+// IB = 1: rows are bit-identical.
+template <int KH, int KL>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_dma_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = rb * kWaves + wave;
+
+  bf16x8 bq[KT];
+#pragma unroll
+  for (int c = 0; c < KT; ++c) bq[c] = Bfr[(t0 * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S = 0.0;
+    // fragment f of a chunk = (tile f / KT, slot chunk f % KT): contiguous
+    // 1 KiB at Aseg + (chunk * 2 * KT + f) * 64; wave w copies f = w, w+4..
+    auto fill = [&](int buf, int jc) {
+      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+      for (int f = wave; f < CH; f += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            src + f * 64 + lane,
+            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+    };
+    __syncthreads();  // the previous segment's readers are done with As
+    if (nj > 0) fill(0, 0);
+    int buf = 0;
+    for (int jc = 0; jc < nj; jc += 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // chunk jc landed (every wave waited for its own pieces) and every
+      // wave finished chunk jc - 64, whose buffer is refilled next
+      __syncthreads();
+      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      float sacc = 0.0f;
+#pragma unroll
+      for (int tile = 0; tile < 2; ++tile) {
+        f32x16 hi = f32x16{}, lo = f32x16{};
+#pragma unroll
+        for (int c = 0; c < KH; ++c) {
+          hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(As[buf][tile * KT + c][lane],
+                                                       bq[c], hi, 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < KL; ++c) {
+          lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              As[buf][tile * KT + KH + c][lane], bq[KH + c], lo, 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        sacc += tile_sum(hi, lo);
+      }
+      S += static_cast<double>(sacc);
+      buf ^= 1;  // the next top barrier also ends every read of this buffer
+    }
+    const double tot = S + __shfl_xor(S, 32, 64);
+    const int64_t i = t0 * 32 + lane;
+    if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+  }
+}
+
 // The same pass with the A fragments of each 64-row chunk staged once per
 // block in LDS (double-buffered) and shared by the kWaves waves, which walk
 // the same j-segments.  Where the register version needs more than 256
@@ -700,6 +779,9 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   if (const char* env = getenv("ABC_KDE_MFMA_IB")) {
     if (atoi(env) == IBH) ib = IBH;
   }
+  bool dma = false;
+  if (const char* env = getenv("ABC_KDE_MFMA_DMA")) dma = atoi(env) != 0;
+  if (dma) ib = 1;
   const MPlan p = make_mplan<D>(M, npad, ib);
   const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
@@ -710,7 +792,12 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.nseg * M) * 8);
   int* fix_rows = n_fix + 4;
   ABC_HIP(hipMemsetAsync(n_fix, 0, 16, st));
-  if (ib == IBF)
+  if (dma)
+    hipLaunchKernelGGL((kde_mfma_dma_kernel<Mk<D>::KH, Mk<D>::KL>),
+                       dim3(static_cast<unsigned>(p.row_blocks * p.split)),
+                       dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,
+                       p.spb, p.jseg, partial);
+  else if (ib == IBF)
     launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, st);
   else
     launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, st);

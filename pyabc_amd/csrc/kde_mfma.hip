@@ -54,6 +54,9 @@ struct Mk {
   static constexpr int KL = (7 * D + 4 + 15) / 16;  // 7 cross terms, aL, bL
   static constexpr int KT = KH + KL;
   static constexpr int IB = D <= 8 ? 3 : (D <= 24 ? 2 : 1);  // i-tiles/wave
+  // row padding unit in i-tiles per wave: every IB the launch may pick
+  // (1, 2, 3 at D <= 8) divides it
+  static constexpr int PADIB = D <= 8 ? 6 : IB;
 };
 
 __device__ inline unsigned short bf16_rne(float x) {
@@ -309,12 +312,69 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
   return e[0];
 }
 
+// Ablation forms of one step (tuning diagnostics only, ABC_KDE_MFMA_ABL):
+// 1 no exp, 2 no MFMA, 3 neither (adds only), 4 MFMA only.  The results are
+// meaningless; they time the pipes separately.
+template <int ABL, int KH, int KL>
+__device__ __forceinline__ void abl_step(const bf16x8* a, const bf16x8* b,
+                                         f32x16& hi, f32x16& lo) {
+  if constexpr (ABL == 5) {
+    // fold: the lo chain first, then the exact hi products on top of it as
+    // the MFMA's C operand (accuracy probe; saves the VALU hi + lo add)
+    lo = f32x16{};
+#pragma unroll
+    for (int c = 0; c < KL; ++c)
+      lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0, 0, 0);
+    hi = lo;
+#pragma unroll
+    for (int c = 0; c < KH; ++c)
+      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
+  } else if constexpr (ABL == 2 || ABL == 3) {
+    asm volatile("" : "+v"(hi), "+v"(lo));
+  } else {
+    mfma_step<KH, KL>(a, b, hi, lo);
+  }
+}
+// (the ablated sum is consumed by an empty asm and replaced by 1, so no row
+// reaches the exact fixup)
+template <int ABL>
+__device__ __forceinline__ float abl_sum(const f32x16& hi, const f32x16& lo) {
+  if constexpr (ABL == 0) return tile_sum(hi, lo);
+  if constexpr (ABL == 5) {
+    float e[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int v = 0; v < w; ++v) e[v] += e[v + w];
+    return e[0];
+  }
+  float r;
+  if constexpr (ABL == 2) {
+    r = tile_sum(hi, lo);
+  } else if constexpr (ABL == 4) {
+    r = hi[0] + lo[0];
+  } else {
+    float e[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) e[v] = hi[v] + lo[v];
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int v = 0; v < w; ++v) e[v] += e[v + w];
+    r = e[0];
+  }
+  asm volatile("" ::"v"(r));
+  return 1.0f;
+}
+
 // main pass.  Block (rb, s): wave w owns i-tiles (rb*kWaves + w)*IB + t and
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB, bool PIPE, bool SCHED = false>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
+template <int KH, int KL, int IB, bool PIPE, bool SCHED, int ABL = 0>
+__device__ __forceinline__ void kde_mfma_body(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
@@ -361,17 +421,17 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
 #pragma unroll
         for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
         f32x16 hi[2], lo[2];
-        mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+        abl_step<ABL, KH, KL>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           if (q + 1 < 2 * IB)
-            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+            abl_step<ABL, KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
                               hi[(q + 1) & 1], lo[(q + 1) & 1]);
           if (q + 1 == IB) {  // last MFMA reading tile 0 is issued
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+          sacc[q % IB] += abl_sum<ABL>(hi[q & 1], lo[q & 1]);
           if constexpr (SCHED) {
             // interleave: each MFMA of step q+1 followed by a share of step
             // q's 48 VALU (16 add, 16 exp, 16 tree/row adds)
@@ -393,8 +453,8 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
-          mfma_step<KH, KL>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += tile_sum(hi, lo);
+          abl_step<ABL, KH, KL>(a[q / IB], bq[q % IB], hi, lo);
+          sacc[q % IB] += abl_sum<ABL>(hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -411,6 +471,22 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
       if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
     }
   }
+}
+
+template <int KH, int KL, int IB, bool PIPE, bool SCHED = false>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  kde_mfma_body<KH, KL, IB, PIPE, SCHED>(Bfr, M, Afr, npad, split, spb, jseg,
+                                         partial);
+}
+
+template <int KH, int KL, int ABL>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_abl_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  kde_mfma_body<KH, KL, 3, true, true, ABL>(Bfr, M, Afr, npad, split, spb,
+                                            jseg, partial);
 }
 
 // The same pass software-pipelined ACROSS 64-row chunks: the MFMAs of step
@@ -489,6 +565,102 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
 #pragma unroll
         for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
       }
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
+// L1-relief form: the A fragments of each 64-row chunk are copied ONCE per
+// block into LDS by LDS-DMA (global_load_lds_dwordx4: no staging registers,
+// double-buffered, one barrier per chunk) and every wave of the block reads
+// them from LDS (128 B/clk/CU) instead of each wave pulling its own 10 KiB
+// per chunk through the vector L1 (64 B/clk/CU: the MFMA path alone ran
+// 114 ms at N = M = 1e6, d = 8, L1-bound, tools/kde_variants.py ablations).
+// NW waves per block share one copy; each keeps IB i-tiles of B in
+// registers.  Per-lane arithmetic and summation order are those of
+// kde_mfma_body: rows are bit-identical.
+template <int KH, int KL, int IB, int NW, bool SCHED>
+__global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * NW + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    // fragment f of a chunk = contiguous 1 KiB at Aseg + (chunk*2*KT + f)*64
+    auto fill = [&](int buf, int jc) {
+      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+      for (int f = wave; f < CH; f += NW)
+        __builtin_amdgcn_global_load_lds(
+            src + f * 64 + lane,
+            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+    };
+    __syncthreads();  // the previous segment's readers are done with As
+    if (nj > 0) fill(0, 0);
+    int buf = 0;
+    for (int jc = 0; jc < nj; jc += 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // chunk jc landed (each wave waited for its own pieces) and every wave
+      // is done with chunk jc - 64, whose buffer is refilled now
+      __syncthreads();
+      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      const bf16x8(*Ab)[64] = As[buf];
+      float sacc[IB];
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+      bf16x8 a[2][KT];
+#pragma unroll
+      for (int c = 0; c < KT; ++c) a[0][c] = Ab[c][lane];
+#pragma unroll
+      for (int c = 0; c < KT; ++c) a[1][c] = Ab[KT + c][lane];
+      f32x16 hi[2], lo[2];
+      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+#pragma unroll
+      for (int q = 0; q < 2 * IB; ++q) {
+        if (q + 1 < 2 * IB)
+          mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+                            hi[(q + 1) & 1], lo[(q + 1) & 1]);
+        sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+        if constexpr (SCHED) {
+          constexpr int VPG = (48 + KT - 1) / KT;
+          if (q + 1 < 2 * IB) {
+#pragma unroll
+            for (int m = 0; m < KT; ++m) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
+            }
+          } else {
+            __builtin_amdgcn_sched_group_barrier(0x002, 48, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+      buf ^= 1;
     }
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
@@ -674,7 +846,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_kernel(
 
 template <int D>
 int64_t mpad_rows(int64_t M) {
-  constexpr int rows = 32 * kWaves * Mk<D>::IB;
+  constexpr int rows = 32 * kWaves * Mk<D>::PADIB;
   return ceil_div(M, rows) * rows;
 }
 
@@ -744,6 +916,42 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if (const char* env = getenv("ABC_KDE_MFMA_SCHED")) sched = atoi(env) != 0;
   bool sw = false;
   if (const char* env = getenv("ABC_KDE_MFMA_SW")) sw = atoi(env) != 0;
+  int dmab = 0;  // LDS-DMA shared A: 1 = 4 waves per block, 2 = 8 waves
+  if (const char* env = getenv("ABC_KDE_MFMA_DMAB")) dmab = atoi(env);
+  if constexpr (D <= 8) {
+    if (dmab == 1 || dmab == 2) {
+#define DMAB(NW, SC)                                                           \
+  hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, NW, SC>),  \
+                     dim3(grid / (NW / kWaves)), dim3(64 * NW), 0, st, Bfr, M, \
+                     Afr, npad, p.split, p.spb, p.jseg, partial)
+      if (dmab == 2 && (p.row_blocks & 1) == 0) {
+        if (sched) DMAB(8, true);
+        else DMAB(8, false);
+      } else {  // 8-wave blocks need an even row-block count
+        if (sched) DMAB(4, true);
+        else DMAB(4, false);
+      }
+#undef DMAB
+      return;
+    }
+  }
+  if constexpr (D == 8 && IB == 3) {
+    int abl = 0;
+    if (const char* env = getenv("ABC_KDE_MFMA_ABL")) abl = atoi(env);
+    if (abl >= 1 && abl <= 5) {
+#define ABLK(A)                                                                \
+  hipLaunchKernelGGL((kde_mfma_abl_kernel<Mk<D>::KH, Mk<D>::KL, A>), dim3(grid), \
+                     dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,     \
+                     p.spb, p.jseg, partial)
+      if (abl == 1) ABLK(1);
+      else if (abl == 5) ABLK(5);
+      else if (abl == 2) ABLK(2);
+      else if (abl == 3) ABLK(3);
+      else ABLK(4);
+#undef ABLK
+      return;
+    }
+  }
   if (sw)
     hipLaunchKernelGGL((kde_mfma_sw_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
                        dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
@@ -775,9 +983,11 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   // (tuning override ABC_KDE_MFMA_IB); a row's arithmetic is the same
   constexpr int IBF = Mk<D>::IB;
   constexpr int IBH = IBF > 1 ? IBF / 2 : 1;
+  constexpr int IB2 = IBF == 3 ? 2 : IBF;  // the third choice at D <= 8
   int ib = IBF;
   if (const char* env = getenv("ABC_KDE_MFMA_IB")) {
-    if (atoi(env) == IBH) ib = IBH;
+    const int v = atoi(env);
+    if (v == IBH || v == IB2) ib = v;
   }
   bool dma = false;
   if (const char* env = getenv("ABC_KDE_MFMA_DMA")) dma = atoi(env) != 0;
@@ -799,6 +1009,8 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
                        p.spb, p.jseg, partial);
   else if (ib == IBF)
     launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, st);
+  else if (ib == IB2)
+    launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, partial, st);
   else
     launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, st);
   ABC_LAUNCH_CHECK("kde_mfma_kernel");

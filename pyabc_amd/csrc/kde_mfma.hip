@@ -584,7 +584,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
 // NW waves per block share one copy; each keeps IB i-tiles of B in
 // registers.  Per-lane arithmetic and summation order are those of
 // kde_mfma_body: rows are bit-identical.
-template <int KH, int KL, int IB, int NW, bool SCHED>
+template <int KH, int KL, int IB, int NW, bool SCHED, int ABL = 0>
 __global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -638,13 +638,13 @@ __global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
 #pragma unroll
       for (int c = 0; c < KT; ++c) a[1][c] = Ab[KT + c][lane];
       f32x16 hi[2], lo[2];
-      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+      abl_step<ABL, KH, KL>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
       for (int q = 0; q < 2 * IB; ++q) {
         if (q + 1 < 2 * IB)
-          mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+          abl_step<ABL, KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
                             hi[(q + 1) & 1], lo[(q + 1) & 1]);
-        sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+        sacc[q % IB] += abl_sum<ABL>(hi[q & 1], lo[q & 1]);
         if constexpr (SCHED) {
           constexpr int VPG = (48 + KT - 1) / KT;
           if (q + 1 < 2 * IB) {
@@ -924,6 +924,22 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, NW, SC>),  \
                      dim3(grid / (NW / kWaves)), dim3(64 * NW), 0, st, Bfr, M, \
                      Afr, npad, p.split, p.spb, p.jseg, partial)
+      int abl = 0;
+      if (const char* env = getenv("ABC_KDE_MFMA_ABL")) abl = atoi(env);
+      if (abl == 4) {  // MFMA + LDS-DMA only (diagnostic)
+        hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, 4,
+                                                 false, 4>),
+                           dim3(grid), dim3(256), 0, st, Bfr, M, Afr, npad,
+                           p.split, p.spb, p.jseg, partial);
+        return;
+      }
+      if (abl == 2) {  // exp + adds only (diagnostic)
+        hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, 4,
+                                                 false, 2>),
+                           dim3(grid), dim3(256), 0, st, Bfr, M, Afr, npad,
+                           p.split, p.spb, p.jseg, partial);
+        return;
+      }
       if (dmab == 2 && (p.row_blocks & 1) == 0) {
         if (sched) DMAB(8, true);
         else DMAB(8, false);

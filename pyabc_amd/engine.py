@@ -353,12 +353,14 @@ class GenerationEngine:
         n_acc = 0
         raw_off = 0
         eval_off = 0
+        # SingleCoreSampler starts evaluation k (1-based) iff k - 1 <
+        # max_eval: at most ceil(max_eval) evaluations (singlecore.py:24-30)
+        cap = math.ceil(max_eval) if math.isfinite(max_eval) else math.inf
         while n_acc < n:
-            if eval_off >= max_eval:
+            if eval_off >= cap:
                 tm["propose_sim_dist"] = time.perf_counter() - t0
                 self.timers = tm
-                return GenerationResult(ok=False, n_eval=int(min(eval_off,
-                                                                max_eval)))
+                return GenerationResult(ok=False, n_eval=int(cap))
             need = n - n_acc
             B_glob = int(min(self.max_batch * R, max(
                 self.min_batch,
@@ -460,6 +462,12 @@ class GenerationEngine:
                                       last, dtype=F64, device=self.dev))
                 n_guard += int(rd["guard"][:last].sum().item())
         n_eval, n_guard = comm.all_reduce_ints([n_eval_loc, n_guard])
+        if n_eval > cap:
+            # the n-th acceptance lies past the evaluation cap: the reference
+            # stops at cap evaluations without it (sample.ok = False)
+            tm["select"] = time.perf_counter() - t0 - tm["propose_sim_dist"]
+            self.timers = tm
+            return GenerationResult(ok=False, n_eval=int(cap))
         take_counts = [[tk[s] for tk in takes] for s in range(R)]
         theta_acc = self._gather(th_loc, (self.d,), take_counts)
         d_acc = self._gather(d_loc, (), take_counts)

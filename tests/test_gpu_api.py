@@ -486,3 +486,50 @@ def test_config5_full_size_10_generations(pa):
           f"{err9:.3f}, sd {st[0][1].mean():.3f} -> {st[9][1].mean():.3f}")
     assert err9 < err0, (err0, err9)
     assert np.all(st[9][1] < st[0][1])
+
+
+def test_singlecore_parity_same_draws(pa):
+    """a9: the device generation equals the reference's SingleCoreSampler
+    driving the reference's own generation closure over the SAME draws
+    (tests/golden/gen_singlecore_replay.py): population rows and their
+    order, distances, importance weights, ``nr_evaluations_``, every
+    recorded evaluation (record_rejected) with its accept flag, and the
+    check_max_eval cut (singlecore.py:19-38, smc.py:543-794)."""
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.engine import DeviceMVNFit, GenerationEngine
+    g = load_golden("singlecore_replay")
+    dev = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64),
+                                    device="cuda")
+    model = LinearGaussianModel(g["A"], g["c"], float(g["sigma"]))
+    S = g["A"].shape[0]
+    n, t = int(g["n"]), int(g["t"])
+    for min_batch in (64, 4096):   # many rounds / one round: same result
+        eng = GenerationEngine(model, g["lo"], g["sc"], seed=int(g["seed"]),
+                               min_batch=min_batch)
+        fit = DeviceMVNFit(dev(g["X"]), dev(g["w"]))
+        np.testing.assert_allclose(fit.cov, g["cov"], rtol=1e-12)
+        res = eng.sample_generation(t, n, fit, dev(g["x0"]), dev(np.ones(S)),
+                                    float(g["eps"]), keep_stats=True,
+                                    record=True, record_particles=True)
+        assert res.ok and res.n_eval == int(g["nr_evaluations"])
+        np.testing.assert_allclose(res.theta.cpu().numpy(), g["theta"],
+                                   rtol=0, atol=1e-12)
+        # statistics carry the simulator's fp32 Box-Muller noise (a few
+        # fp32 ulps from the oracle's restatement the reference ran on)
+        np.testing.assert_allclose(res.d.cpu().numpy(), g["d"], rtol=1e-5)
+        w = res.w.cpu().numpy()
+        np.testing.assert_allclose(w / w.sum(), g["weight"] / g["weight"].sum(),
+                                   rtol=1e-5)
+        np.testing.assert_allclose(res.rec_stats_T.cpu().numpy().T,
+                                   g["rec_stats"], rtol=0, atol=1e-5)
+        np.testing.assert_array_equal(res.rec_acc.cpu().numpy() > 0,
+                                      g["rec_acc"])
+    for me, ok, nr in zip(g["cut_max_eval"], g["cut_ok"],
+                          g["cut_nr_evaluations"]):
+        eng = GenerationEngine(model, g["lo"], g["sc"], seed=int(g["seed"]),
+                               min_batch=64)
+        fit = DeviceMVNFit(dev(g["X"]), dev(g["w"]))
+        res = eng.sample_generation(t, n, fit, dev(g["x0"]), dev(np.ones(S)),
+                                    float(g["eps"]), max_eval=float(me))
+        assert bool(res.ok) == bool(ok) and res.n_eval == int(nr), (me, res.ok,
+                                                                  res.n_eval)

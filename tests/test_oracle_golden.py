@@ -189,3 +189,39 @@ def test_philox_normal4_f32_distribution():
     q = z.reshape(-1, 4)
     c = np.corrcoef(q.T)
     assert np.all(np.abs(c - np.eye(4)) < 0.01)
+
+
+def test_singlecore_replay_fixture():
+    """The a9 fixture (tests/golden/gen_singlecore_replay.py): the oracle's
+    restatement of the device draws, decided by the oracle's distance and
+    acceptance and cut at the n-th acceptance, gives the reference's
+    population, evaluation count, recorded set and weights."""
+    g = load_golden("singlecore_replay")
+    X, w, cov = g["X"], g["w"], g["cov"]
+    d, S, n, seed, t = X.shape[1], g["A"].shape[0], int(g["n"]), \
+        int(g["seed"]), int(g["t"])
+    np.testing.assert_allclose(ref.mvn_fit_cov(X, w), cov, rtol=1e-13)
+    P = 3000
+    sid = 8 * t
+    u = ref.philox_uniform(seed, 2 * sid, P)
+    z = ref.philox_normal(seed, 2 * sid + 1, P * d).reshape(P, d)
+    _, th = ref.resample_perturb(X, w, cov, u, z)
+    valid = th[ref.uniform_box_support(th, g["lo"], g["sc"])]
+    E = valid.shape[0]
+    noise = ref.philox_normal4_f32(seed, 2 * (sid + 1), E * S).reshape(E, S)
+    stats = valid @ g["A"].T + g["c"] + g["sigma"] * noise.astype(np.float64)
+    dist = ref.pnorm_distance(stats, g["x0"], np.ones(S), 2.0)
+    acc = ref.accept(dist, float(g["eps"]))
+    n_eval = int(np.flatnonzero(acc)[n - 1]) + 1
+    assert n_eval == int(g["nr_evaluations"])
+    np.testing.assert_array_equal(acc[:n_eval], g["rec_acc"])
+    np.testing.assert_allclose(stats[:n_eval], g["rec_stats"], rtol=1e-15,
+                               atol=1e-15)
+    np.testing.assert_array_equal(valid[acc][:n], g["theta"])
+    np.testing.assert_allclose(dist[acc][:n], g["d"], rtol=1e-13)
+    prior = ref.uniform_box_pdf(g["theta"], g["lo"], g["sc"])
+    wt = ref.importance_weight(prior, ref.kde_transition_pd(g["theta"], X, w,
+                                                            cov))
+    # the accepted Population normalises its weights (population.py:120-142)
+    wn, _ = ref.normalize_population_weights(wt)
+    np.testing.assert_allclose(wn, g["weight"], rtol=1e-12)

@@ -181,7 +181,7 @@ def main():
     dist = comm.all_gather_rows(d0)
     w = torch.full((theta.shape[0],), 1.0 / theta.shape[0],
                    dtype=torch.float64, device="cuda")
-    eps = float(K.weighted_quantile(dist, w, 0.5)[0].item())
+    eps = float(K.weighted_quantile(dist, w, 0.5, comm=comm)[0].item())
     fit = DeviceMVNFit(theta, w)
 
     # the CPU leg reruns up to 4 evenly spaced timed generations; their fits
@@ -200,7 +200,8 @@ def main():
             state["k"] += 1
         res = eng.sample_generation(t, N, state["fit"], x0, fw, state["eps"])
         th, dd, ww, n_eval, _ = eng.gather_population(res)
-        state["eps"] = float(K.weighted_quantile(dd, ww, 0.5)[0].item())
+        state["eps"] = float(K.weighted_quantile(dd, ww, 0.5,
+                                                 comm=comm)[0].item())
         state["fit"] = DeviceMVNFit(th, ww)
         state["n_eval"] = n_eval
         state["t"] = t + 1

@@ -214,6 +214,22 @@ size_t abc_wquantile_workspace_bytes(void);
 int abc_wquantile_f64(const double* d, const double* w, int64_t n,
                       double alpha, double* out4, void* ws, size_t ws_bytes,
                       hipStream_t stream);
+/* The same select as exchangeable steps, for a population sharded over
+ * ranks ("the multi-GPU variant exposes its histogram pass so
+ * RCCL can all-reduce between passes"; 8(e) epsilon).  Each rank runs the
+ * step sequence 0, 1, 2, 3, 10, 20, 11, 21, ..., 17, 27, 30, 31, 32 on its
+ * rows (n_local of n_total); after a step, abc_wquantile_exchange names the
+ * words of ws to all-reduce across ranks before the next step (offset in
+ * bytes, count of int64 words, op 1 = sum, 2 = max, 3 = min, 4 = max of the
+ * first word and min of the second).  Every exchanged word is an integer
+ * (fixed-point masses, keys), so the result is bit-identical for any rank
+ * count and equals abc_wquantile_f64 on the whole population. */
+int abc_wquantile_step_f64(int step, const double* d, const double* w,
+                           int64_t n_local, int64_t n_total, double alpha,
+                           double* out4, void* ws, size_t ws_bytes,
+                           hipStream_t stream);
+int abc_wquantile_exchange(int step, int64_t* offset_bytes, int64_t* count,
+                           int* op);
 
 /* ---------------- (a8) LocalTransition -----------------------------------
  * Replaces cKDTree(X).query(X, k+1)                 local_transition.py:82-83

@@ -117,6 +117,9 @@ _SIGS = {
     "abc_wquantile_workspace_bytes": (c_size, []),
     "abc_wquantile_f64": (c_int, [c_ptr, c_ptr, c_i64, c_dbl, c_ptr, c_ptr,
                                   c_size, c_ptr]),
+    "abc_wquantile_step_f64": (c_int, [c_int, c_ptr, c_ptr, c_i64, c_i64,
+                                       c_dbl, c_ptr, c_ptr, c_size, c_ptr]),
+    "abc_wquantile_exchange": (c_int, [c_int, c_ptr, c_ptr, c_ptr]),
     # (a8)
     "abc_knn_workspace_bytes": (c_size, [c_i64, c_int]),
     "abc_knn_f64": (c_int, [c_ptr, c_i64, c_int, c_int, c_ptr, c_ptr, c_ptr,

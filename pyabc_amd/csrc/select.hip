@@ -17,12 +17,13 @@
 //   pyabc/transition/util.py:4-15), deterministic block partials.
 // * deterministic sums and the importance weight prior / transition
 //   (pyabc/smc.py:776-792).
+#include <cstddef>
+
 #include "common.hpp"
 
 namespace abc {
 
 constexpr int kBins = 256;
-constexpr double kFix = 4611686018427387904.0;  // 2^62
 
 // ---------------------------------------------------------------------------
 // deterministic sums (fixed grid + ordered final reduce)
@@ -54,58 +55,104 @@ __global__ __launch_bounds__(256) void final_sum_kernel(const double* __restrict
 // ---------------------------------------------------------------------------
 // weighted quantile
 // ---------------------------------------------------------------------------
+// Every quantity the ranks exchange is an integer (fixed-point masses, key
+// bounds), so a histogram merged over any number of ranks -- in any order --
+// is exactly the one-GPU histogram, and the selected knots are bit-identical
+// for any GPU count.  The fixed-point scale is a power of two fixed by the
+// largest weight and the total count (both exact under a max-reduction):
+// scale = 2^(62 - ceil(log2(n_total * w_max))), so sum(fix(w)) <= 2^62.
+//
+// Exchange words (XW, u64 / i64, all-reduced by the host between steps when
+// the population is sharded over ranks; see abc_wquantile_exchange):
+struct WQXchg {
+  long long wmax_bits;        // MAX: largest weight (positive double bits)
+  unsigned long long w_tot;   // SUM: total fixed-point mass
+  long long kprev_x;          // MAX: largest key below the knot (key ^ 2^63)
+  long long knext_x;          // MIN: smallest key above the knot
+  unsigned long long wprev;   // SUM: mass of the key kprev
+  unsigned long long wnext;   // SUM: mass of the key knext
+  unsigned long long pad[2];
+  unsigned long long hist_w[kBins];  // SUM: fixed-point mass per digit
+  unsigned long long hist_c[kBins];  // SUM: count per digit
+};
 struct WQState {
+  WQXchg x;
   unsigned long long prefix;    // selected high digits
   unsigned long long remaining; // target minus selected lower mass
   unsigned long long w_less;    // fixed-point mass of keys < selected prefix
   unsigned long long w_eq;      // mass of the final key
-  unsigned long long w_tot;     // total mass
-  unsigned long long kprev, knext, wprev, wnext;
   int none;                     // alpha beyond the last knot
   int pad;
-  double scale;                 // 2^62 / sum(w)
-  double sumw;
+  double scale;                 // power-of-two fixed-point scale
 };
+constexpr unsigned long long kKeyFlip = 0x8000000000000000ull;
 
 __device__ inline unsigned long long fixw(double w, double scale) {
   return static_cast<unsigned long long>(__double2ull_rn(w * scale));
 }
 
-__global__ void wq_init_kernel(WQState* st, const double* __restrict__ sumw) {
-  st->prefix = 0;
-  st->w_less = 0;
-  st->w_eq = 0;
-  st->w_tot = 0;
-  st->kprev = 0;
-  st->knext = ~0ull;
-  st->wprev = 0;
-  st->wnext = 0;
-  st->none = 0;
-  st->sumw = *sumw;
-  st->scale = kFix / *sumw;
+__global__ void wq_reset_kernel(WQState* st) {
+  const int t = threadIdx.x;
+  st->x.hist_w[t] = 0;
+  st->x.hist_c[t] = 0;
+  if (t == 0) {
+    st->x.wmax_bits = 0;
+    st->x.w_tot = 0;
+    st->x.kprev_x = static_cast<long long>(0ull ^ kKeyFlip);   // key 0
+    st->x.knext_x = static_cast<long long>(~0ull ^ kKeyFlip);  // key max
+    st->x.wprev = 0;
+    st->x.wnext = 0;
+    st->prefix = 0;
+    st->w_less = 0;
+    st->w_eq = 0;
+    st->none = 0;
+  }
 }
 
+// largest weight (weights are >= 0: their bits order as signed integers)
+__global__ __launch_bounds__(256) void wq_wmax_kernel(const double* __restrict__ w,
+                                                      int64_t n, WQState* st) {
+  long long m = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const long long b = __double_as_longlong(w ? w[i] : 1.0);
+    m = b > m ? b : m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(m, o, 64);
+    m = a > m ? a : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(&st->x.wmax_bits, m);
+}
+
+// scale from the (reduced) largest weight and the total count, then the
+// local fixed-point total
 __global__ __launch_bounds__(256) void wq_total_kernel(const double* __restrict__ w,
-                                                       int64_t n, WQState* st) {
-  const double scale = st->scale;
+                                                       int64_t n, int64_t n_total,
+                                                       WQState* st) {
+  const double wmax = __longlong_as_double(st->x.wmax_bits);
+  int E = 0;
+  frexp(static_cast<double>(n_total) * wmax, &E);  // n*wmax < 2^E
+  const double scale = wmax > 0.0 ? ldexp(1.0, 62 - E) : 0.0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->scale = scale;
   unsigned long long s = 0;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256)
-    s += w ? fixw(w[i], scale) : fixw(1.0, scale);
+    s += fixw(w ? w[i] : 1.0, scale);
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) atomicAdd(&st->w_tot, s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(&st->x.w_tot, s);
 }
 
 __global__ void wq_target_kernel(WQState* st, double alpha) {
-  const double t = alpha * static_cast<double>(st->w_tot);
-  unsigned long long T = t >= 18446744073709551615.0 ? ~0ull : static_cast<unsigned long long>(t);
-  st->remaining = T;
+  const double t = alpha * static_cast<double>(st->x.w_tot);
+  st->remaining = t >= 18446744073709551615.0 ? ~0ull
+                                              : static_cast<unsigned long long>(t);
 }
 
 __global__ __launch_bounds__(256) void wq_hist_kernel(
     const double* __restrict__ d, const double* __restrict__ w, int64_t n,
-    const WQState* __restrict__ st, int shift, unsigned long long mask,
-    unsigned long long* __restrict__ hist_w, unsigned* __restrict__ hist_c) {
+    WQState* __restrict__ st, int shift, unsigned long long mask) {
   __shared__ unsigned long long hw[kBins];
   __shared__ unsigned hc[kBins];
   hw[threadIdx.x] = 0;
@@ -118,25 +165,27 @@ __global__ __launch_bounds__(256) void wq_hist_kernel(
     const uint64_t k = f64_key(d[i]);
     if (((k ^ prefix) & mask) == 0) {
       const int bin = static_cast<int>((k >> shift) & 0xff);
-      atomicAdd(&hw[bin], w ? fixw(w[i], scale) : fixw(1.0, scale));
+      atomicAdd(&hw[bin], fixw(w ? w[i] : 1.0, scale));
       atomicAdd(&hc[bin], 1u);
     }
   }
   __syncthreads();
   if (hc[threadIdx.x]) {
-    atomicAdd(&hist_w[threadIdx.x], hw[threadIdx.x]);
-    atomicAdd(&hist_c[threadIdx.x], hc[threadIdx.x]);
+    atomicAdd(&st->x.hist_w[threadIdx.x], hw[threadIdx.x]);
+    atomicAdd(&st->x.hist_c[threadIdx.x],
+              static_cast<unsigned long long>(hc[threadIdx.x]));
   }
 }
 
-__global__ __launch_bounds__(256) void wq_select_kernel(
-    WQState* st, int shift, unsigned long long* __restrict__ hist_w,
-    unsigned* __restrict__ hist_c, int last) {
+// the (merged) digit histogram -> the digit whose mass interval holds the
+// remaining target; clears the histogram for the next pass
+__global__ __launch_bounds__(256) void wq_select_kernel(WQState* st, int shift,
+                                                        int last) {
   __shared__ unsigned long long s[kBins];
   __shared__ int found;
   const int t = threadIdx.x;
-  const unsigned long long v = hist_w[t];
-  const unsigned c = hist_c[t];
+  const unsigned long long v = st->x.hist_w[t];
+  const unsigned long long c = st->x.hist_c[t];
   s[t] = v;
   if (t == 0) found = -1;
   __syncthreads();
@@ -157,8 +206,8 @@ __global__ __launch_bounds__(256) void wq_select_kernel(
     if (last) st->w_eq = v;
   }
   if (t == 0 && found < 0 && st->none == 0) st->none = 1;
-  hist_w[t] = 0;
-  hist_c[t] = 0;
+  st->x.hist_w[t] = 0;
+  st->x.hist_c[t] = 0;
 }
 
 __global__ __launch_bounds__(256) void wq_neighbors_kernel(const double* __restrict__ d,
@@ -179,53 +228,56 @@ __global__ __launch_bounds__(256) void wq_neighbors_kernel(const double* __restr
     kn = b < kn ? b : kn;
   }
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(&st->kprev, kp);
-    atomicMin(&st->knext, kn);
+    atomicMax(&st->x.kprev_x, static_cast<long long>(kp ^ kKeyFlip));
+    atomicMin(&st->x.knext_x, static_cast<long long>(kn ^ kKeyFlip));
   }
 }
 
 __global__ __launch_bounds__(256) void wq_neighbor_mass_kernel(
     const double* __restrict__ d, const double* __restrict__ w, int64_t n,
     WQState* st) {
-  const unsigned long long kp = st->kprev, kn = st->knext;
+  const unsigned long long kp = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
+  const unsigned long long kn = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
   const double scale = st->scale;
   unsigned long long sp = 0, sn = 0;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     const uint64_t k = f64_key(d[i]);
-    const unsigned long long wi = w ? fixw(w[i], scale) : fixw(1.0, scale);
+    const unsigned long long wi = fixw(w ? w[i] : 1.0, scale);
     if (k == kp) sp += wi;
     if (k == kn) sn += wi;
   }
   sp = wave_sum(sp);
   sn = wave_sum(sn);
   if ((threadIdx.x & 63) == 0) {
-    if (sp) atomicAdd(&st->wprev, sp);
-    if (sn) atomicAdd(&st->wnext, sn);
+    if (sp) atomicAdd(&st->x.wprev, sp);
+    if (sn) atomicAdd(&st->x.wnext, sn);
   }
 }
 
 // np.interp(alpha, xp, fp) restricted to the bracketing knots
-__global__ void wq_finalize_kernel(const WQState* st, int64_t n, double alpha,
+__global__ void wq_finalize_kernel(const WQState* st, double alpha,
                                    double* __restrict__ out) {
-  const double W = static_cast<double>(st->w_tot);
+  const double W = static_cast<double>(st->x.w_tot);
+  const unsigned long long kprev = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
+  const unsigned long long knext = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
   double eps;
   if (st->none) {
-    eps = key_f64(st->kprev);  // alpha past the last knot: largest point
+    eps = key_f64(kprev);  // alpha past the last knot: largest point
   } else {
     const double pk = key_f64(st->prefix);
     const double wk = static_cast<double>(st->w_eq) / W;
     const double csk = static_cast<double>(st->w_less + st->w_eq) / W;
     const double xk = csk - 0.5 * wk;
     // a sorted neighbour exists (zero-mass neighbours are knots too)
-    const bool prev_ok = st->kprev != 0;
-    const bool next_ok = st->knext != ~0ull;
+    const bool prev_ok = kprev != 0;
+    const bool next_ok = knext != ~0ull;
     if (alpha >= xk) {
       if (!next_ok || alpha == xk) {
         eps = pk;
       } else {
-        const double pn = key_f64(st->knext);
-        const double wn = static_cast<double>(st->wnext) / W;
+        const double pn = key_f64(knext);
+        const double wn = static_cast<double>(st->x.wnext) / W;
         const double xn = csk + wn - 0.5 * wn;
         const double slope = (pn - pk) / (xn - xk);
         eps = slope * (alpha - xk) + pk;
@@ -234,8 +286,8 @@ __global__ void wq_finalize_kernel(const WQState* st, int64_t n, double alpha,
       if (!prev_ok) {
         eps = pk;
       } else {
-        const double pp = key_f64(st->kprev);
-        const double wp = static_cast<double>(st->wprev) / W;
+        const double pp = key_f64(kprev);
+        const double wp = static_cast<double>(st->x.wprev) / W;
         const double csp = static_cast<double>(st->w_less) / W;
         const double xp = csp - 0.5 * wp;
         if (alpha == xp) {
@@ -251,6 +303,55 @@ __global__ void wq_finalize_kernel(const WQState* st, int64_t n, double alpha,
   out[1] = key_f64(st->prefix);
   out[2] = static_cast<double>(st->w_less) / W;
   out[3] = static_cast<double>(st->w_eq) / W;
+}
+
+// one step of the sharded select (see abc_wquantile_step_f64)
+enum WQStep {
+  kWqReset = 0, kWqWmax = 1, kWqTotal = 2, kWqTarget = 3,
+  kWqHist0 = 10, kWqSelect0 = 20, kWqNeighbors = 30, kWqMass = 31,
+  kWqFinish = 32
+};
+
+int wq_step(int step, const double* d, const double* w, int64_t n,
+            int64_t n_total, double alpha, double* out4, WQState* s,
+            hipStream_t st) {
+  const unsigned g = stream_grid(n > 0 ? n : 1, 256, 1024);
+  if (step == kWqReset) {
+    hipLaunchKernelGGL(wq_reset_kernel, dim3(1), dim3(kBins), 0, st, s);
+  } else if (step == kWqWmax) {
+    if (n > 0)
+      hipLaunchKernelGGL(wq_wmax_kernel, dim3(g), dim3(256), 0, st, w, n, s);
+  } else if (step == kWqTotal) {
+    hipLaunchKernelGGL(wq_total_kernel, dim3(g), dim3(256), 0, st, w, n,
+                       n_total, s);
+  } else if (step == kWqTarget) {
+    hipLaunchKernelGGL(wq_target_kernel, dim3(1), dim3(1), 0, st, s, alpha);
+  } else if (step >= kWqHist0 && step < kWqHist0 + 8) {
+    const int pass = step - kWqHist0;
+    const int shift = 56 - 8 * pass;
+    const unsigned long long mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
+    if (n > 0)
+      hipLaunchKernelGGL(wq_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,
+                         shift, mask);
+  } else if (step >= kWqSelect0 && step < kWqSelect0 + 8) {
+    const int pass = step - kWqSelect0;
+    hipLaunchKernelGGL(wq_select_kernel, dim3(1), dim3(256), 0, st, s,
+                       56 - 8 * pass, pass == 7 ? 1 : 0);
+  } else if (step == kWqNeighbors) {
+    if (n > 0)
+      hipLaunchKernelGGL(wq_neighbors_kernel, dim3(g), dim3(256), 0, st, d, n, s);
+  } else if (step == kWqMass) {
+    if (n > 0)
+      hipLaunchKernelGGL(wq_neighbor_mass_kernel, dim3(g), dim3(256), 0, st, d,
+                         w, n, s);
+  } else if (step == kWqFinish) {
+    hipLaunchKernelGGL(wq_finalize_kernel, dim3(1), dim3(1), 0, st, s, alpha,
+                       out4);
+  } else {
+    set_error("wquantile: unknown step %d", step);
+    return kInvalidArg;
+  }
+  return kOk;
 }
 
 // ---------------------------------------------------------------------------
@@ -821,8 +922,45 @@ int abc_importance_weights_f64(const double* logpd, const double* prior,
   return kOk;
 }
 
-size_t abc_wquantile_workspace_bytes(void) {
-  return sizeof(WQState) + kBins * 12 + 8 + kRedGrid * 8 + 256;
+size_t abc_wquantile_workspace_bytes(void) { return sizeof(WQState) + 256; }
+
+int abc_wquantile_step_f64(int step, const double* d, const double* w,
+                           int64_t n_local, int64_t n_total, double alpha,
+                           double* out4, void* ws, size_t ws_bytes,
+                           hipStream_t st) {
+  ABC_REQUIRE(n_local >= 0 && n_total > 0 && n_local <= n_total && ws,
+              "wquantile_step: bad args");
+  ABC_REQUIRE(n_local == 0 || d, "wquantile_step: null d");
+  ABC_REQUIRE(step != kWqFinish || out4, "wquantile_step: null out");
+  ABC_REQUIRE(ws_bytes >= abc_wquantile_workspace_bytes(),
+              "wquantile_step: workspace too small");
+  const int rc = wq_step(step, d, w, n_local, n_total, alpha, out4,
+                         static_cast<WQState*>(ws), st);
+  if (rc != kOk) return rc;
+  ABC_LAUNCH_CHECK("wquantile step");
+  return kOk;
+}
+
+int abc_wquantile_exchange(int step, int64_t* offset_bytes, int64_t* count,
+                           int* op) {
+  ABC_REQUIRE(offset_bytes && count && op, "wquantile_exchange: null");
+  *offset_bytes = 0;
+  *count = 0;
+  *op = 0;  // 0 none, 1 sum, 2 max, 3 min (int64 words)
+  if (step == kWqWmax) {
+    *offset_bytes = offsetof(WQXchg, wmax_bits); *count = 1; *op = 2;
+  } else if (step == kWqTotal) {
+    *offset_bytes = offsetof(WQXchg, w_tot); *count = 1; *op = 1;
+  } else if (step >= kWqHist0 && step < kWqHist0 + 8) {
+    *offset_bytes = offsetof(WQXchg, hist_w); *count = 2 * kBins; *op = 1;
+  } else if (step == kWqNeighbors) {
+    // two words with different ops: kprev_x (max) then knext_x (min); the
+    // host reduces the first with MAX and the second with MIN
+    *offset_bytes = offsetof(WQXchg, kprev_x); *count = 2; *op = 4;
+  } else if (step == kWqMass) {
+    *offset_bytes = offsetof(WQXchg, wprev); *count = 2; *op = 1;
+  }
+  return kOk;
 }
 
 int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
@@ -830,39 +968,14 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
   ABC_REQUIRE(n > 0 && d && out4 && ws, "wquantile: bad args");
   ABC_REQUIRE(ws_bytes >= abc_wquantile_workspace_bytes(),
               "wquantile: workspace too small");
-  char* base = static_cast<char*>(ws);
-  WQState* s = reinterpret_cast<WQState*>(base);
-  unsigned long long* hw = reinterpret_cast<unsigned long long*>(base + 256);
-  unsigned* hc = reinterpret_cast<unsigned*>(base + 256 + kBins * 8);
-  double* sumw = reinterpret_cast<double*>(base + 256 + kBins * 12);
-  double* part = sumw + 1;
-  if (w) {
-    hipLaunchKernelGGL(partial_sum_kernel, dim3(kRedGrid), dim3(256), 0, st, w,
-                       n, 0, part);
-    hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part,
-                       kRedGrid, sumw);
-  } else {
-    const double nn = static_cast<double>(n);
-    ABC_HIP(hipMemcpyAsync(sumw, &nn, 8, hipMemcpyHostToDevice, st));
+  WQState* s = static_cast<WQState*>(ws);
+  static const int kSeq[] = {kWqReset, kWqWmax, kWqTotal, kWqTarget,
+                             10, 20, 11, 21, 12, 22, 13, 23, 14, 24, 15, 25,
+                             16, 26, 17, 27, kWqNeighbors, kWqMass, kWqFinish};
+  for (int step : kSeq) {
+    const int rc = wq_step(step, d, w, n, n, alpha, out4, s, st);
+    if (rc != kOk) return rc;
   }
-  ABC_HIP(hipMemsetAsync(hw, 0, kBins * 12, st));
-  hipLaunchKernelGGL(wq_init_kernel, dim3(1), dim3(1), 0, st, s, sumw);
-  const unsigned g = stream_grid(n, 256, 1024);
-  hipLaunchKernelGGL(wq_total_kernel, dim3(g), dim3(256), 0, st, w, n, s);
-  hipLaunchKernelGGL(wq_target_kernel, dim3(1), dim3(1), 0, st, s, alpha);
-  for (int pass = 0; pass < 8; ++pass) {
-    const int shift = 56 - 8 * pass;
-    const unsigned long long mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
-    hipLaunchKernelGGL(wq_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,
-                       shift, mask, hw, hc);
-    hipLaunchKernelGGL(wq_select_kernel, dim3(1), dim3(256), 0, st, s, shift,
-                       hw, hc, pass == 7 ? 1 : 0);
-  }
-  hipLaunchKernelGGL(wq_neighbors_kernel, dim3(g), dim3(256), 0, st, d, n, s);
-  hipLaunchKernelGGL(wq_neighbor_mass_kernel, dim3(g), dim3(256), 0, st, d, w,
-                     n, s);
-  hipLaunchKernelGGL(wq_finalize_kernel, dim3(1), dim3(1), 0, st, s, n, alpha,
-                     out4);
   ABC_LAUNCH_CHECK("wquantile kernels");
   return kOk;
 }

@@ -138,6 +138,23 @@ class Comm:
         dist.all_reduce(x)
         return int(x.item())
 
+    def all_reduce_words(self, x, op):
+        """In-place all-reduce of an int64 device view (op 1 sum, 2 max,
+        3 min, 4 max of x[0] and min of x[1]); gloo stages through host."""
+        if not self.active:
+            return
+        ops = {1: dist.ReduceOp.SUM, 2: dist.ReduceOp.MAX,
+               3: dist.ReduceOp.MIN}
+        y = x.cpu() if (self._host_staged and x.is_cuda) else x.clone()
+        if op == 4:
+            a, b = y[0:1].clone(), y[1:2].clone()
+            dist.all_reduce(a, op=dist.ReduceOp.MAX)
+            dist.all_reduce(b, op=dist.ReduceOp.MIN)
+            y = torch.cat([a, b])
+        else:
+            dist.all_reduce(y, op=ops[op])
+        x.copy_(y)
+
     def all_reduce_max_float(self, v):
         if not self.active:
             return float(v)

@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
+from .distributed import Comm
 
 logger = logging.getLogger("Epsilon")
 
@@ -136,7 +137,11 @@ class QuantileEpsilon(Epsilon):
         d, w = _columns(weighted_distances)
         # weighted: w / sum(w) (epsilon.py:214-218); else uniform 1/n
         wq = w if self.weighted else None
-        q = float(K.weighted_quantile(d, wq, self.alpha)[0].item())
+        # a device population is the same global population on every rank:
+        # each rank histograms its share, the histograms are all-reduced
+        comm = Comm.current() if hasattr(weighted_distances,
+                                         "distance_tensor") else None
+        q = float(K.weighted_quantile(d, wq, self.alpha, comm=comm)[0].item())
         self._look_up[t] = q * self.quantile_multiplier
 
 

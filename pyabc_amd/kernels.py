@@ -6,6 +6,7 @@ tensors of the stated dtype and layout; there is no host/CPU path.  Small
 d x d linear algebra (eigh/svd of the KDE covariance) is done by the callers on
 the host, exactly where the reference calls numpy/scipy on d x d matrices.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -354,15 +355,43 @@ def column_std(data_T, n=None):
     return mean, std
 
 
-def weighted_quantile(d, w, alpha):
-    """Device [eps, p_k, cs_{k-1}, w_k] for interp(alpha, cs - w/2, sort d)."""
+_WQ_SEQ = [0, 1, 2, 3] + [s for p in range(8) for s in (10 + p, 20 + p)] \
+    + [30, 31, 32]
+
+
+def weighted_quantile(d, w, alpha, comm=None):
+    """Device [eps, p_k, cs_{k-1}, w_k] for interp(alpha, cs - w/2, sort d).
+
+    With ``comm`` over several ranks (every rank holding the same global
+    population) each rank histograms only its row_range of (d, w) and the
+    integer histograms / key bounds are all-reduced between the radix passes
+    (SURVEY 8(e)); the result is bit-identical to one rank's."""
     n = d.numel()
     out = torch.empty(4, dtype=F64, device=_dev())
     wsb = nat.lib().abc_wquantile_workspace_bytes()
     ws = WS.get(wsb, "wq")
-    call("abc_wquantile_f64", ptr(_contig(d, F64)),
-         ptr(None if w is None else _contig(w, F64)), n, float(alpha),
-         ptr(out), ptr(ws), wsb, nat.stream())
+    d = _contig(d, F64)
+    w = None if w is None else _contig(w, F64)
+    if comm is None or not comm.active:
+        call("abc_wquantile_f64", ptr(d), ptr(w), n, float(alpha), ptr(out),
+             ptr(ws), wsb, nat.stream())
+        return out
+    q, m = divmod(n, comm.world)
+    lo = comm.rank * q + min(comm.rank, m)
+    hi = lo + q + (1 if comm.rank < m else 0)
+    dl = d[lo:hi]
+    wl = None if w is None else w[lo:hi]
+    words = ws[:(wsb // 8) * 8].view(torch.int64)
+    off, cnt, op = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+    for step in _WQ_SEQ:
+        call("abc_wquantile_step_f64", step, ptr(dl) if hi > lo else None,
+             ptr(wl) if (wl is not None and hi > lo) else None, hi - lo, n,
+             float(alpha), ptr(out), ptr(ws), wsb, nat.stream())
+        call("abc_wquantile_exchange", step, ctypes.byref(off),
+             ctypes.byref(cnt), ctypes.byref(op))
+        if op.value:
+            a = off.value // 8
+            comm.all_reduce_words(words[a:a + cnt.value], op.value)
     return out
 
 

@@ -53,12 +53,12 @@ def _generation(comm, n, min_batch, record):
     dist = comm.all_gather_rows(d0)
     w = torch.full((theta.shape[0],), 1.0 / theta.shape[0],
                    dtype=torch.float64, device="cuda")
-    eps = float(K.weighted_quantile(dist, w, 0.5)[0].item())
+    eps = float(K.weighted_quantile(dist, w, 0.5, comm=comm)[0].item())
     fit = DeviceMVNFit(theta, w)
     res = eng.sample_generation(1, n, fit, x0, fw, eps, keep_stats=True,
                                 record=record)
     th, dd, ww, n_eval, _ = eng.gather_population(res)
-    eps1 = float(K.weighted_quantile(dd, ww, 0.5)[0].item())
+    eps1 = float(K.weighted_quantile(dd, ww, 0.5, comm=comm)[0].item())
     fit1 = DeviceMVNFit(th, ww)
     # exact-inference generation: stochastic acceptance with u keyed by the
     # global evaluation id, acceptance weights, particle records

@@ -41,6 +41,10 @@ size_t abc_moments_workspace_bytes(int d);
 int abc_weighted_moments_f64(const double* X, const double* w, int64_t n,
                              int d, double* out, void* ws, size_t ws_bytes,
                              hipStream_t stream);
+/* fp32 storage of X and w (SURVEY 8(b) minimum set), the same fp64 sums */
+int abc_weighted_moments_f32(const float* X, const float* w, int64_t n,
+                             int d, double* out, void* ws, size_t ws_bytes,
+                             hipStream_t stream);
 
 /* ---------------- (a2) MultivariateNormalTransition.rvs + prior support ----
  * Replaces np.random.choice(p=w) (cumsum, /= cdf[-1], searchsorted 'right')
@@ -56,6 +60,15 @@ int abc_resample_perturb_f64(const double* X, int64_t N, int d,
                              const double* z, const double* A,
                              const double* lo, const double* scale, int64_t B,
                              double* theta, int64_t* idx, uint8_t* in_support,
+                             hipStream_t stream);
+/* fp32 storage form (X, z, A, theta fp32; z A accumulated in fp32; the CDF
+ * search and the support test in fp64): 12d + 25 B per proposal
+ *                                                    multivariatenormal.py:87-95 */
+int abc_resample_perturb_f32(const float* X, int64_t N, int d,
+                             const double* cdf, const double* u,
+                             const float* z, const float* A,
+                             const double* lo, const double* scale, int64_t B,
+                             float* theta, int64_t* idx, uint8_t* in_support,
                              hipStream_t stream);
 /* production variant: u, z drawn from Philox4x32-10 (seed, streams 2*sid and
  * 2*sid+1, counter offset) inside the kernel */
@@ -89,6 +102,17 @@ int abc_philox_uniform_f64(uint64_t seed, uint64_t sid, uint64_t offset,
                            int64_t n, double* u, hipStream_t stream);
 int abc_philox_normal_f64(uint64_t seed, uint64_t sid, uint64_t offset,
                           int64_t n, double* z, hipStream_t stream);
+/* The draws of proposals offset .. offset + nu - 1 as arrays (SURVEY 8(b)
+ * abc_philox_fill): u[i] from stream 2*sid, z[i*dz + k] (dz = nz / nu) from
+ * stream 2*sid+1 -- exactly what abc_propose_philox_f64 draws in-kernel,
+ * so abc_resample_perturb_f64(u, z) reproduces it bit for bit. Replaces the
+ * numpy draws u = random_sample(), z = standard_normal(d)
+ *                                                    multivariatenormal.py:89-94 */
+int abc_philox_fill(uint64_t seed, uint64_t sid, uint64_t offset, double* u,
+                    int64_t nu, double* z, int64_t nz, hipStream_t stream);
+int abc_philox_fill_f32(uint64_t seed, uint64_t sid, uint64_t offset,
+                        double* u, int64_t nu, float* z, int64_t nz,
+                        hipStream_t stream);
 /* order-preserving compaction: proposal ids for in-support draws only
  * (out-of-support redraws are not evaluations, smc.py:629-645) */
 size_t abc_compact_workspace_bytes(int64_t n);
@@ -134,6 +158,21 @@ int abc_kde_logpdf_f32(const float* Ynew, int64_t M, const float* P,
 int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
                        int64_t npad, int d, const double* lw2max,
                        double log_const, double* out_logpd, void* ws,
+                       size_t ws_bytes, hipStream_t stream);
+/* SURVEY 8(b) form on rows already whitened with scipy's U:
+ *   out[i] = log_offset + log sum_j exp(logw[j] - |Ynew_i - Yprev_j|^2 / 2)
+ * (the host adds -(rank log 2pi + log_pdet)/2 and the prior); Ynew [M*d],
+ * Yprev [N*d], logw [N] in T, the same fixed-segment pass as above.
+ *                                  multivariatenormal.py:102-125 (scipy _PSD) */
+size_t abc_kde_logsum_workspace_bytes_f32(int64_t M, int64_t N, int d);
+size_t abc_kde_logsum_workspace_bytes_f64(int64_t M, int64_t N, int d);
+int abc_kde_logsum_f32(const float* Ynew, const float* Yprev, const float* logw,
+                       int64_t M, int64_t N, int d, float log_offset,
+                       float* out_log_sum, void* ws, size_t ws_bytes,
+                       hipStream_t stream);
+int abc_kde_logsum_f64(const double* Ynew, const double* Yprev,
+                       const double* logw, int64_t M, int64_t N, int d,
+                       double log_offset, double* out_log_sum, void* ws,
                        size_t ws_bytes, hipStream_t stream);
 /* Same density on the matrix cores (v_mfma_f32_32x32x16_bf16): the
  * exponent lw2_j - |y_i - y_j|^2 is expanded as a_j + b_i + 2 y_i.y_j with
@@ -241,6 +280,19 @@ int abc_knn_f64(const double* X, int64_t N, int d, int k, int32_t* nbr,
 int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
                       const int32_t* nbr, int k, double scaling,
                       double* covs, double* inv_covs, double* dets,
+                      hipStream_t stream);
+/* fp32 storage forms (SURVEY 8(b) abc_knn_topk_f32 / abc_local_cov_f32):
+ * the fp32 points are widened (exactly) and the fp64 kernels run on them;
+ * neighbour sets are those of the fp32 points, results rounded to fp32.
+ *                              local_transition.py:82-83, 112-139 */
+size_t abc_knn_topk_f32_workspace_bytes(int64_t N, int d, int k);
+int abc_knn_topk_f32(const float* X, int64_t N, int d, int k, int32_t* nbr,
+                     float* nbr_d2, void* ws, size_t ws_bytes,
+                     hipStream_t stream);
+size_t abc_local_cov_f32_workspace_bytes(int64_t N, int d);
+int abc_local_cov_f32(const float* X, const float* w, int64_t N, int d,
+                      const int32_t* nbr, int k, double scaling, float* covs,
+                      float* inv_covs, float* dets, void* ws, size_t ws_bytes,
                       hipStream_t stream);
 /* The same for the particles [row0, row0 + nrows) only (one rank's share of
  * the fit): nbr / nbr_d2 / covs / inv_covs / dets hold those

@@ -113,6 +113,30 @@ _SIGS = {
     "abc_column_std_workspace_bytes": (c_size, [c_i64, c_int]),
     "abc_column_std_ws_f64": (c_int, [c_ptr, c_i64, c_i64, c_int, c_ptr,
                                       c_ptr, c_ptr, c_size, c_ptr]),
+    # SURVEY 8(b) fp32-storage and logsum forms
+    "abc_weighted_moments_f32": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
+                                         c_ptr, c_size, c_ptr]),
+    "abc_resample_perturb_f32": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                         c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
+                                         c_ptr, c_ptr, c_ptr, c_ptr]),
+    "abc_philox_fill": (c_int, [c_u64, c_u64, c_u64, c_ptr, c_i64, c_ptr,
+                                c_i64, c_ptr]),
+    "abc_philox_fill_f32": (c_int, [c_u64, c_u64, c_u64, c_ptr, c_i64, c_ptr,
+                                    c_i64, c_ptr]),
+    "abc_kde_logsum_workspace_bytes_f32": (c_size, [c_i64, c_i64, c_int]),
+    "abc_kde_logsum_workspace_bytes_f64": (c_size, [c_i64, c_i64, c_int]),
+    "abc_kde_logsum_f32": (c_int, [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int,
+                                   ctypes.c_float, c_ptr, c_ptr, c_size,
+                                   c_ptr]),
+    "abc_kde_logsum_f64": (c_int, [c_ptr, c_ptr, c_ptr, c_i64, c_i64, c_int,
+                                   c_dbl, c_ptr, c_ptr, c_size, c_ptr]),
+    "abc_knn_topk_f32_workspace_bytes": (c_size, [c_i64, c_int, c_int]),
+    "abc_knn_topk_f32": (c_int, [c_ptr, c_i64, c_int, c_int, c_ptr, c_ptr,
+                                 c_ptr, c_size, c_ptr]),
+    "abc_local_cov_f32_workspace_bytes": (c_size, [c_i64, c_int]),
+    "abc_local_cov_f32": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr, c_int,
+                                  c_dbl, c_ptr, c_ptr, c_ptr, c_ptr, c_size,
+                                  c_ptr]),
     # (a7)
     "abc_wquantile_workspace_bytes": (c_size, []),
     "abc_wquantile_f64": (c_int, [c_ptr, c_ptr, c_i64, c_dbl, c_ptr, c_ptr,

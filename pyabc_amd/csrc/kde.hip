@@ -573,6 +573,145 @@ static int pack_dispatch(const double* X, const double* w, int64_t n, int d,
   return kOk;
 }
 
+// ---------------------------------------------------------------------------
+// abc_kde_logsum (SURVEY 8(b) minimum set): the same pass on rows the caller
+// has already whitened with scipy's U, and log-weights:
+//   out_i = log_offset + log sum_j exp(logw_j - |y_i - y_j|^2 / 2)
+// The rows are rescaled by sqrt(log2(e)/2) and the log-weights moved to
+// log2 units relative to their maximum, then the packed-population pass of
+// logpdf_impl runs unchanged (finalize adds ln2 * max + log_offset).
+// ---------------------------------------------------------------------------
+constexpr double kSqrtHalfLog2e = 0.84932180028801907;  // sqrt(log2(e) / 2)
+constexpr double kLog2e = 1.4426950408889634;
+
+template <typename T>
+__global__ __launch_bounds__(256) void logw_max_kernel(
+    const T* __restrict__ logw, int64_t n, unsigned long long* __restrict__ key) {
+  uint64_t m = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const double v = static_cast<double>(logw[i]);
+    if (v == v) m = max(m, f64_key(v));  // NaN ignored
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t u = __shfl_xor(m, o, 64);
+    m = u > m ? u : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(key, static_cast<unsigned long long>(m));
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void logsum_pack_kernel(
+    const T* __restrict__ Yp, const T* __restrict__ logw, int64_t n, int d,
+    T* __restrict__ P, int64_t npad, const unsigned long long* __restrict__ key,
+    double* __restrict__ lw2max_out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const double L = key_f64(*key) * kLog2e;
+  if (i == 0) *lw2max_out = L;
+  if (i >= npad) return;
+  T* row = P + i * (D + 1);
+  if (i >= n) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) row[k] = T(0);
+    row[D] = static_cast<T>(kPadLw);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    row[k] = k < d ? static_cast<T>(static_cast<double>(Yp[i * d + k]) *
+                                    kSqrtHalfLog2e)
+                   : T(0);
+  double lw = static_cast<double>(logw[i]) * kLog2e - L;
+  if (!(lw >= static_cast<double>(kPadLw))) lw = kPadLw;  // -inf / NaN
+  row[D] = static_cast<T>(lw);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void logsum_rows_kernel(
+    const T* __restrict__ Yn, int64_t M, int d, T* __restrict__ Y) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    Y[i * D + k] = k < d ? static_cast<T>(static_cast<double>(Yn[i * d + k]) *
+                                          kSqrtHalfLog2e)
+                         : T(0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void store_out_kernel(const double* __restrict__ src,
+                                                        int64_t M,
+                                                        T* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < M) out[i] = static_cast<T>(src[i]);
+}
+
+template <typename T>
+size_t logsum_ws_bytes(int64_t M, int64_t N, int d) {
+  const int D = padded_dim(d);
+  if (D < 0 || M < 0 || N < 0) return 0;
+  const int64_t npad = ceil_div(N > 0 ? N : 1, kRowPad) * kRowPad;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  return 256 + al(static_cast<size_t>(npad) * (D + 1) * sizeof(T)) +
+         al(static_cast<size_t>(M) * D * sizeof(T)) +
+         al(static_cast<size_t>(M) * 8) + ws_bytes_impl<T>(M, npad, d);
+}
+
+template <typename T>
+int logsum_impl(const T* Ynew, const T* Yprev, const T* logw, int64_t M,
+                int64_t N, int d, T log_offset, T* out, void* ws,
+                size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(M >= 0 && N > 0, "kde_logsum: need M >= 0, N > 0");
+  const int D = padded_dim(d);
+  if (D < 0) {
+    set_error("kde_logsum: unsupported dimension d=%d (max 32)", d);
+    return kUnsupported;
+  }
+  if (M == 0) return kOk;
+  ABC_REQUIRE(Ynew && Yprev && logw && out && ws, "kde_logsum: null pointer");
+  ABC_REQUIRE(ws_bytes >= logsum_ws_bytes<T>(M, N, d),
+              "kde_logsum: workspace too small");
+  const int64_t npad = ceil_div(N, kRowPad) * kRowPad;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  char* base = static_cast<char*>(ws);
+  unsigned long long* key = reinterpret_cast<unsigned long long*>(base);
+  double* lw2max = reinterpret_cast<double*>(base + 64);
+  char* q = base + 256;
+  T* P = reinterpret_cast<T*>(q);
+  q += al(static_cast<size_t>(npad) * (D + 1) * sizeof(T));
+  T* Y = reinterpret_cast<T*>(q);
+  q += al(static_cast<size_t>(M) * D * sizeof(T));
+  double* tmp = reinterpret_cast<double*>(q);
+  q += al(static_cast<size_t>(M) * 8);
+  const size_t rest = ws_bytes - static_cast<size_t>(q - base);
+  ABC_HIP(hipMemsetAsync(key, 0, 8, st));
+  hipLaunchKernelGGL((logw_max_kernel<T>), dim3(stream_grid(N, 256, 1024)),
+                     dim3(256), 0, st, logw, N, key);
+  switch (D) {
+#define CASE(DD)                                                               \
+  case DD:                                                                     \
+    hipLaunchKernelGGL((logsum_pack_kernel<T, DD>), dim3(ceil_div(npad, 256)), \
+                       dim3(256), 0, st, Yprev, logw, N, d, P, npad, key,      \
+                       lw2max);                                                \
+    hipLaunchKernelGGL((logsum_rows_kernel<T, DD>), dim3(ceil_div(M, 256)),    \
+                       dim3(256), 0, st, Ynew, M, d, Y);                       \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+  }
+  ABC_LAUNCH_CHECK("kde_logsum pack kernels");
+  const int rc = logpdf_dispatch<T>(Y, M, P, npad, d, lw2max,
+                                    static_cast<double>(log_offset), tmp, q,
+                                    rest, st);
+  if (rc != kOk) return rc;
+  hipLaunchKernelGGL((store_out_kernel<T>), dim3(ceil_div(M, 256)), dim3(256),
+                     0, st, tmp, M, out);
+  ABC_LAUNCH_CHECK("kde_logsum store");
+  return kOk;
+}
+
 // shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum
 // and underflow detection of the fp32-exponent pass, then the exact fixup in
 // fp64 on fp64 rows.  An fp32 copy of a far row (|y| ~ 30 in log2 units)
@@ -642,6 +781,27 @@ int abc_kde_split(int64_t M, int64_t npad, int d) {
 #undef CASE
     default: return -1;
   }
+}
+
+size_t abc_kde_logsum_workspace_bytes_f32(int64_t M, int64_t N, int d) {
+  return logsum_ws_bytes<float>(M, N, d);
+}
+size_t abc_kde_logsum_workspace_bytes_f64(int64_t M, int64_t N, int d) {
+  return logsum_ws_bytes<double>(M, N, d);
+}
+int abc_kde_logsum_f32(const float* Ynew, const float* Yprev, const float* logw,
+                       int64_t M, int64_t N, int d, float log_offset,
+                       float* out_log_sum, void* ws, size_t ws_bytes,
+                       hipStream_t st) {
+  return logsum_impl<float>(Ynew, Yprev, logw, M, N, d, log_offset,
+                            out_log_sum, ws, ws_bytes, st);
+}
+int abc_kde_logsum_f64(const double* Ynew, const double* Yprev,
+                       const double* logw, int64_t M, int64_t N, int d,
+                       double log_offset, double* out_log_sum, void* ws,
+                       size_t ws_bytes, hipStream_t st) {
+  return logsum_impl<double>(Ynew, Yprev, logw, M, N, d, log_offset,
+                             out_log_sum, ws, ws_bytes, st);
 }
 
 int abc_whiten_f32(const double* X, int64_t n, int d, const double* mu,

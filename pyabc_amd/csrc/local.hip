@@ -712,6 +712,26 @@ __global__ __launch_bounds__(256) void propose_local_kernel(
   sup[b] = ok ? 1 : 0;
 }
 
+// fp32-storage entry points (SURVEY 8(b) abc_knn_topk_f32 /
+// abc_local_cov_f32): the fp32 inputs are widened into the workspace and the
+// fp64 kernels run on them (every fp32 value is exact in fp64, so the kNN
+// sets are those of the fp32 points), results rounded to fp32 on the way out.
+template <typename S, typename D>
+__global__ __launch_bounds__(256) void convert_kernel(const S* __restrict__ src,
+                                                      int64_t n,
+                                                      D* __restrict__ dst) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    dst[i] = static_cast<D>(src[i]);
+}
+template <typename S, typename D>
+void convert(const S* src, int64_t n, D* dst, hipStream_t st) {
+  if (n > 0)
+    hipLaunchKernelGGL((convert_kernel<S, D>), dim3(stream_grid(n, 256, 2048)),
+                       dim3(256), 0, st, src, n, dst);
+}
+inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+
 }  // namespace abc
 
 using namespace abc;
@@ -989,6 +1009,70 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   }
 #undef L
   ABC_LAUNCH_CHECK("local_logpdf_f32 kernels");
+  return kOk;
+}
+
+size_t abc_knn_topk_f32_workspace_bytes(int64_t N, int d, int k) {
+  return al256(static_cast<size_t>(N) * d * 8) +
+         al256(static_cast<size_t>(N) * k * 8) + abc_knn_workspace_bytes(N, k);
+}
+
+int abc_knn_topk_f32(const float* X, int64_t N, int d, int k, int32_t* nbr,
+                     float* nbr_d2, void* ws, size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(N >= 1 && d >= 1 && k >= 1, "knn_topk_f32: bad sizes");
+  ABC_REQUIRE(X && nbr && nbr_d2 && ws, "knn_topk_f32: null pointer");
+  ABC_REQUIRE(ws_bytes >= abc_knn_topk_f32_workspace_bytes(N, d, k),
+              "knn_topk_f32: workspace too small");
+  char* q = static_cast<char*>(ws);
+  double* Xd = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * d * 8);
+  double* d2 = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * k * 8);
+  convert(X, N * d, Xd, st);
+  const int rc = abc_knn_rows_f64(Xd, N, d, k, 0, N, nbr, d2, q,
+                                  ws_bytes - static_cast<size_t>(
+                                                 q - static_cast<char*>(ws)),
+                                  st);
+  if (rc != kOk) return rc;
+  convert(d2, N * k, nbr_d2, st);
+  ABC_LAUNCH_CHECK("knn_topk_f32");
+  return kOk;
+}
+
+size_t abc_local_cov_f32_workspace_bytes(int64_t N, int d) {
+  return al256(static_cast<size_t>(N) * d * 8) + al256(static_cast<size_t>(N) * 8) +
+         2 * al256(static_cast<size_t>(N) * d * d * 8) +
+         al256(static_cast<size_t>(N) * 8);
+}
+
+int abc_local_cov_f32(const float* X, const float* w, int64_t N, int d,
+                      const int32_t* nbr, int k, double scaling, float* covs,
+                      float* inv_covs, float* dets, void* ws, size_t ws_bytes,
+                      hipStream_t st) {
+  ABC_REQUIRE(N >= 1 && d >= 1 && k >= 1, "local_cov_f32: bad sizes");
+  ABC_REQUIRE(X && w && nbr && covs && inv_covs && dets && ws,
+              "local_cov_f32: null pointer");
+  ABC_REQUIRE(ws_bytes >= abc_local_cov_f32_workspace_bytes(N, d),
+              "local_cov_f32: workspace too small");
+  char* q = static_cast<char*>(ws);
+  double* Xd = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * d * 8);
+  double* wd = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * 8);
+  double* C = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * d * d * 8);
+  double* Ci = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(N) * d * d * 8);
+  double* dt = reinterpret_cast<double*>(q);
+  convert(X, N * d, Xd, st);
+  convert(w, N, wd, st);
+  const int rc = abc_local_cov_rows_f64(Xd, wd, N, d, nbr, k, 0, N, scaling, C,
+                                        Ci, dt, st);
+  if (rc != kOk) return rc;
+  convert(C, N * d * d, covs, st);
+  convert(Ci, N * d * d, inv_covs, st);
+  convert(dt, N, dets, st);
+  ABC_LAUNCH_CHECK("local_cov_f32");
   return kOk;
 }
 

@@ -504,6 +504,67 @@ __global__ __launch_bounds__(256) void resample_perturb_kernel(
                  sup + b, a_stride);
 }
 
+// fp32 storage form (SURVEY 8(b) abc_resample_perturb_f32): X, z, A and
+// theta in fp32, the perturbation z A accumulated in fp32 in the same order
+// as the fp64 kernel; the CDF search and the support test ((theta - lo) /
+// scale in fp64 on the fp32 theta) as in perturb_one.  12d + 25 B/proposal.
+template <int D>
+__global__ __launch_bounds__(256) void resample_perturb_f32_kernel(
+    const float* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ cdf, const double* __restrict__ u,
+    const float* __restrict__ z, const float* __restrict__ A,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    int64_t B, float* __restrict__ theta, int64_t* __restrict__ idx,
+    uint8_t* __restrict__ sup) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int64_t i = search_right(cdf, N, u[b]);
+  const int64_t ic = i < N ? i : N - 1;
+  float zz[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) zz[k] = k < d ? z[b * d + k] : 0.0f;
+  bool ok = true;
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+    if (l < d) {
+      float p = 0.0f;
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        if (k < d) p = fmaf(zz[k], A[k * d + l], p);
+      const float th = X[ic * d + l] + p;
+      theta[b * d + l] = th;
+      if (lo) {
+        const double x = (static_cast<double>(th) - lo[l]) / scale[l];
+        ok = ok && (x >= 0.0) && (x <= 1.0);
+      }
+    }
+  }
+  idx[b] = i;
+  sup[b] = ok ? 1 : 0;
+}
+
+// The production proposal draws as arrays (SURVEY 8(b) abc_philox_fill):
+// u[i] = the uniform of proposal offset + i, z[i*dz + k] its k-th normal
+// (dz = nz / nu), so abc_resample_perturb_f64 on (u, z) reproduces
+// abc_propose_philox_f64 at the same (seed, sid, offset) bit for bit.
+template <typename T>
+__global__ __launch_bounds__(256) void philox_fill_kernel(
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t nu, int64_t dz,
+    int64_t nz, double* __restrict__ u, T* __restrict__ z) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < nu) {
+    const uint64_t ui = offset + static_cast<uint64_t>(i);
+    const u32x4 b = philox_block(seed, 2 * sid, ui >> 1);
+    u[i] = (ui & 1) ? u53(b.z, b.w) : u53(b.x, b.y);
+  }
+  if (i < nz) {
+    const uint64_t zi = offset * static_cast<uint64_t>(dz) + static_cast<uint64_t>(i);
+    double c0, c1;
+    box_muller(philox_block(seed, 2 * sid + 1, zi >> 1), c0, c1);
+    z[i] = static_cast<T>((zi & 1) ? c1 : c0);
+  }
+}
+
 // Production proposals: u from stream (2*sid), z from stream (2*sid+1).
 //   u[b]   = philox_uniform(seed, 2*sid,   offset + b)
 //   z[b,k] = philox_normal (seed, 2*sid+1, (offset + b) * d + k)
@@ -679,6 +740,23 @@ static int check_dim(int d) {
   else if ((d) <= 24) { MACRO(24) } \
   else { MACRO(32) }
 
+template <typename T>
+static int philox_fill_impl(uint64_t seed, uint64_t sid, uint64_t offset,
+                            double* u, int64_t nu, T* z, int64_t nz,
+                            hipStream_t st) {
+  ABC_REQUIRE(nu >= 0 && nz >= 0, "philox_fill: negative size");
+  ABC_REQUIRE(nu == 0 || nz % nu == 0,
+              "philox_fill: nz must be a multiple of nu (rows of d normals)");
+  ABC_REQUIRE((nu == 0 || u) && (nz == 0 || z), "philox_fill: null pointer");
+  const int64_t n = nu > nz ? nu : nz;
+  if (n == 0) return kOk;
+  const int64_t dz = nu ? nz / nu : 1;
+  hipLaunchKernelGGL((philox_fill_kernel<T>), dim3(ceil_div(n, 256)), dim3(256),
+                     0, st, seed, sid, offset, nu, dz, nz, u, z);
+  ABC_LAUNCH_CHECK("philox_fill_kernel");
+  return kOk;
+}
+
 }  // namespace abc
 
 using namespace abc;
@@ -742,6 +820,41 @@ int abc_resample_perturb_f64(const double* X, int64_t N, int d,
 #undef L
   ABC_LAUNCH_CHECK("resample_perturb_kernel");
   return kOk;
+}
+
+int abc_resample_perturb_f32(const float* X, int64_t N, int d,
+                             const double* cdf, const double* u,
+                             const float* z, const float* A, const double* lo,
+                             const double* scale, int64_t B, float* theta,
+                             int64_t* idx, uint8_t* in_support,
+                             hipStream_t st) {
+  ABC_REQUIRE(check_dim(d), "resample_perturb_f32: unsupported d=%d", d);
+  ABC_REQUIRE(N > 0 && B >= 0, "resample_perturb_f32: bad sizes");
+  if (B == 0) return kOk;
+  ABC_REQUIRE(X && cdf && u && z && A && theta && idx && in_support,
+              "resample_perturb_f32: null pointer");
+  ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
+              "resample_perturb_f32: lo and scale must both be given or NULL");
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+#define L(DD)                                                                 \
+  hipLaunchKernelGGL((resample_perturb_f32_kernel<DD>), dim3(g), dim3(256), 0, \
+                     st, X, N, d, cdf, u, z, A, lo, scale, B, theta, idx,      \
+                     in_support);
+  DISPATCH_D(d, L)
+#undef L
+  ABC_LAUNCH_CHECK("resample_perturb_f32_kernel");
+  return kOk;
+}
+
+int abc_philox_fill(uint64_t seed, uint64_t sid, uint64_t offset, double* u,
+                    int64_t nu, double* z, int64_t nz, hipStream_t st) {
+  return philox_fill_impl<double>(seed, sid, offset, u, nu, z, nz, st);
+}
+
+int abc_philox_fill_f32(uint64_t seed, uint64_t sid, uint64_t offset,
+                        double* u, int64_t nu, float* z, int64_t nz,
+                        hipStream_t st) {
+  return philox_fill_impl<float>(seed, sid, offset, u, nu, z, nz, st);
 }
 
 int abc_resample_perturb_local_f64(const double* X, int64_t N, int d,

@@ -661,8 +661,9 @@ __global__ __launch_bounds__(256) void col_std_kernel(const double* __restrict__
 // C = sum_i w_i (x_i - mu)(x_i - mu)^T (unnormalised; host divides by
 // sw - sw2/sw as np.cov(aweights) does)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void moments1_kernel(const double* __restrict__ X,
-                                                       const double* __restrict__ w,
+template <typename T>
+__global__ __launch_bounds__(256) void moments1_kernel(const T* __restrict__ X,
+                                                       const T* __restrict__ w,
                                                        int64_t n, int d,
                                                        double* __restrict__ part) {
   __shared__ double red[4];
@@ -671,8 +672,10 @@ __global__ __launch_bounds__(256) void moments1_kernel(const double* __restrict_
     double s = 0.0;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * 256) {
-      const double wi = w[i];
-      s += v == 0 ? wi : (v == 1 ? wi * wi : wi * X[i * d + (v - 2)]);
+      const double wi = static_cast<double>(w[i]);
+      s += v == 0 ? wi
+                  : (v == 1 ? wi * wi
+                            : wi * static_cast<double>(X[i * d + (v - 2)]));
     }
     s = block_sum<double, 256>(s, red);
     if (threadIdx.x == 0) part[blockIdx.x * nv + v] = s;
@@ -694,8 +697,9 @@ __global__ __launch_bounds__(256) void moments1_final_kernel(const double* __res
   if (threadIdx.x < d) out[2 + threadIdx.x] = out[2 + threadIdx.x] / out[0];
 }
 
-__global__ __launch_bounds__(256) void moments2_kernel(const double* __restrict__ X,
-                                                       const double* __restrict__ w,
+template <typename T>
+__global__ __launch_bounds__(256) void moments2_kernel(const T* __restrict__ X,
+                                                       const T* __restrict__ w,
                                                        int64_t n, int d,
                                                        const double* __restrict__ mom,
                                                        double* __restrict__ part) {
@@ -724,9 +728,9 @@ __global__ __launch_bounds__(256) void moments2_kernel(const double* __restrict_
     __syncthreads();
     for (int t = threadIdx.x; t < rows * d; t += 256) {
       const int r = t / d, k = t % d;
-      tile[r * 33 + k] = X[(base + r) * d + k] - mu[k];
+      tile[r * 33 + k] = static_cast<double>(X[(base + r) * d + k]) - mu[k];
     }
-    if (threadIdx.x < rows) tw[threadIdx.x] = w[base + threadIdx.x];
+    if (threadIdx.x < rows) tw[threadIdx.x] = static_cast<double>(w[base + threadIdx.x]);
     __syncthreads();
     for (int q = 0; q < 3; ++q) {
       if (threadIdx.x + q * 256 < np) {
@@ -781,9 +785,9 @@ __device__ inline void block_sums_to(double (&v)[NV], double* __restrict__ out,
     out[q] = ((lds[0][q] + lds[1][q]) + lds[2][q]) + lds[3][q];
 }
 
-template <int D>
+template <typename T, int D>
 __global__ __launch_bounds__(256) void moments1_reg_kernel(
-    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    const T* __restrict__ X, const T* __restrict__ w, int64_t n,
     double* __restrict__ part) {
   constexpr int NV = 2 + D;
   __shared__ double lds[4][NV];
@@ -792,18 +796,19 @@ __global__ __launch_bounds__(256) void moments1_reg_kernel(
   for (int q = 0; q < NV; ++q) v[q] = 0.0;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
-    const double wi = w[i];
+    const double wi = static_cast<double>(w[i]);
     v[0] += wi;
     v[1] = fma(wi, wi, v[1]);
 #pragma unroll
-    for (int k = 0; k < D; ++k) v[2 + k] = fma(wi, X[i * D + k], v[2 + k]);
+    for (int k = 0; k < D; ++k)
+      v[2 + k] = fma(wi, static_cast<double>(X[i * D + k]), v[2 + k]);
   }
   block_sums_to<D, NV>(v, part + static_cast<int64_t>(blockIdx.x) * NV, lds);
 }
 
-template <int D>
+template <typename T, int D>
 __global__ __launch_bounds__(256) void moments2_reg_kernel(
-    const double* __restrict__ X, const double* __restrict__ w, int64_t n,
+    const T* __restrict__ X, const T* __restrict__ w, int64_t n,
     const double* __restrict__ mom, double* __restrict__ part) {
   constexpr int NP = D * (D + 1) / 2;
   __shared__ double lds[4][NP];
@@ -815,10 +820,10 @@ __global__ __launch_bounds__(256) void moments2_reg_kernel(
   for (int q = 0; q < NP; ++q) v[q] = 0.0;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
-    const double wi = w[i];
+    const double wi = static_cast<double>(w[i]);
     double xc[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) xc[k] = X[i * D + k] - mu[k];
+    for (int k = 0; k < D; ++k) xc[k] = static_cast<double>(X[i * D + k]) - mu[k];
     int q = 0;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -880,6 +885,57 @@ __global__ __launch_bounds__(256) void scale_kernel(double* __restrict__ x, int6
        i += static_cast<int64_t>(gridDim.x) * 256)
     x[i] = x[i] / dv;
 }
+
+size_t moments_ws_bytes(int d) {
+  const int np = d * (d + 1) / 2;
+  const int grid = kMomGrid > kRedGrid ? kMomGrid : kRedGrid;
+  return static_cast<size_t>(grid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
+}
+
+template <typename T>
+int moments_impl(const T* X, const T* w, int64_t n, int d, double* out,
+                 void* ws, size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(n > 0 && d >= 1 && d <= 32, "moments: bad sizes (d <= 32)");
+  ABC_REQUIRE(ws_bytes >= moments_ws_bytes(d), "moments: workspace too small");
+  double* part = static_cast<double*>(ws);
+  if (d <= 8) {
+#define L(DD)                                                                    \
+  hipLaunchKernelGGL((moments1_reg_kernel<T, DD>), dim3(kMomGrid), dim3(256), 0, st, \
+                     X, w, n, part);                                             \
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(2 + DD), dim3(64), 0, st,   \
+                     part, kMomGrid, 2 + DD, DD, 1, out);                        \
+  hipLaunchKernelGGL(moments_mu_kernel, dim3(1), dim3(64), 0, st, out, DD);      \
+  hipLaunchKernelGGL((moments2_reg_kernel<T, DD>), dim3(kMomGrid), dim3(256), 0, st, \
+                     X, w, n, out, part);                                        \
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(DD * (DD + 1) / 2),         \
+                     dim3(64), 0, st, part, kMomGrid, DD * (DD + 1) / 2, DD, 2,  \
+                     out);
+    switch (d) {
+      case 1: L(1) break;
+      case 2: L(2) break;
+      case 3: L(3) break;
+      case 4: L(4) break;
+      case 5: L(5) break;
+      case 6: L(6) break;
+      case 7: L(7) break;
+      case 8: L(8) break;
+    }
+#undef L
+    ABC_LAUNCH_CHECK("moments kernels");
+    return kOk;
+  }
+  hipLaunchKernelGGL(moments1_kernel<T>, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
+                     d, part);
+  hipLaunchKernelGGL(moments1_final_kernel, dim3(1), dim3(256), 0, st, part,
+                     kRedGrid, d, out);
+  hipLaunchKernelGGL(moments2_kernel<T>, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
+                     d, out, part);
+  hipLaunchKernelGGL(moments2_final_kernel, dim3(1), dim3(256), 0, st, part,
+                     kRedGrid, d, out);
+  ABC_LAUNCH_CHECK("moments kernels");
+  return kOk;
+}
+
 
 }  // namespace abc
 
@@ -1133,55 +1189,19 @@ int abc_column_std_f64(const double* data_T, int64_t ld, int64_t n, int S,
   return kOk;
 }
 
-size_t abc_moments_workspace_bytes(int d) {
-  const int np = d * (d + 1) / 2;
-  const int grid = kMomGrid > kRedGrid ? kMomGrid : kRedGrid;
-  return static_cast<size_t>(grid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
-}
+size_t abc_moments_workspace_bytes(int d) { return moments_ws_bytes(d); }
 
 int abc_weighted_moments_f64(const double* X, const double* w, int64_t n, int d,
                              double* out, void* ws, size_t ws_bytes,
                              hipStream_t st) {
-  ABC_REQUIRE(n > 0 && d >= 1 && d <= 32, "moments: bad sizes (d <= 32)");
-  ABC_REQUIRE(ws_bytes >= abc_moments_workspace_bytes(d),
-              "moments: workspace too small");
-  double* part = static_cast<double*>(ws);
-  if (d <= 8) {
-#define L(DD)                                                                    \
-  hipLaunchKernelGGL((moments1_reg_kernel<DD>), dim3(kMomGrid), dim3(256), 0, st, \
-                     X, w, n, part);                                             \
-  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(2 + DD), dim3(64), 0, st,   \
-                     part, kMomGrid, 2 + DD, DD, 1, out);                        \
-  hipLaunchKernelGGL(moments_mu_kernel, dim3(1), dim3(64), 0, st, out, DD);      \
-  hipLaunchKernelGGL((moments2_reg_kernel<DD>), dim3(kMomGrid), dim3(256), 0, st, \
-                     X, w, n, out, part);                                        \
-  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(DD * (DD + 1) / 2),         \
-                     dim3(64), 0, st, part, kMomGrid, DD * (DD + 1) / 2, DD, 2,  \
-                     out);
-    switch (d) {
-      case 1: L(1) break;
-      case 2: L(2) break;
-      case 3: L(3) break;
-      case 4: L(4) break;
-      case 5: L(5) break;
-      case 6: L(6) break;
-      case 7: L(7) break;
-      case 8: L(8) break;
-    }
-#undef L
-    ABC_LAUNCH_CHECK("moments kernels");
-    return kOk;
-  }
-  hipLaunchKernelGGL(moments1_kernel, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
-                     d, part);
-  hipLaunchKernelGGL(moments1_final_kernel, dim3(1), dim3(256), 0, st, part,
-                     kRedGrid, d, out);
-  hipLaunchKernelGGL(moments2_kernel, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
-                     d, out, part);
-  hipLaunchKernelGGL(moments2_final_kernel, dim3(1), dim3(256), 0, st, part,
-                     kRedGrid, d, out);
-  ABC_LAUNCH_CHECK("moments kernels");
-  return kOk;
+  return moments_impl<double>(X, w, n, d, out, ws, ws_bytes, st);
+}
+
+// fp32 storage of X and w; every sum in fp64 as above
+int abc_weighted_moments_f32(const float* X, const float* w, int64_t n, int d,
+                             double* out, void* ws, size_t ws_bytes,
+                             hipStream_t st) {
+  return moments_impl<float>(X, w, n, d, out, ws, ws_bytes, st);
 }
 
 }  // extern "C"

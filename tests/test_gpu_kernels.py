@@ -642,3 +642,191 @@ def test_local_logpdf_f32_wide_population(K, d, spread):
                               precision="f32"))
     assert np.all(np.isfinite(got))
     np.testing.assert_allclose(np.exp(got - exact), 1.0, atol=1e-5)
+
+
+# ------------------------------------- SURVEY 8(b) minimum-set entry points
+def _nat():
+    from pyabc_amd import _native as nat
+    return nat
+
+
+def _ws(nbytes):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device="cuda")
+
+
+def test_philox_fill_reproduces_production_proposals(K):
+    """abc_philox_fill hands out exactly the draws abc_propose_philox_f64
+    makes in-kernel: injecting them into abc_resample_perturb_f64 gives the
+    same indices, draws and support flags bit for bit."""
+    nat = _nat()
+    rng = np.random.default_rng(21)
+    N, d, B = 3000, 5, 20000
+    X = rng.normal(size=(N, d))
+    w = rng.uniform(size=N)
+    w /= w.sum()
+    A = ref.svd_factor(ref.mvn_fit_cov(X, w))
+    lo, sc = np.full(d, -2.0), np.full(d, 4.0)
+    cdf = K.resample_cdf(dev(w))
+    seed, sid, off = 99, 5, 777
+    th, idx, sup = K.propose_philox(dev(X), cdf, dev(A), dev(lo), dev(sc),
+                                    seed, sid, off, B)
+    u = torch.empty(B, dtype=torch.float64, device="cuda")
+    z = torch.empty(B * d, dtype=torch.float64, device="cuda")
+    nat.call("abc_philox_fill", seed, sid, off, u.data_ptr(), B, z.data_ptr(),
+             B * d, nat.stream())
+    np.testing.assert_array_equal(host(u), ref.philox_uniform(
+        seed, 2 * sid, off + B)[off:])
+    th2, idx2, sup2 = K.resample_perturb(dev(X), cdf, u, z.view(B, d), dev(A),
+                                         dev(lo), dev(sc))
+    np.testing.assert_array_equal(host(idx2), host(idx))
+    np.testing.assert_array_equal(host(th2), host(th))
+    np.testing.assert_array_equal(host(sup2), host(sup))
+    z32 = torch.empty(B * d, dtype=torch.float32, device="cuda")
+    nat.call("abc_philox_fill_f32", seed, sid, off, u.data_ptr(), B,
+             z32.data_ptr(), B * d, nat.stream())
+    np.testing.assert_array_equal(host(z32), host(z).astype(np.float32))
+
+
+def test_resample_perturb_f32(K):
+    """fp32 storage: indices bit-exact with the fp64 oracle on the same u;
+    theta within fp32 rounding of the oracle on the fp32 inputs; support
+    flags equal wherever theta is not within fp32 rounding of a bound."""
+    nat = _nat()
+    rng = np.random.default_rng(22)
+    N, d, B = 4096, 8, 30000
+    X = rng.normal(size=(N, d)).astype(np.float32)
+    w = rng.uniform(size=N)
+    w /= w.sum()
+    A = ref.svd_factor(ref.mvn_fit_cov(X.astype(np.float64), w)).astype(
+        np.float32)
+    u = rng.uniform(size=B)
+    z = rng.normal(size=(B, d)).astype(np.float32)
+    lo, sc = np.full(d, -2.5), np.full(d, 5.0)
+    cdf = K.resample_cdf(dev(w))
+    th = torch.empty((B, d), dtype=torch.float32, device="cuda")
+    idx = torch.empty(B, dtype=torch.int64, device="cuda")
+    sup = torch.empty(B, dtype=torch.uint8, device="cuda")
+    Xd, zd, Ad = (dev(a, torch.float32) for a in (X, z, A))
+    ud, lod, scd = dev(u), dev(lo), dev(sc)   # alive until the kernel ran
+    nat.call("abc_resample_perturb_f32", Xd.data_ptr(), N, d, cdf.data_ptr(),
+             ud.data_ptr(), zd.data_ptr(), Ad.data_ptr(), lod.data_ptr(),
+             scd.data_ptr(), B, th.data_ptr(), idx.data_ptr(), sup.data_ptr(),
+             nat.stream())
+    torch.cuda.synchronize()
+    idx_ref = ref.resample_indices(ref.resample_cdf(w), u)
+    np.testing.assert_array_equal(host(idx), idx_ref)
+    th_ref = X[idx_ref].astype(np.float64) + z.astype(np.float64) @ \
+        A.astype(np.float64)
+    scale = np.abs(X[idx_ref]).astype(np.float64) + np.abs(z).astype(
+        np.float64) @ np.abs(A).astype(np.float64)
+    err = np.abs(host(th) - th_ref)
+    assert np.all(err <= (d + 2) * 2.0 ** -24 * scale)
+    s_ref = ref.uniform_box_support(host(th).astype(np.float64), lo, sc)
+    np.testing.assert_array_equal(host(sup).astype(bool), s_ref)
+
+
+@pytest.mark.parametrize("d", [3, 8, 12])
+def test_weighted_moments_f32(K, d):
+    """fp32 X, w: the fp64 moments of the widened values (1e-12)."""
+    nat = _nat()
+    rng = np.random.default_rng(23 + d)
+    n = 50001
+    X = (rng.normal(size=(n, d)) * 2 + 1).astype(np.float32)
+    w = rng.uniform(0.2, 1.0, n).astype(np.float32)
+    out = torch.empty(2 + d + d * d, dtype=torch.float64, device="cuda")
+    wsb = nat.lib().abc_moments_workspace_bytes(d)
+    ws = _ws(wsb)
+    Xd, wd = dev(X, torch.float32), dev(w, torch.float32)
+    nat.call("abc_weighted_moments_f32", Xd.data_ptr(), wd.data_ptr(), n, d,
+             out.data_ptr(), ws.data_ptr(), wsb, nat.stream())
+    o = host(out)
+    X64, w64 = X.astype(np.float64), w.astype(np.float64)
+    np.testing.assert_allclose(o[0], w64.sum(), rtol=1e-12)
+    np.testing.assert_allclose(o[1], (w64 ** 2).sum(), rtol=1e-12)
+    mu = (w64[:, None] * X64).sum(0) / w64.sum()
+    np.testing.assert_allclose(o[2:2 + d], mu, rtol=1e-12)
+    C = ((X64 - mu) * w64[:, None]).T @ (X64 - mu)
+    np.testing.assert_allclose(o[2 + d:].reshape(d, d), C, rtol=1e-11,
+                               atol=1e-9)
+
+
+@pytest.mark.parametrize("d", [1, 4, 8, 20])
+def test_kde_logsum(K, d):
+    """abc_kde_logsum_{f32,f64}: log_offset + log sum_j exp(logw_j -
+    |y_i - y_j|^2 / 2) on pre-whitened rows: 1e-12 relative
+    for fp64, 1e-5 relative (of the sum) for fp32."""
+    nat = _nat()
+    rng = np.random.default_rng(30 + d)
+    N, M = 3001, 700
+    Yp = rng.normal(size=(N, d)) * 1.5
+    Yn = np.concatenate([Yp[:M - 50] + 0.1 * rng.normal(size=(M - 50, d)),
+                         rng.normal(size=(50, d)) * 4])
+    logw = np.log(rng.uniform(0.1, 1.0, N)) - 3.0
+    off = 0.75
+    d2 = ((Yn[:, None, :] - Yp[None, :, :]) ** 2).sum(-1)
+    a = logw[None, :] - 0.5 * d2
+    m = a.max(1)
+    want = off + m + np.log(np.exp(a - m[:, None]).sum(1))
+    for T, name, tol in ((np.float64, "f64", 1e-12), (np.float32, "f32", 1e-5)):
+        tt = torch.float64 if T is np.float64 else torch.float32
+        wsb = getattr(nat.lib(), f"abc_kde_logsum_workspace_bytes_{name}")(
+            M, N, d)
+        ws = _ws(wsb)
+        out = torch.empty(M, dtype=tt, device="cuda")
+        a1, a2, a3 = (dev(x.astype(T), tt) for x in (Yn, Yp, logw))
+        nat.call(f"abc_kde_logsum_{name}", a1.data_ptr(), a2.data_ptr(),
+                 a3.data_ptr(), M, N, d, float(off), out.data_ptr(),
+                 ws.data_ptr(), wsb, nat.stream())
+        got = host(out).astype(np.float64)
+        if T is np.float32:
+            # the reference value of the fp32-rounded inputs
+            Yn32, Yp32, lw32 = (x.astype(np.float32).astype(np.float64)
+                                for x in (Yn, Yp, logw))
+            d2 = ((Yn32[:, None, :] - Yp32[None, :, :]) ** 2).sum(-1)
+            a = lw32[None, :] - 0.5 * d2
+            m = a.max(1)
+            want32 = np.float32(off) + m + np.log(np.exp(a - m[:, None]).sum(1))
+            err = np.abs(got - want32)
+            bad = err > tol + 4e-7 * np.abs(want32)
+            assert not bad.any(), (name, np.flatnonzero(bad)[:5],
+                                   got[bad][:5], want32[bad][:5])
+        else:
+            np.testing.assert_allclose(got, want, rtol=tol, atol=tol)
+
+
+def test_knn_topk_and_local_cov_f32(K):
+    """fp32 storage kNN / local covariances: neighbour sets of the fp32
+    points equal a brute force; covariances equal the fp64 kernel's on the
+    widened points rounded to fp32."""
+    nat = _nat()
+    rng = np.random.default_rng(41)
+    N, d, k = 1500, 6, 20
+    X = rng.normal(size=(N, d)).astype(np.float32)
+    w = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    nbr = torch.empty((N, k), dtype=torch.int32, device="cuda")
+    d2 = torch.empty((N, k), dtype=torch.float32, device="cuda")
+    wsb = nat.lib().abc_knn_topk_f32_workspace_bytes(N, d, k)
+    ws = _ws(wsb)
+    Xd, wd = dev(X, torch.float32), dev(w, torch.float32)
+    nat.call("abc_knn_topk_f32", Xd.data_ptr(), N, d, k, nbr.data_ptr(),
+             d2.data_ptr(), ws.data_ptr(), wsb, nat.stream())
+    want = ref.knn_indices(X.astype(np.float64), k)
+    got = host(nbr)
+    for i in range(N):
+        assert set(got[i]) == set(want[i])
+    X64 = X.astype(np.float64)
+    dd = ((X64[want] - X64[:, None, :]) ** 2).sum(-1)
+    np.testing.assert_allclose(np.sort(host(d2), 1), np.sort(dd, 1),
+                               rtol=1e-6)
+    C = torch.empty((N, d, d), dtype=torch.float32, device="cuda")
+    Ci = torch.empty_like(C)
+    dt = torch.empty(N, dtype=torch.float32, device="cuda")
+    wsb = nat.lib().abc_local_cov_f32_workspace_bytes(N, d)
+    ws = _ws(wsb)
+    nat.call("abc_local_cov_f32", Xd.data_ptr(), wd.data_ptr(), N, d,
+             nbr.data_ptr(), k, 1.0, C.data_ptr(), Ci.data_ptr(),
+             dt.data_ptr(), ws.data_ptr(), wsb, nat.stream())
+    covs, invs, dets = ref.local_covs(X64, w.astype(np.float64), host(nbr))
+    np.testing.assert_allclose(host(C), covs, rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(host(dt), dets, rtol=1e-5)
+    np.testing.assert_allclose(host(Ci), invs, rtol=1e-4, atol=1e-4)

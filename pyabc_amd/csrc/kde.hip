@@ -275,13 +275,13 @@ __global__ __launch_bounds__(256) void kde_finalize_kernel(
     const double* __restrict__ partial, int64_t M, int nseg,
     const double* __restrict__ lw2max, double log_const,
     double* __restrict__ out_logpd, int* __restrict__ n_fix,
-    int* __restrict__ fix_rows) {
+    int* __restrict__ fix_rows, double thr) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= M) return;
   double S = 0.0;
   for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * M + i];
   const double off = kLn2 * (*lw2max) + log_const;
-  if (!(S >= KdeCfg<T>::underflow)) {
+  if (!(S >= thr)) {
     const int slot = atomicAdd(n_fix, 1);
     fix_rows[slot] = static_cast<int>(i);
     out_logpd[i] = -INFINITY;
@@ -486,7 +486,8 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
   }
   hipLaunchKernelGGL((kde_finalize_kernel<T>), dim3(ceil_div(M, 256)),
                      dim3(256), 0, stream, partial, M, p.nseg, lw2max,
-                     log_const, out_logpd, n_fix, fix_rows);
+                     log_const, out_logpd, n_fix, fix_rows,
+                     KdeCfg<T>::underflow);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
   hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(64), dim3(256), 0, stream,
                      Ynew, P, npad, lw2max, log_const, n_fix, fix_rows,
@@ -723,9 +724,12 @@ int kde_finish_mfma(const double* partial, int64_t M, int nseg,
                     const double* Ynew, const double* P, int64_t npad, int d,
                     const double* lw2max, double log_const, double* out_logpd,
                     int* n_fix, int* fix_rows, hipStream_t stream) {
+  // the MFMA pass re-evaluates rows below 2^-32 exactly: its folded
+  // exponent error grows with the dominant |e| (kde_mfma.hip, kFoldKL)
+  constexpr double kMfmaFixupSum = 2.3283064365386963e-10;  // 2^-32
   hipLaunchKernelGGL((kde_finalize_kernel<float>), dim3(ceil_div(M, 256)),
                      dim3(256), 0, stream, partial, M, nseg, lw2max,
-                     log_const, out_logpd, n_fix, fix_rows);
+                     log_const, out_logpd, n_fix, fix_rows, kMfmaFixupSum);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
   switch (padded_dim(d)) {
 #define CASE(DD)                                                              \

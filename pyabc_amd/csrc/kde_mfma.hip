@@ -285,23 +285,47 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
   store_frags<D, false>(B, i, y1, y2, y3, h, l);
 }
 
-// one (32-row tile, i-tile) product: hi (exact) and lo accumulators
+// Folded accumulation (KL <= kFoldKL, i.e. D <= 8, the VALU-bound shapes):
+// the exact hi products first, then the lo chain accumulated ON TOP of them
+// in the same accumulator, so the MFMA delivers e = hi + lo itself and the
+// VALU add per pair disappears (143.6 vs 156.6 ms at N = M = 1e6, d = 8).
+// hi is exact in any order (multiples of G below 2^24 G); each of the KL lo
+// MFMAs then rounds at |e| instead of once, so a term's exponent carries
+// about (KL + 1) / 2 ulps of |e| instead of 1/2: relative error ~8e-8 |e|
+// at KL = 4.  A row's error is the t-weighted mean of its terms' errors,
+// bounded by ~8e-8 log2(N / S) for a row sum S; rows with S < 2^-32 (dominant
+// exponents beyond ~32) take the exact fp64 fixup (kMfmaFixupSum), so the
+// bound is ~4e-6 at N = 1e6 (measured: tests/test_gpu_fullsize.py, DESIGN
+// section 4).  The opt-in LDS / DMA variants keep the split order.
+constexpr int kFoldKL = 4;
+
+// one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
+// folded e in hi
 template <int KH, int KL>
 __device__ __forceinline__ void mfma_step(const bf16x8* a, const bf16x8* b,
                                           f32x16& hi, f32x16& lo) {
   hi = f32x16{};
-  lo = f32x16{};
 #pragma unroll
   for (int c = 0; c < KH; ++c)
     hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
+  if constexpr (KL <= kFoldKL) {
 #pragma unroll
-  for (int c = 0; c < KL; ++c)
-    lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0, 0, 0);
+    for (int c = 0; c < KL; ++c)
+      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], hi, 0,
+                                                   0, 0);
+  } else {
+    lo = f32x16{};
+#pragma unroll
+    for (int c = 0; c < KL; ++c)
+      lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0,
+                                                   0, 0);
+  }
 }
 
 // sum of 2^(hi+lo) over the lane's 16 values: 16 independent exps, then a
 // fixed pairwise tree (v, v+8), (v, v+4), (v, v+2), (v, v+1)
-__device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
+__device__ __forceinline__ float tile_sum_split(const f32x16& hi,
+                                                const f32x16& lo) {
   float e[16];
 #pragma unroll
   for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v] + lo[v]);
@@ -311,6 +335,28 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
     for (int v = 0; v < w; ++v) e[v] += e[v + w];
   return e[0];
 }
+
+// the same after mfma_step (folded: e is in hi)
+template <int KL>
+__device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
+  if constexpr (KL > kFoldKL) {
+    return tile_sum_split(hi, lo);
+  } else {
+    float e[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int v = 0; v < w; ++v) e[v] += e[v + w];
+    return e[0];
+  }
+}
+
+// VALU instructions of one step's sum (16 exps + the tree + the row add,
+// plus the 16 hi + lo adds when not folded): the sched_group_barrier share
+template <int KL>
+constexpr int step_valu() { return KL <= kFoldKL ? 32 : 48; }
 
 // Ablation forms of one step (tuning diagnostics only, ABC_KDE_MFMA_ABL):
 // 1 no exp, 2 no MFMA, 3 neither (adds only), 4 MFMA only.  The results are
@@ -329,6 +375,16 @@ __device__ __forceinline__ void abl_step(const bf16x8* a, const bf16x8* b,
 #pragma unroll
     for (int c = 0; c < KH; ++c)
       hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
+  } else if constexpr (ABL == 6) {
+    // fold the other way: the exact hi products first, then the lo chain
+    // accumulated on top of them (rounding at |e|, not at the hi partials)
+    hi = f32x16{};
+#pragma unroll
+    for (int c = 0; c < KH; ++c)
+      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < KL; ++c)
+      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], hi, 0, 0, 0);
   } else if constexpr (ABL == 2 || ABL == 3) {
     asm volatile("" : "+v"(hi), "+v"(lo));
   } else {
@@ -337,10 +393,10 @@ __device__ __forceinline__ void abl_step(const bf16x8* a, const bf16x8* b,
 }
 // (the ablated sum is consumed by an empty asm and replaced by 1, so no row
 // reaches the exact fixup)
-template <int ABL>
+template <int ABL, int KL>
 __device__ __forceinline__ float abl_sum(const f32x16& hi, const f32x16& lo) {
-  if constexpr (ABL == 0) return tile_sum(hi, lo);
-  if constexpr (ABL == 5) {
+  if constexpr (ABL == 0) return tile_sum<KL>(hi, lo);
+  if constexpr (ABL == 5 || ABL == 6) {
     float e[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v]);
@@ -352,7 +408,7 @@ __device__ __forceinline__ float abl_sum(const f32x16& hi, const f32x16& lo) {
   }
   float r;
   if constexpr (ABL == 2) {
-    r = tile_sum(hi, lo);
+    r = tile_sum_split(hi, lo);
   } else if constexpr (ABL == 4) {
     r = hi[0] + lo[0];
   } else {
@@ -431,11 +487,11 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += abl_sum<ABL>(hi[q & 1], lo[q & 1]);
+          sacc[q % IB] += abl_sum<ABL, KL>(hi[q & 1], lo[q & 1]);
           if constexpr (SCHED) {
             // interleave: each MFMA of step q+1 followed by a share of step
-            // q's 48 VALU (16 add, 16 exp, 16 tree/row adds)
-            constexpr int VPG = (48 + KT - 1) / KT;
+            // q's VALU (16 exp, 16 tree/row adds, 16 hi + lo adds unless folded)
+            constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;
             if (q + 1 < 2 * IB) {
 #pragma unroll
               for (int m = 0; m < KT; ++m) {
@@ -443,7 +499,7 @@ __device__ __forceinline__ void kde_mfma_body(
                 __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
               }
             } else {
-              __builtin_amdgcn_sched_group_barrier(0x002, 48, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, step_valu<KL>(), 0);
             }
           }
         }
@@ -454,7 +510,7 @@ __device__ __forceinline__ void kde_mfma_body(
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
           abl_step<ABL, KH, KL>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += abl_sum<ABL>(hi, lo);
+          sacc[q % IB] += abl_sum<ABL, KL>(hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -501,7 +557,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
   constexpr int NS = 2 * IB;                  // steps per 64-row chunk
-  constexpr int VPG = (48 + KT - 1) / KT;     // VALU per MFMA gap
+  constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;  // VALU per gap
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int s = blockIdx.x % split;
@@ -553,7 +609,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[1][c] = an[(KT + c) * 64];
           }
-          sacc[q % IB] += tile_sum(hi[q & 1], lo[q & 1]);
+          sacc[q % IB] += tile_sum<KL>(hi[q & 1], lo[q & 1]);
           if (q + 1 < NS || more) {
 #pragma unroll
             for (int m = 0; m < KT; ++m) {
@@ -644,9 +700,9 @@ __global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
         if (q + 1 < 2 * IB)
           abl_step<ABL, KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
                             hi[(q + 1) & 1], lo[(q + 1) & 1]);
-        sacc[q % IB] += abl_sum<ABL>(hi[q & 1], lo[q & 1]);
+        sacc[q % IB] += abl_sum<ABL, KL>(hi[q & 1], lo[q & 1]);
         if constexpr (SCHED) {
-          constexpr int VPG = (48 + KT - 1) / KT;
+          constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;
           if (q + 1 < 2 * IB) {
 #pragma unroll
             for (int m = 0; m < KT; ++m) {
@@ -654,7 +710,7 @@ __global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
               __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
             }
           } else {
-            __builtin_amdgcn_sched_group_barrier(0x002, 48, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, step_valu<KL>(), 0);
           }
         }
       }
@@ -739,7 +795,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_dma_kernel(
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         }
-        sacc += tile_sum(hi, lo);
+        sacc += tile_sum_split(hi, lo);
       }
       S += static_cast<double>(sacc);
       buf ^= 1;  // the next top barrier also ends every read of this buffer
@@ -821,7 +877,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_kernel(
         for (int c = 0; c < KL; ++c)
           lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               Ab[(tile * KT + KH + c) * 64 + lane], bq[it][KH + c], lo, 0, 0, 0);
-        sacc[it] += tile_sum(hi, lo);
+        sacc[it] += tile_sum_split(hi, lo);
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
@@ -954,13 +1010,14 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if constexpr (D == 8 && IB == 3) {
     int abl = 0;
     if (const char* env = getenv("ABC_KDE_MFMA_ABL")) abl = atoi(env);
-    if (abl >= 1 && abl <= 5) {
+    if (abl >= 1 && abl <= 6) {
 #define ABLK(A)                                                                \
   hipLaunchKernelGGL((kde_mfma_abl_kernel<Mk<D>::KH, Mk<D>::KL, A>), dim3(grid), \
                      dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,     \
                      p.spb, p.jseg, partial)
       if (abl == 1) ABLK(1);
       else if (abl == 5) ABLK(5);
+      else if (abl == 6) ABLK(6);
       else if (abl == 2) ABLK(2);
       else if (abl == 3) ABLK(3);
       else ABLK(4);

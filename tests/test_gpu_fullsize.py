@@ -137,8 +137,13 @@ def _check(d, N, gens, n_random, n_tail, n_edge, tag):
         - 0.5 * (rank * ref.LOG_2PI + log_pdet)
     err_ref = _rel_err(lp_rows_mfma, lp_ref)
     err_64_ref = _rel_err(lp_rows_64, lp_ref)
+    # rows the MFMA pass hands to the exact fp64 fixup (sum below 2^-32 of
+    # the largest weight's scale)
+    off = math.log(2) * float(fit.packed.lw2max.item()) + fit.packed.log_const
+    n_fix = int(np.sum(lp64 - off < -32 * math.log(2)))
     stats = dict(
         tag=tag, d=d, N=int(fit.n), M=int(M), gens=gens, grid_g=g,
+        n_fixup_rows=n_fix,
         max_abs_y_new=float(np.abs(Yn).max()),
         max_rel_err_all_rows_vs_f64=float(err_all.max()),
         p99_rel_err_all_rows_vs_f64=float(np.quantile(err_all, 0.99)),

@@ -82,7 +82,8 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
 
     The pass is bound by the SIMD's instruction issue: per 32x32 tile of
     pairs a wave issues MFMAs (the d-dimensional exponent on the matrix
-    cores) and VALU (hi+lo add, v_exp_f32, row-sum add).  The ceiling is
+    cores) and VALU (v_exp_f32, row-sum add; plus the hi+lo add when the
+    accumulation is not folded, d > 8).  The ceiling is
     the instruction mix COUNTED by PMC (profiles/r02_kde_pmc.json: per-tile
     SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32, SQ_INSTS_MFMA) priced at the
     guide's per-instruction SIMD cycles (plain VALU 2, transcendental 8,
@@ -104,8 +105,10 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         src = "profiles/r02_kde_pmc.json (rocprofv3 --pmc, per-tile counts)"
     else:   # static count of the kernel's per-tile code
         D = K.padded_dim(d)
-        F = (D + 6 + 15) // 16 + (7 * D + 4 + 15) // 16
-        V, T = 48.0, 16.0
+        KL = (7 * D + 4 + 15) // 16
+        F = (D + 6 + 15) // 16 + KL
+        # folded accumulation (KL <= 4): no hi + lo add (kde_mfma.hip)
+        V, T = (32.0 if KL <= 4 else 48.0), 16.0
         src = "static per-tile instruction count (no PMC file for this d)"
     cyc = max(2 * (V - T) + 8 * T + 8 * F, 32 * F)
     t_ceil = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
@@ -115,8 +118,9 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     return {
         "bound": "valu",
         "kernel": "kde_mfma_kernel (exact-grid bf16 pieces: "
-                  "v_mfma_f32_32x32x16_bf16 for the d-dim exponent, "
-                  "v_add + v_exp_f32 + v_add per pair on the VALU)",
+                  "v_mfma_f32_32x32x16_bf16 for the d-dim exponent -- at "
+                  "d <= 8 hi and lo in one accumulator -- then v_exp_f32 + "
+                  "the row-sum add per pair on the VALU)",
         "achieved": achieved_tf,
         "peak": peak_tf,
         "unit": "TFLOP/s",

@@ -806,6 +806,106 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_dma_kernel(
   }
 }
 
+// MFMA-bound form for d > 8.  Per 32x32 tile a wave runs KT = KH + KL
+// MFMAs; with A streamed per wave from L2 (kde_mfma_kernel) every MFMA needs
+// 1 KiB of A per 32 cycles, i.e. 128 B/clk/CU at IB = 1 and 64 at IB = 2 --
+// the vector L1's whole bandwidth, so the matrix pipe ran at ~50 % (21 ms at
+// N = M = 262144, d = 20).  Here the A fragments of each 64-row chunk are
+// copied ONCE per block into LDS by LDS-DMA (double-buffered, one barrier
+// per chunk), and each fragment read back from LDS (ds_read_b128) feeds IB
+// MFMAs, one per i-tile held in registers: LDS serves 128/IB B/clk/CU, L2
+// only 1/(kWaves*IB) of the A bytes.  A wave holds B (IB*KT fragments), the
+// 2*IB accumulators and one A fragment in flight, so two waves share a SIMD
+// and one wave's exp block runs beside another's MFMA chain.  Per-lane
+// arithmetic and summation order are those of kde_mfma_body (split hi / lo
+// accumulators, tile 0 then tile 1 of each chunk): the rows are
+// bit-identical to kde_mfma_kernel's.
+template <int KH, int KL, int IB, bool FOLD>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    // fragment f of a chunk = contiguous 1 KiB at Aseg + (chunk*2*KT + f)*64
+    auto fill = [&](int buf, int jc) {
+      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+      for (int f = wave; f < CH; f += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            src + f * 64 + lane,
+            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+    };
+    __syncthreads();  // the previous segment's readers are done with As
+    if (nj > 0) fill(0, 0);
+    int buf = 0;
+    for (int jc = 0; jc < nj; jc += 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // chunk jc landed (each wave waited for its own pieces) and every wave
+      // is done with chunk jc - 64, whose buffer is refilled now
+      __syncthreads();
+      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      const bf16x8(*Ab)[64] = As[buf];
+      float sacc[IB];
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+#pragma unroll
+      for (int tile = 0; tile < 2; ++tile) {
+        f32x16 hi[IB], lo[IB];
+#pragma unroll
+        for (int t = 0; t < IB; ++t) hi[t] = lo[t] = f32x16{};
+#pragma unroll
+        for (int c = 0; c < KT; ++c) {
+          const bf16x8 a = Ab[tile * KT + c][lane];
+#pragma unroll
+          for (int t = 0; t < IB; ++t) {
+            if (c < KH || FOLD)
+              hi[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t][c], hi[t],
+                                                              0, 0, 0);
+            else
+              lo[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t][c], lo[t],
+                                                              0, 0, 0);
+          }
+          // one fragment read ahead of its IB MFMAs, no early hoisting
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, IB, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < IB; ++t)
+          sacc[t] += FOLD ? tile_sum<0>(hi[t], lo[t]) : tile_sum_split(hi[t], lo[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+      buf ^= 1;  // the next top barrier also ends every read of this buffer
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
 // The same pass with the A fragments of each 64-row chunk staged once per
 // block in LDS (double-buffered) and shared by the kWaves waves, which walk
 // the same j-segments.  Where the register version needs more than 256
@@ -974,6 +1074,26 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if (const char* env = getenv("ABC_KDE_MFMA_SW")) sw = atoi(env) != 0;
   int dmab = 0;  // LDS-DMA shared A: 1 = 4 waves per block, 2 = 8 waves
   if (const char* env = getenv("ABC_KDE_MFMA_DMAB")) dmab = atoi(env);
+  // LDS-DMA A with IB MFMAs per LDS fragment: the MFMA-bound shapes (d > 8)
+  // (default at d > 8: d = 20 21.5 -> 20.4 ms, d = 12 18.6 -> 15.1, d = 24
+  // 27.0 -> 23.8 at N = M = 262144, rows bit-identical; tools/kde_variants.py)
+  bool lds2 = D > 8;
+  if (const char* env = getenv("ABC_KDE_MFMA_LDS2")) lds2 = atoi(env) != 0;
+  if constexpr (D > 8) {
+    if (lds2) {
+      bool fold = false;
+      if (const char* env = getenv("ABC_KDE_MFMA_FOLD")) fold = atoi(env) != 0;
+      if (fold)
+        hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
+                           dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr,
+                           npad, p.split, p.spb, p.jseg, partial);
+      else
+        hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
+                           dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr,
+                           npad, p.split, p.spb, p.jseg, partial);
+      return;
+    }
+  }
   if constexpr (D <= 8) {
     if (dmab == 1 || dmab == 2) {
 #define DMAB(NW, SC)                                                           \

@@ -80,4 +80,37 @@ __device__ inline void box_muller(u32x4 b, double& z0, double& z1) {
   z1 = r * s;
 }
 
+// normals zi0 .. zi0 + d - 1 of one stream into z[0 .. d) (z[k] = 0 for
+// k >= d): normal zi is branch zi & 1 of the Box-Muller pair of block zi / 2,
+// and each pair the range touches is computed ONCE (the per-element form
+// evaluated every pair twice and kept one branch).  Same values bit for bit.
+template <int D>
+__device__ inline void philox_normals(uint64_t seed, uint64_t stream,
+                                      uint64_t zi0, int d, double (&z)[D]) {
+#pragma unroll
+  for (int k = 0; k < D; ++k) z[k] = 0.0;
+  const uint64_t p0 = zi0 >> 1;
+  if ((zi0 & 1) == 0) {  // pair q covers k = 2q (cos), 2q + 1 (sin)
+#pragma unroll
+    for (int q = 0; q < (D + 1) / 2; ++q) {
+      if (2 * q < d) {
+        double c0, c1;
+        box_muller(philox_block(seed, stream, p0 + q), c0, c1);
+        z[2 * q] = c0;
+        if (2 * q + 1 < D && 2 * q + 1 < d) z[2 * q + 1] = c1;
+      }
+    }
+  } else {  // pair q covers k = 2q - 1 (cos), 2q (sin)
+#pragma unroll
+    for (int q = 0; q < D / 2 + 1; ++q) {
+      if (2 * q - 1 < d) {
+        double c0, c1;
+        box_muller(philox_block(seed, stream, p0 + q), c0, c1);
+        if (q > 0 && 2 * q - 1 < D) z[2 * q - 1] = c0;
+        if (2 * q < D && 2 * q < d) z[2 * q] = c1;
+      }
+    }
+  }
+}
+
 }  // namespace abc

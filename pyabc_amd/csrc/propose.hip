@@ -582,18 +582,7 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
   const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
   const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
   double zz[D];
-  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    if (k < d) {
-      const uint64_t zi = zi0 + k;
-      double c0, c1;
-      box_muller(philox_block(seed, 2 * sid + 1, zi >> 1), c0, c1);
-      zz[k] = (zi & 1) ? c1 : c0;
-    } else {
-      zz[k] = 0.0;
-    }
-  }
+  philox_normals<D>(seed, 2 * sid + 1, ui * static_cast<uint64_t>(d), d, zz);
   perturb_one<D>(X, N, d, cdf, u, zz, A, lo, scale, theta + b * d, idx + b,
                  sup + b, 0, tab, log2k);
 }

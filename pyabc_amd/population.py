@@ -1,5 +1,8 @@
 """Particles and populations (API of pyabc/population.py:1-286), plus the
 columnar device population the GPU sampler produces."""
+import concurrent.futures
+import threading
+
 import numpy as np
 import pandas as pd
 import torch
@@ -140,6 +143,7 @@ class ColumnarPopulation:
 
     def __init__(self, theta, w, d, names, stats_T=None, stat_keys=None,
                  m=0, normalize=True):
+        self._pending = None      # host offload in flight (to_host)
         self.theta = theta
         self.d = d
         self.names = list(names)
@@ -158,12 +162,46 @@ class ColumnarPopulation:
 
     def to_host(self):
         """Move the columns to host memory (History keeps only the newest
-        population on the device); readers work on either."""
-        for name in ("theta", "w", "d", "stats_T"):
-            t = getattr(self, name)
-            if t is not None and t.is_cuda:
-                setattr(self, name, t.cpu())
+        population on the device); readers work on either.
+
+        The copy runs asynchronously: a worker thread copies the columns on
+        a side stream (after an event recorded on the caller's stream), so
+        the next generation's kernels are not held behind a D2H copy of the
+        statistics matrix (80 MB at N = 1e5, S = 100).  The first access to
+        a column waits for it."""
+        if self._pending is not None:
+            return self
+        cols = {n: self.__dict__.get("_" + n) for n in _COLUMNS}
+        if not any(t is not None and t.is_cuda for t in cols.values()):
+            return self
+        dev = next(t.device for t in cols.values()
+                   if t is not None and t.is_cuda)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+
+        def copy():
+            with torch.cuda.device(dev):
+                s = _side_stream(dev)
+                with torch.cuda.stream(s):
+                    s.wait_event(ev)
+                    return {n: (t.to("cpu") if t is not None and t.is_cuda
+                                else t) for n, t in cols.items()}
+
+        self._pending = _offload_pool().submit(copy)
         return self
+
+    def device_bytes(self):
+        """Bytes of the columns held in device memory (0 once offloaded)."""
+        if self._pending is not None:
+            return 0
+        return sum(t.numel() * t.element_size()
+                   for t in (self.__dict__.get("_" + n) for n in _COLUMNS)
+                   if t is not None and t.is_cuda)
+
+    def _finish_offload(self):
+        fut, self._pending = self._pending, None
+        for n, t in fut.result().items():
+            self.__dict__["_" + n] = t
 
     def get_model_probabilities(self):
         return self._model_probabilities
@@ -211,3 +249,45 @@ class ColumnarPopulation:
             out.append(Particle(self.m, Parameter(dict(zip(self.names, th[i]))),
                                 float(w[i]), ss, [float(d[i])]))
         return out
+
+
+_COLUMNS = ("theta", "w", "d", "stats_T")
+_pool = None
+_side = {}
+_pool_lock = threading.Lock()
+
+
+def _offload_pool():
+    global _pool
+    with _pool_lock:
+        if _pool is None:
+            _pool = concurrent.futures.ThreadPoolExecutor(
+                max_workers=1, thread_name_prefix="abc-offload")
+        return _pool
+
+
+def _side_stream(dev):
+    with _pool_lock:
+        if dev not in _side:
+            _side[dev] = torch.cuda.Stream(device=dev)
+        return _side[dev]
+
+
+def _column(name):
+    key = "_" + name
+
+    def get(self):
+        if self.__dict__.get("_pending") is not None:
+            self._finish_offload()
+        return self.__dict__.get(key)
+
+    def set(self, value):
+        if self.__dict__.get("_pending") is not None:
+            self._finish_offload()
+        self.__dict__[key] = value
+
+    return property(get, set)
+
+
+for _n in _COLUMNS:
+    setattr(ColumnarPopulation, _n, _column(_n))

@@ -33,6 +33,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import pandas as pd
+import torch
 
 from .population import ColumnarPopulation, Particle, Population
 from .parameters import Parameter
@@ -42,6 +43,18 @@ from .acceptor import save_dict_to_json, load_dict_from_json  # noqa: F401
 # History objects by db id, held weakly (a finished run's device and host
 # populations are freed with its last reference)
 _REGISTRY = weakref.WeakValueDictionary()
+
+
+def _device_budget():
+    """Device bytes a History may keep in older populations
+    (``ABC_HISTORY_DEVICE_BYTES``, default a tenth of the device memory)."""
+    env = os.environ.get("ABC_HISTORY_DEVICE_BYTES")
+    if env is not None:
+        return int(float(env))
+    if not torch.cuda.is_available():
+        return 0
+    return torch.cuda.get_device_properties(
+        torch.cuda.current_device()).total_memory // 10
 
 # CREATE TABLE statements as SQLAlchemy emits them for db_model.py:35-127
 _DDL = [
@@ -506,6 +519,20 @@ class History:
         if env_world() > 1:
             agree_int(self._id)
 
+    def _offload_over_budget(self, t_new):
+        held = []
+        for t_old in sorted(self._pops):
+            pop = self._pops[t_old]["population"]
+            if t_old != t_new and hasattr(pop, "device_bytes"):
+                held.append((t_old, pop))
+        total = sum(p.device_bytes() for _, p in held)
+        budget = _device_budget()
+        for _, pop in held:          # oldest first
+            if total <= budget:
+                break
+            total -= pop.device_bytes()
+            pop.to_host()
+
     def update_nr_samples(self, t=PRE_TIME, nr_samples=0):
         if t == History.PRE_TIME:
             self._pre_nr_samples = nr_samples
@@ -525,12 +552,13 @@ class History:
         self._pops[t] = dict(population=population, eps=current_epsilon,
                              n_sim=nr_simulations, names=model_names,
                              end=datetime.datetime.now())
-        # only the newest population stays on the device (the next fit and
-        # the loop read it); earlier ones move to host memory, where every
-        # reader still finds them
-        for t_old, e in self._pops.items():
-            if t_old != t and hasattr(e["population"], "to_host"):
-                e["population"].to_host()
+        # populations stay on the device up to a byte budget (default a tenth
+        # of the device's memory: ~29 GB on an MI355X, ten generations of
+        # N = 1e6, S = 100 statistics); beyond it the oldest move to host
+        # memory (asynchronously, ColumnarPopulation.to_host), where every
+        # reader still finds them.  The newest always stays (the next fit
+        # and the loop read it).
+        self._offload_over_budget(t)
         if self._sql is None or self._readonly:
             return
         mp = population.get_model_probabilities()

@@ -95,6 +95,40 @@ def test_config2_adaptive_mad_batch_path(pa):
     _check_against_reference(g, "c2", 3, eps, _post_stats(h, names), d)
 
 
+@pytest.mark.parametrize("budget", ["0", "1e12"])
+def test_history_device_budget_offload(pa, monkeypatch, budget):
+    """History keeps older populations on the device up to
+    ABC_HISTORY_DEVICE_BYTES and offloads the oldest beyond it (an async
+    copy on a side stream); the readers return the same values either way,
+    and the newest population always stays on the device."""
+    monkeypatch.setenv("ABC_HISTORY_DEVICE_BYTES", budget)
+    g = load_golden("e2e_stats")
+    A, x0v = g["A2"], g["x0_2"]
+    S, d = A.shape
+    keys = [f"y{k:03d}" for k in range(S)]
+    names = [f"p{k}" for k in range(d)]
+    model = pa.LinearGaussianModel(A, None, 0.5, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2), population_size=500,
+                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.GPUBatchSampler(seed=3))
+    abc.new(f"mem://budget{budget}", dict(zip(keys, x0v)))
+    h = abc.run(max_nr_populations=4)
+    pops = [h._pops[t]["population"] for t in sorted(h._pops)]
+    on_dev = [p.device_bytes() > 0 for p in pops]
+    assert on_dev[-1]
+    assert all(on_dev) == (budget != "0")
+    # readers see identical values whether a population was offloaded or not
+    for t, p in zip(sorted(h._pops), pops):
+        df, w = h.get_distribution(0, t)
+        assert p.theta.device.type == ("cuda" if on_dev[t] else "cpu")
+        np.testing.assert_array_equal(df[names].values, p.theta.cpu().numpy())
+        w = w.cpu().numpy() if torch.is_tensor(w) else np.asarray(w)
+        np.testing.assert_array_equal(w, p.w.cpu().numpy())
+        st = h.get_weighted_sum_stats(t)
+        assert len(st[0]) == 500
+
+
 def test_config2_full_size_N1e5(pa):
     """C2 at its BASELINE size (N = 1e5, one MI355X): AdaptivePNormDistance
     (MAD), QuantileEpsilon(0.5), 4 generations.  The reference cannot run

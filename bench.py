@@ -86,10 +86,11 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     accumulation is not folded, d > 8).  The ceiling is
     the instruction mix COUNTED by PMC (profiles/r02_kde_pmc.json: per-tile
     SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32, SQ_INSTS_MFMA) priced at the
-    guide's per-instruction SIMD cycles (plain VALU 2, transcendental 8,
+    guide's per-instruction SIMD issue cycles (plain or packed VALU 4,
+    transcendental 8,
     MFMA issue 8 / matrix pipe 32) at the 2.4 GHz peak clock on 1024 SIMDs:
 
-        t_ceiling = tiles * max(2 V + 8 T + 8 F, 32 F) / (1024 * 2.4e9)
+        t_ceiling = tiles * max(4 (V - T) + 8 T + 8 F, 32 F) / (1024 * 2.4e9)
 
     frac = t_ceiling / t_launch (<= 1).  achieved / peak are the same ratio
     in SURVEY 8(d)'s algorithmic unit (3d+4 FLOP per pair).  The FP32
@@ -110,7 +111,7 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         # folded accumulation (KL <= 4): no hi + lo add (kde_mfma.hip)
         V, T = (32.0 if KL <= 4 else 48.0), 16.0
         src = "static per-tile instruction count (no PMC file for this d)"
-    cyc = max(2 * (V - T) + 8 * T + 8 * F, 32 * F)
+    cyc = max(4 * (V - T) + 8 * T + 8 * F, 32 * F)
     t_ceil = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
     frac = t_ceil / avg_launch_s
     peak_tf = achieved_tf / frac
@@ -128,7 +129,7 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "traffic": traffic,
         "traffic_source": traffic_src,
         "peak_basis": "SIMD issue ceiling of the PMC-counted instruction mix "
-                      "(VALU 2, TRANS 8, MFMA 8 issue / 32 pipe cycles per "
+                      "(VALU 4, TRANS 8, MFMA 8 issue / 32 pipe cycles per "
                       "wave64 instruction, 1024 SIMDs at 2.4 GHz), expressed "
                       f"in algorithmic {fpp} FLOP/pair; {src}",
         "ceiling_cycles_per_tile": cyc,

@@ -103,6 +103,54 @@ __device__ inline T block_sum(T v, T* lds /* >= BLOCK/64 */) {
   return r;
 }
 
+// Block-wide reduction then ONE device atomic per block.  Per-wave atomics
+// on a single address serialise (~100 per microsecond chip-wide): the
+// one-pass max / sum kernels spent 20-40 us in them at n = 1e5.  Every
+// thread of the block must call these (they hold a barrier).
+template <int BLOCK>
+__device__ inline void block_atomic_max_u64(unsigned long long* addr,
+                                            unsigned long long v) {
+  __shared__ unsigned long long red[BLOCK / 64];
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < BLOCK / 64; ++i) v = red[i] > v ? red[i] : v;
+    if (v) atomicMax(addr, v);
+  }
+}
+template <int BLOCK>
+__device__ inline void block_atomic_min_u64(unsigned long long* addr,
+                                            unsigned long long v) {
+  __shared__ unsigned long long red[BLOCK / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < BLOCK / 64; ++i) v = red[i] < v ? red[i] : v;
+    if (v != ~0ull) atomicMin(addr, v);
+  }
+}
+template <int BLOCK>
+__device__ inline void block_atomic_add_u64(unsigned long long* addr,
+                                            unsigned long long v) {
+  __shared__ unsigned long long red[BLOCK / 64];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < BLOCK / 64; ++i) v += red[i];
+    if (v) atomicAdd(addr, v);
+  }
+}
+
 // Order-preserving map of an IEEE double to uint64 (total order, -0 < +0).
 __device__ inline uint64_t f64_key(double x) {
   uint64_t b = __double_as_longlong(x);

@@ -88,12 +88,7 @@ __global__ __launch_bounds__(256) void max_key_kernel(
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
        i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
     m = max(m, f64_key(w[i]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t u = __shfl_xor(m, o, 64);
-    m = u > m ? u : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(out_key, static_cast<unsigned long long>(m));
+  block_atomic_max_u64<256>(out_key, static_cast<unsigned long long>(m));
 }
 
 template <typename T, int D>
@@ -594,12 +589,7 @@ __global__ __launch_bounds__(256) void logw_max_kernel(
     const double v = static_cast<double>(logw[i]);
     if (v == v) m = max(m, f64_key(v));  // NaN ignored
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    uint64_t u = __shfl_xor(m, o, 64);
-    m = u > m ? u : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(key, static_cast<unsigned long long>(m));
+  block_atomic_max_u64<256>(key, static_cast<unsigned long long>(m));
 }
 
 template <typename T, int D>

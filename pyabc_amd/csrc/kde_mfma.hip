@@ -214,9 +214,7 @@ __global__ __launch_bounds__(256) void ymax_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) m = fmax(m, fabs(y[k]));
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0)
-    atomicMax(key, static_cast<unsigned long long>(f64_key(m)));
+  block_atomic_max_u64<256>(key, static_cast<unsigned long long>(f64_key(m)));
 }
 
 __device__ inline double grid_from_key(const unsigned long long* key) {

@@ -73,9 +73,8 @@ __global__ __launch_bounds__(256) void knn_prep_kernel(
       m = fmax(m, fabs(v));
     }
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0)
-    atomicMax(amax, static_cast<unsigned long long>(__double_as_longlong(m)));
+  block_atomic_max_u64<256>(
+      amax, static_cast<unsigned long long>(__double_as_longlong(m)));
 }
 
 // (d2, idx) lexicographic order, ascending; the reference breaks no ties
@@ -161,7 +160,8 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
     const int i = h * 64 + lane;
     if (i < cnt) {
       ix[h] = buf[i];
-      v[h] = knn_exact_d2<D>(X, row, ix[h]);
+      // the row itself passes the filter (d2f = 0); it ranks last
+      v[h] = ix[h] == row ? INFINITY : knn_exact_d2<D>(X, row, ix[h]);
     } else {
       ix[h] = 0x7fffffff;
       v[h] = INFINITY;
@@ -191,14 +191,18 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
   return __shfl(tk, lk, 64);
 }
 
-// One wave per kNN_ROWS rows, no block barriers: every lane streams one
-// candidate per step (fp32 centred coordinates, prefetched one step ahead)
-// against the wave's rows (packed-fp32 pairs in VGPRs); lanes passing the
-// fp32 filter append the candidate INDEX to the row's LDS buffer; a full
-// buffer is re-ranked by exact fp64 distance in registers (reg_bitonic) and
-// cut back to k, which sets tau.  Buffers hold indices only (H*64*4 B per
-// row), so many waves fit per CU.
-template <int D, int H>
+// One wave per R rows, no block barriers: every lane streams one candidate
+// per step (fp32 centred coordinates, prefetched one step ahead) against the
+// wave's rows (packed-fp32 pairs in VGPRs); lanes passing the fp32 filter
+// append the candidate INDEX to the row's LDS buffer; a full buffer is
+// re-ranked by exact fp64 distance in registers (reg_bitonic) and cut back
+// to k, which sets tau.  Buffers hold indices only (H*64*4 B per row).
+// The per-step test is ONE compare per row: lanes past N carry coordinates
+// whose d2f is +inf, rows past rhi a threshold of -inf, and the row itself
+// (d2f = 0) is dropped by the exact ranking (knn_sort_cut), so the common
+// step -- no lane passes for any row -- is R compares, R ballots and one
+// branch.
+template <int D, int H, int R>
 __global__ __launch_bounds__(64) void knn_kernel(
     const double* __restrict__ X, const float* __restrict__ Xf,
     const unsigned long long* __restrict__ amax, int64_t N, int k,
@@ -206,44 +210,42 @@ __global__ __launch_bounds__(64) void knn_kernel(
     double* __restrict__ nbr_d2) {
   // query rows [rlo, rhi) against all N; row r's output is row r - rlo
   constexpr int CAP = H * 64;
-  __shared__ int buf[kKnnRows][CAP];
+  __shared__ int buf[R][CAP];
   const int lane = threadIdx.x;
-  const int64_t row0 = rlo + static_cast<int64_t>(blockIdx.x) * kKnnRows;
+  const int64_t row0 = rlo + static_cast<int64_t>(blockIdx.x) * R;
   const double A = __longlong_as_double(static_cast<long long>(*amax));
+  constexpr float kFar = 1e30f;  // (kFar - x)^2 overflows to +inf
 
-  f32x2 xrf[kKnnRows / 2][D];   // rows in pairs for packed fp32 math
+  f32x2 xrf[R / 2][D];   // rows in pairs for packed fp32 math
 #pragma unroll
-  for (int p = 0; p < kKnnRows / 2; ++p) {
+  for (int p = 0; p < R / 2; ++p) {
     const int64_t ra = row0 + 2 * p < rhi ? row0 + 2 * p : rhi - 1;
     const int64_t rb = row0 + 2 * p + 1 < rhi ? row0 + 2 * p + 1 : rhi - 1;
 #pragma unroll
     for (int q = 0; q < D; ++q) xrf[p][q] = f32x2{Xf[ra * D + q], Xf[rb * D + q]};
   }
-  float Tf[kKnnRows];
-  int cnt[kKnnRows];
+  float Tf[R];
+  int cnt[R];
 #pragma unroll
-  for (int r = 0; r < kKnnRows; ++r) {
-    Tf[r] = INFINITY;
+  for (int r = 0; r < R; ++r) {
+    Tf[r] = row0 + r < rhi ? INFINITY : -INFINITY;
     cnt[r] = 0;
   }
   float nx[D];
 #pragma unroll
-  for (int q = 0; q < D; ++q) nx[q] = lane < N ? Xf[lane * D + q] : 0.f;
+  for (int q = 0; q < D; ++q) nx[q] = lane < N ? Xf[lane * D + q] : kFar;
 
   for (int64_t base = 0; base < N; base += 64) {
     const int64_t j = base + lane;
-    const bool valid = j < N;
     float xj[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) xj[q] = nx[q];
     const int64_t jn = j + 64;
-    if (jn < N) {
 #pragma unroll
-      for (int q = 0; q < D; ++q) nx[q] = Xf[jn * D + q];
-    }
-    float d2f[kKnnRows];
+    for (int q = 0; q < D; ++q) nx[q] = jn < N ? Xf[jn * D + q] : kFar;
+    float d2f[R];
 #pragma unroll
-    for (int p = 0; p < kKnnRows / 2; ++p) {
+    for (int p = 0; p < R / 2; ++p) {
       f32x2 acc = f32x2{0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < D; ++q) {
@@ -253,30 +255,36 @@ __global__ __launch_bounds__(64) void knn_kernel(
       d2f[2 * p] = acc.x;
       d2f[2 * p + 1] = acc.y;
     }
+    uint64_t m[R];
+    uint64_t any = 0;
 #pragma unroll
-    for (int r = 0; r < kKnnRows; ++r) {
+    for (int r = 0; r < R; ++r) {
+      m[r] = __ballot(d2f[r] < Tf[r]);
+      any |= m[r];
+    }
+    if (!any) continue;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!m[r]) continue;
       const int64_t row = row0 + r;
-      bool cand = valid && j != row && row < rhi &&
-                  (d2f[r] < Tf[r] || Tf[r] == INFINITY);
-      uint64_t m = __ballot(cand);
-      if (!m) continue;
-      if (cnt[r] + __popcll(m) > CAP) {
+      bool cand = d2f[r] < Tf[r];
+      if (cnt[r] + __popcll(m[r]) > CAP) {
         const double tau = knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane,
                                               nullptr, nullptr);
         cnt[r] = k;
         Tf[r] = knn_filter_bound(tau, D, A);
         cand = cand && d2f[r] < Tf[r];
-        m = __ballot(cand);
+        m[r] = __ballot(cand);
       }
-      if (cand) buf[r][cnt[r] + __popcll(m & ((1ull << lane) - 1ull))] =
+      if (cand) buf[r][cnt[r] + __popcll(m[r] & ((1ull << lane) - 1ull))] =
           static_cast<int>(j);
-      cnt[r] += __popcll(m);
+      cnt[r] += __popcll(m[r]);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int r = 0; r < kKnnRows; ++r) {
+  for (int r = 0; r < R; ++r) {
     const int64_t row = row0 + r;
     if (row < rhi)
       knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane, nbr + (row - rlo) * k,
@@ -440,13 +448,7 @@ __global__ __launch_bounds__(256) void local_const_kernel(
       for (int b = a + 1; b < d; ++b) c[t++] = A[a * d + b] + A[b * d + a];
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t u = __shfl_xor(key, o, 64);
-    key = u > key ? u : key;
-  }
-  if ((threadIdx.x & 63) == 0 && key)
-    atomicMax(lc_max_key, static_cast<unsigned long long>(key));
+  block_atomic_max_u64<256>(lc_max_key, static_cast<unsigned long long>(key));
 }
 
 // q = (theta - X_n)^T inv_n (theta - X_n) from the packed symmetric form
@@ -785,18 +787,22 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
   float* Xf = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
   const unsigned pg = static_cast<unsigned>(ceil_div(N, 256));
-  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, kKnnRows));
+  int rows = kKnnRows;  // rows per wave (tuning override ABC_KNN_ROWS=16)
+  if (const char* env = getenv("ABC_KNN_ROWS")) rows = atoi(env) == 16 ? 16 : 8;
+  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, rows));
   const int64_t rlo = row0, rhi = row0 + nrows;
+#define KNN(DD, H, R)                                                           \
+  hipLaunchKernelGGL((knn_kernel<DD, H, R>), dim3(grid), dim3(64), 0, st, X,    \
+                     Xf, amax, N, k, rlo, rhi, nbr, nbr_d2)
 #define L(DD)                                                                   \
   {                                                                             \
     hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(pg), dim3(256), 0, st, X, N, \
                        Xf, amax);                                               \
-    if (k <= 64)                                                                \
-      hipLaunchKernelGGL((knn_kernel<DD, 2>), dim3(grid), dim3(64), 0, st, X,   \
-                         Xf, amax, N, k, rlo, rhi, nbr, nbr_d2);                \
-    else                                                                        \
-      hipLaunchKernelGGL((knn_kernel<DD, 4>), dim3(grid), dim3(64), 0, st, X,   \
-                         Xf, amax, N, k, rlo, rhi, nbr, nbr_d2);                \
+    if (k <= 64) {                                                              \
+      if (rows == 16) KNN(DD, 2, 16); else KNN(DD, 2, 8);                       \
+    } else {                                                                    \
+      if (rows == 16) KNN(DD, 4, 16); else KNN(DD, 4, 8);                       \
+    }                                                                           \
   }
   switch (d) {
     case 1: L(1) break;
@@ -812,6 +818,7 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
       return kUnsupported;
   }
 #undef L
+#undef KNN
   ABC_LAUNCH_CHECK("knn_kernel");
   return kOk;
 }

@@ -118,12 +118,10 @@ __global__ __launch_bounds__(256) void wq_wmax_kernel(const double* __restrict__
     const long long b = __double_as_longlong(w ? w[i] : 1.0);
     m = b > m ? b : m;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const long long a = __shfl_xor(m, o, 64);
-    m = a > m ? a : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(&st->x.wmax_bits, m);
+  // weights >= 0: their bits order the same as signed or unsigned integers
+  block_atomic_max_u64<256>(
+      reinterpret_cast<unsigned long long*>(&st->x.wmax_bits),
+      static_cast<unsigned long long>(m));
 }
 
 // scale from the (reduced) largest weight and the total count, then the
@@ -140,8 +138,7 @@ __global__ __launch_bounds__(256) void wq_total_kernel(const double* __restrict_
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256)
     s += fixw(w ? w[i] : 1.0, scale);
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(&st->x.w_tot, s);
+  block_atomic_add_u64<256>(&st->x.w_tot, s);
 }
 
 __global__ void wq_target_kernel(WQState* st, double alpha) {
@@ -220,14 +217,26 @@ __global__ __launch_bounds__(256) void wq_neighbors_kernel(const double* __restr
     if (k < key && k > kp) kp = k;
     if (k > key && k < kn) kn = k;
   }
+  // kprev_x / knext_x hold key ^ 2^63 as signed words (the exchange's
+  // MAX / MIN); unsigned order of the keys is signed order of key ^ 2^63
+  __shared__ unsigned long long rp[4], rn[4];
+  kp = wave_max(kp);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long a = __shfl_xor(kp, o, 64);
     const unsigned long long b = __shfl_xor(kn, o, 64);
-    kp = a > kp ? a : kp;
     kn = b < kn ? b : kn;
   }
   if ((threadIdx.x & 63) == 0) {
+    rp[threadIdx.x >> 6] = kp;
+    rn[threadIdx.x >> 6] = kn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      kp = rp[i] > kp ? rp[i] : kp;
+      kn = rn[i] < kn ? rn[i] : kn;
+    }
     atomicMax(&st->x.kprev_x, static_cast<long long>(kp ^ kKeyFlip));
     atomicMin(&st->x.knext_x, static_cast<long long>(kn ^ kKeyFlip));
   }
@@ -247,12 +256,9 @@ __global__ __launch_bounds__(256) void wq_neighbor_mass_kernel(
     if (k == kp) sp += wi;
     if (k == kn) sn += wi;
   }
-  sp = wave_sum(sp);
-  sn = wave_sum(sn);
-  if ((threadIdx.x & 63) == 0) {
-    if (sp) atomicAdd(&st->x.wprev, sp);
-    if (sn) atomicAdd(&st->x.wnext, sn);
-  }
+  block_atomic_add_u64<256>(&st->x.wprev, sp);
+  __syncthreads();
+  block_atomic_add_u64<256>(&st->x.wnext, sn);
 }
 
 // np.interp(alpha, xp, fp) restricted to the bracketing knots

@@ -9,11 +9,12 @@ one launch computes (Mpad/32 * npad/32) and writes
 ``profiles/<tag>_kde_pmc.json``.  bench.py prices its live launch with these
 per-tile counts (the issue ceiling):
 
-    cycles per tile per SIMD = max(2 * VALU_plain + 8 * TRANS + 8 * MFMA,
+    cycles per tile per SIMD = max(4 * VALU_plain + 8 * TRANS + 8 * MFMA,
                                    32 * MFMA)
 
-with the MI355X_MICROARCH.md per-instruction SIMD costs (plain fp32 VALU
-2 cycles per wave64 instruction, transcendental 8, an MFMA holding vector
+with the MI355X_MICROARCH.md per-instruction SIMD issue costs (plain or
+packed fp32 VALU 4 cycles per wave64 instruction -- the round-1 probe's
+2.41 for v_fma_f32 timed SLP-packed pairs --, transcendental 8, an MFMA holding vector
 issue for 8 of its 32 matrix-pipe cycles), SQ_INSTS_VALU counting the
 non-MFMA VALU instructions (TRANS included) and SQ_INSTS_MFMA the MFMAs.
 """
@@ -59,7 +60,7 @@ def main(prof_dir, tag, N=1_000_000, M=1_000_000, d=8):
     valu = per_tile["SQ_INSTS_VALU"]
     trans = per_tile.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
     mfma = per_tile["SQ_INSTS_MFMA"]
-    issue = 2 * (valu - trans) + 8 * trans + 8 * mfma
+    issue = 4 * (valu - trans) + 8 * trans + 8 * mfma
     cyc = max(issue, 32 * mfma)
     out = {
         "source": f"rocprofv3 --pmc passes over bench.py ({prof_dir}), "
@@ -71,7 +72,7 @@ def main(prof_dir, tag, N=1_000_000, M=1_000_000, d=8):
         "issue_cycles_per_tile": issue,
         "mfma_pipe_cycles_per_tile": 32 * mfma,
         "ceiling_cycles_per_tile": cyc,
-        "cost_model": "plain VALU 2, TRANS 8, MFMA issue 8 / pipe 32 SIMD "
+        "cost_model": "plain VALU 4, TRANS 8, MFMA issue 8 / pipe 32 SIMD "
                       "cycles per wave64 instruction (MI355X_MICROARCH.md)",
     }
     if "GRBM_GUI_ACTIVE" in avg and "_ns" in avg:

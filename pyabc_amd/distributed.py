@@ -17,10 +17,13 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, rank=0, world=1, group=None):
+    def __init__(self, rank=0, world=1, group=None, force=False):
         self.rank = rank
         self.world = world
         self.group = group
+        # a one-rank process group whose collectives still run (the RCCL
+        # self-test on a one-GPU box: ABC_COMM_FORCE=1 under torchrun)
+        self.force = force
 
     @staticmethod
     def single():
@@ -34,7 +37,8 @@ class Comm:
         rehearsal of the multi-rank path on a one-GPU box puts every rank on
         device 0 with the "gloo" backend."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
-        if world == 1:
+        force = os.environ.get("ABC_COMM_FORCE") == "1"
+        if world == 1 and not force:
             return Comm.single()
         if not dist.is_initialized():
             if backend is None:
@@ -43,14 +47,15 @@ class Comm:
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0"))
                                       if device is None else device)
             dist.init_process_group(backend=backend)
-        return Comm(dist.get_rank(), dist.get_world_size(), None)
+        return Comm(dist.get_rank(), dist.get_world_size(), None, force)
 
     @staticmethod
     def current():
         """The already-initialised process group (or a single rank)."""
+        force = os.environ.get("ABC_COMM_FORCE") == "1"
         if dist.is_available() and dist.is_initialized() and \
-                dist.get_world_size() > 1:
-            return Comm(dist.get_rank(), dist.get_world_size(), None)
+                (dist.get_world_size() > 1 or force):
+            return Comm(dist.get_rank(), dist.get_world_size(), None, force)
         return Comm.single()
 
     def broadcast_int(self, v, src=0):
@@ -68,7 +73,7 @@ class Comm:
 
     @property
     def active(self):
-        return self.world > 1
+        return self.world > 1 or self.force
 
     def barrier(self):
         if self.active:

@@ -145,7 +145,7 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     local = torch.cat(pieces) if pieces else torch.empty(
         (0,) + tuple(row_shape), dtype=F64, device=device)
     R = comm.world
-    if R == 1:
+    if not comm.active:
         return local
     allr = comm.all_gather_rows(local, [sum(c) for c in counts])
     starts = [0]
@@ -529,7 +529,7 @@ class GenerationEngine:
     def _gather_cols(self, pieces, counts):
         """Stat-major [S, cols] version of :meth:`_gather` (contiguous)."""
         S = self.model.n_stats
-        if self.comm.world == 1:
+        if not self.comm.active:
             return torch.cat(pieces, 1) if pieces else torch.empty(
                 (S, 0), dtype=F64, device=self.dev)
         rows = self._gather([x.t() for x in pieces], (S,), counts)

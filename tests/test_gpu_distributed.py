@@ -139,6 +139,65 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     assert one["eps1"] <= one["eps0"]
 
 
+def _rccl_main(rank, port, n, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      ABC_COMM_FORCE="1")
+    sys.path.insert(0, ROOT)
+    from pyabc_amd.distributed import Comm
+    comm = Comm.from_env("nccl")
+    assert comm.active and torch.distributed.get_backend() == "nccl"
+    out["rccl"] = _generation(comm, n, 1 << 11, record=True)
+    out["single"] = _generation(Comm.single(), n, 1 << 11, record=True)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_rccl_collectives_one_rank_equal_no_comm():
+    """The "nccl" (RCCL) branches of pyabc_amd.distributed on the GPU: a
+    one-rank process group whose collectives still run (ABC_COMM_FORCE=1)
+    drives the whole generation -- count all-gathers, row all-gathers of the
+    population and statistics, the log-density all-gather, the sharded
+    quantile's histogram all-reduces -- through RCCL, and gives exactly the
+    no-communicator result."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rccl_main, args=(_free_port(), 5001, out), nprocs=1,
+                 join=True)
+        res = dict(out)
+    one, got = res["single"], res["rccl"]
+    for k in ("theta0", "theta", "d", "w", "logpd", "stats", "rec", "cov1",
+              "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta", "s_rec_d",
+              "s_rec_acc"):
+        np.testing.assert_array_equal(got[k], one[k], err_msg=k)
+    for k in ("eps0", "eps1", "n_eval", "s_n_eval"):
+        assert got[k] == one[k], k
+
+
+@pytest.mark.timeout(300)
+def test_bench_rccl_one_rank():
+    """bench.py under torchrun over RCCL ("nccl" backend), one rank with its
+    collectives forced on: barrier, all-gathers and the max-over-ranks
+    timing run through RCCL and rank 0 prints one line."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "1", "--warmup", "1", "--particles",
+           "40000", "--no-cpu-baseline"]
+    env = dict(os.environ, ABC_COMM_FORCE="1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280,
+                       cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines()
+             if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["n_gpus"] == 1 and lines[0]["value"] > 0
+
+
 @pytest.mark.timeout(300)
 def test_bench_two_rank_rehearsal():
     """bench.py's own N>1 path (barrier, max-over-ranks timing, rank-0 JSON)

@@ -1064,9 +1064,10 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   bool lds = false;
   if (const char* env = getenv("ABC_KDE_MFMA_LDS")) lds = atoi(env) != 0;
   // sched_group_barrier interleave of step q+1's MFMAs with step q's VALU:
-  // 156.4 -> 151.2 ms at N = M = 1e6, d = 8; slower at d = 4 (1.37 -> 1.44
-  // ms) and d = 20 (21 -> 52 ms), so on at D = 8 only (tools/bench_kde.py sw)
-  bool sched = D == 8;
+  // 156.4 -> 151.2 ms at N = M = 1e6, d = 8 with SLP-packed adds, but with
+  // plain adds (no SLP, Makefile) the hardware's own interleave is faster:
+  // 143.4 (sched) vs 139.2 ms (tools/kde_ab.py); slower at d = 4 and 20
+  bool sched = false;
   if (const char* env = getenv("ABC_KDE_MFMA_SCHED")) sched = atoi(env) != 0;
   bool sw = false;
   if (const char* env = getenv("ABC_KDE_MFMA_SW")) sw = atoi(env) != 0;

@@ -377,28 +377,34 @@ struct SegState {
   int pad;
 };
 
-// After 16 (or, failing that, 24) key bits a column's selected bucket is
+// After 24 (or, failing that, 32) key bits a column's selected bucket is
 // usually far smaller than the column: its keys are compacted (one more
 // read) and the remaining passes histogram the buffer instead of
 // re-reading the column.  A column whose bucket exceeds kCandCap keys
 // (ties, one dominant value) keeps reading its full column.
-constexpr int kCompactFirst = 1, kCompactLast = 2;
 constexpr int kCandCap = 65536;
+// digit widths of the passes, most significant first (64 bits)
+constexpr int kSegPasses = 7;
+constexpr int kSegBits[kSegPasses] = {12, 12, 8, 8, 8, 8, 8};
+constexpr int kWideBins = 1 << 12;
 
 template <int MODE>  // 0: key(x), 1: key(|x - center|)
 __device__ inline uint64_t seg_key(double x, double c) {
   return MODE == 0 ? f64_key(x) : f64_key(fabs(x - c));
 }
 
-template <int MODE>
+// BITS-wide digit (12 for the two leading passes: 24 key bits after two
+// reads, so the bucket almost always fits the candidate buffer; 8 after)
+template <int MODE, int BITS>
 __global__ __launch_bounds__(256) void seg_hist_kernel(
     const double* __restrict__ data, int64_t ld, int64_t n, int S, int bps,
     const double* __restrict__ center, const SegState* __restrict__ st,
     int shift, unsigned long long mask, unsigned* __restrict__ hist) {
-  __shared__ unsigned hc[kBins];
+  constexpr int NB = 1 << BITS;
+  __shared__ unsigned hc[NB];
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
   if (st[s].compacted) return;   // block-uniform: seg_hist_cand_kernel's
-  hc[threadIdx.x] = 0;
+  for (int b = threadIdx.x; b < NB; b += 256) hc[b] = 0;
   __syncthreads();
   const unsigned long long prefix = st[s].prefix;
   const double c = MODE == 1 ? center[s] : 0.0;
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(256) void seg_hist_kernel(
       if (i < n) {
         const uint64_t k = seg_key<MODE>(v[u], c);
         in = ((k ^ prefix) & mask) == 0;
-        bin = static_cast<unsigned>(k >> shift) & 0xffu;
+        bin = static_cast<unsigned>(k >> shift) & (NB - 1u);
       }
       // wave-aggregated count: in the leading passes most keys of a column
       // share one bin (sign + exponent), and 64 same-address LDS atomics
@@ -440,34 +446,52 @@ __global__ __launch_bounds__(256) void seg_hist_kernel(
     }
   }
   __syncthreads();
-  if (hc[threadIdx.x]) atomicAdd(&hist[s * kBins + threadIdx.x], hc[threadIdx.x]);
+  for (int b = threadIdx.x; b < NB; b += 256)
+    if (hc[b]) atomicAdd(&hist[static_cast<int64_t>(s) * NB + b], hc[b]);
 }
 
+// the (merged) digit histogram of a BITS-wide pass -> the digit holding the
+// remaining rank; thread t owns bins [t * PER, (t + 1) * PER); clears them
+template <int BITS>
 __global__ __launch_bounds__(256) void seg_select_kernel(SegState* st, int shift,
                                                          unsigned* __restrict__ hist,
                                                          int last) {
-  __shared__ long long sc[kBins];
+  constexpr int NB = 1 << BITS, PER = NB / 256;
+  __shared__ long long sc[256];
   const int s = blockIdx.x, t = threadIdx.x;
-  const long long v = hist[s * kBins + t];
-  sc[t] = v;
+  unsigned* h = hist + static_cast<int64_t>(s) * NB + t * PER;
+  long long v[PER];
+  long long tot = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = h[j];
+    tot += v[j];
+  }
+  sc[t] = tot;
   __syncthreads();
-  for (int o = 1; o < kBins; o <<= 1) {
+  for (int o = 1; o < 256; o <<= 1) {
     const long long a = t >= o ? sc[t - o] : 0;
     __syncthreads();
     sc[t] += a;
     __syncthreads();
   }
-  const long long incl = sc[t], excl = incl - v;
+  long long run = sc[t] - tot;
   const long long rank = st[s].rank;
   __syncthreads();
-  if (v > 0 && excl <= rank && rank < incl) {
-    st[s].prefix |= static_cast<unsigned long long>(t) << shift;
-    st[s].rank = rank - excl;
-    st[s].less += excl;
-    st[s].cand = v;
-    if (last) st[s].eq = v;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const long long incl = run + v[j];
+    if (v[j] > 0 && run <= rank && rank < incl) {
+      st[s].prefix |= static_cast<unsigned long long>(t * PER + j) << shift;
+      st[s].rank = rank - run;
+      st[s].less += run;
+      st[s].cand = v[j];
+      if (last) st[s].eq = v[j];
+    }
+    run = incl;
   }
-  hist[s * kBins + t] = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) h[j] = 0;
 }
 
 __global__ void seg_init_kernel(SegState* st, int S, long long rank) {
@@ -1043,7 +1067,7 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
 }
 
 size_t abc_column_select_workspace_bytes(int S) {
-  return static_cast<size_t>(S) * (sizeof(SegState) + kBins * 4 +
+  return static_cast<size_t>(S) * (sizeof(SegState) + kWideBins * 4 +
                                    kCandCap * 8) + 256;
 }
 
@@ -1058,8 +1082,8 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
   unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
                                                static_cast<size_t>(S) * sizeof(SegState));
   unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
-      hist + static_cast<size_t>(S) * kBins);
-  ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * kBins * 4, st));
+      hist + static_cast<size_t>(S) * kWideBins);
+  ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * kWideBins * 4, st));
   int bps = static_cast<int>(ceil_div(2048, S));
   const int64_t maxb = ceil_div(n, 256);
   if (bps > maxb) bps = static_cast<int>(maxb);
@@ -1070,21 +1094,32 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
     double* out = round == 0 ? median_out : mad_out;
     hipLaunchKernelGGL(seg_init_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, st,
                        sst, S, k);
-    for (int pass = 0; pass < 8; ++pass) {
-      const int shift = 56 - 8 * pass;
-      const unsigned long long mask = pass == 0 ? 0ull : (~0ull << (shift + 8));
-      if (round == 0)
-        hipLaunchKernelGGL(seg_hist_kernel<0>, dim3(S * bps), dim3(256), 0, st,
-                           data_T, ld, n, S, bps, center, sst, shift, mask, hist);
-      else
-        hipLaunchKernelGGL(seg_hist_kernel<1>, dim3(S * bps), dim3(256), 0, st,
-                           data_T, ld, n, S, bps, center, sst, shift, mask, hist);
-      if (pass > kCompactFirst)
+    int consumed = 0;  // key bits selected so far
+    for (int pass = 0; pass < kSegPasses; ++pass) {
+      const int bits = kSegBits[pass];
+      const int shift = 64 - consumed - bits;
+      const unsigned long long mask = consumed == 0 ? 0ull : (~0ull << (64 - consumed));
+#define HIST(MODE, B)                                                            \
+  hipLaunchKernelGGL((seg_hist_kernel<MODE, B>), dim3(S * bps), dim3(256), 0, st, \
+                     data_T, ld, n, S, bps, center, sst, shift, mask, hist)
+      if (bits == 12) {
+        if (round == 0) HIST(0, 12); else HIST(1, 12);
+      } else {
+        if (round == 0) HIST(0, 8); else HIST(1, 8);
+      }
+#undef HIST
+      if (pass > 1)  // 8-bit passes over the compacted columns' candidates
         hipLaunchKernelGGL(seg_hist_cand_kernel, dim3(S), dim3(256), 0, st, sst,
                            cbuf, shift, mask, hist);
-      hipLaunchKernelGGL(seg_select_kernel, dim3(S), dim3(256), 0, st, sst, shift,
-                         hist, pass == 7 ? 1 : 0);
-      if (pass >= kCompactFirst && pass <= kCompactLast) {
+      const int last = pass == kSegPasses - 1 ? 1 : 0;
+      if (bits == 12)
+        hipLaunchKernelGGL(seg_select_kernel<12>, dim3(S), dim3(256), 0, st, sst,
+                           shift, hist, last);
+      else
+        hipLaunchKernelGGL(seg_select_kernel<8>, dim3(S), dim3(256), 0, st, sst,
+                           shift, hist, last);
+      consumed += bits;
+      if (pass == 1 || pass == 2) {  // compaction after 24, else 32 bits
         const unsigned long long cmask = ~0ull << shift;
         hipLaunchKernelGGL(seg_mark_kernel, dim3(ceil_div(S, 256)), dim3(256), 0,
                            st, sst, S);

@@ -3,7 +3,7 @@
 # rocprofv3 kernel stats + PMC passes of the headline bench, then the bench
 # line with its CPU baseline.
 set -e -o pipefail
-OUT=gpurun_out/r02g
+OUT=gpurun_out/r02h
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 240 --timeout-method thread > $OUT/gpu_all.txt 2>&1

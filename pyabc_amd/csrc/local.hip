@@ -510,6 +510,11 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
 // itself, not of the distance R to X[0], so the density's accuracy does not
 // degrade with the population's extent over the local bandwidth (a single
 // fp32 rounding of x - X[0] costs ~ sqrt(q) (R / sigma) 2^-23 relative).
+// Layout: particles in PAIRS (n, n + 1) interleaved per coordinate, so one
+// 64-bit scalar load feeds a packed-fp32 operand (v_pk_*_f32) that serves
+// two particles at once: X2[(n / 2) * D + q] = (x_n, x_{n+1}), the same for
+// the lo parts, coef2[(n / 2) * NC + t] and lc2[n / 2].  The count is padded
+// to even with a particle of lc = -inf (exp2 -> 0).
 template <int D>
 __global__ __launch_bounds__(256) void local_pack32_kernel(
     const double* __restrict__ X, const double* __restrict__ coef,
@@ -518,19 +523,32 @@ __global__ __launch_bounds__(256) void local_pack32_kernel(
     float* __restrict__ coef32, float* __restrict__ lc32) {
   constexpr int NC = D * (D + 1) / 2;
   const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (n >= N) return;
+  if (n >= ((N + 1) & ~int64_t{1})) return;
+  const int64_t pr = n >> 1;
+  const int h = static_cast<int>(n & 1);
+  if (n >= N) {  // padding particle of an odd count
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      X32[(pr * D + q) * 2 + h] = 0.0f;
+      X32lo[(pr * D + q) * 2 + h] = 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < NC; ++t) coef32[(pr * NC + t) * 2 + h] = 0.0f;
+    lc32[n] = -INFINITY;
+    return;
+  }
   const double L = key_f64(*lc_max_key);
   constexpr double kLog2e = 1.4426950408889634;
 #pragma unroll
   for (int q = 0; q < D; ++q) {
     const double c = X[n * D + q] - X[q];
-    const float h = static_cast<float>(c);
-    X32[n * D + q] = h;
-    X32lo[n * D + q] = static_cast<float>(c - static_cast<double>(h));
+    const float hi = static_cast<float>(c);
+    X32[(pr * D + q) * 2 + h] = hi;
+    X32lo[(pr * D + q) * 2 + h] = static_cast<float>(c - static_cast<double>(hi));
   }
 #pragma unroll
   for (int t = 0; t < NC; ++t)
-    coef32[n * NC + t] = static_cast<float>(coef[n * NC + t] * (0.5 * kLog2e));
+    coef32[(pr * NC + t) * 2 + h] = static_cast<float>(coef[n * NC + t] * (0.5 * kLog2e));
   lc32[n] = static_cast<float>((lc[n] - L) * kLog2e);
 }
 
@@ -551,47 +569,58 @@ __global__ __launch_bounds__(256) void local_pts32_kernel(const double* __restri
   }
 }
 
+// Two particles per packed-fp32 lane pair: the (hi, lo) differences, the
+// quadratic form's FMAs and the exponent arguments of particles n and n + 1
+// run as v_pk_add / v_pk_fma / v_pk_mul on SGPR-pair operands, about half
+// the VALU instructions of the one-particle loop; two v_exp_f32 per pair.
+// Terms of 8 pairs are added in fp32 (even and odd particles apart), then
+// into fp64.  nchunk is even, so no pair straddles two chunks.
 template <int D>
 __global__ __launch_bounds__(256) void local_pdf32_kernel(
     const float* __restrict__ pts, const float* __restrict__ ptslo, int64_t M,
-    const float* __restrict__ X, const float* __restrict__ Xlo,
-    const float* __restrict__ coef, const float* __restrict__ lc, int64_t N,
+    const f32x2* __restrict__ X2, const f32x2* __restrict__ X2lo,
+    const f32x2* __restrict__ coef2, const f32x2* __restrict__ lc2, int64_t N,
     int split, int64_t nchunk, double* __restrict__ part) {
   constexpr int NC = D * (D + 1) / 2;
   const int s = blockIdx.x % split;
   const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
   const int64_t i = i0 < M ? i0 : M - 1;
-  float th[D], tl[D];
+  f32x2 th[D], tl[D];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
-    th[q] = pts[i * D + q];
-    tl[q] = ptslo[i * D + q];
+    const float a = pts[i * D + q], b = ptslo[i * D + q];
+    th[q] = f32x2{a, a};
+    tl[q] = f32x2{b, b};
   }
   double acc = 0.0;
-  const int64_t n0 = static_cast<int64_t>(s) * nchunk;
+  const int64_t n0 = static_cast<int64_t>(s) * nchunk;  // even
   int64_t n1 = n0 + nchunk;
-  if (n1 > N) n1 = N;
+  const int64_t npair = (N + 1) & ~int64_t{1};
+  if (n1 > npair) n1 = npair;
   for (int64_t b = n0; b < n1; b += 16) {
     const int64_t be = b + 16 < n1 ? b + 16 : n1;
-    float a16 = 0.0f;
-    for (int64_t n = b; n < be; ++n) {
-      float dl[D];
+    f32x2 a2 = f32x2{0.0f, 0.0f};
+    for (int64_t n = b; n < be; n += 2) {
+      const int64_t pr = n >> 1;
+      f32x2 dl[D];
 #pragma unroll
       for (int q = 0; q < D; ++q)
-        dl[q] = (th[q] - X[n * D + q]) + (tl[q] - Xlo[n * D + q]);
-      const float* c = coef + n * NC;
-      float qf = 0.0f;
+        dl[q] = (th[q] - X2[pr * D + q]) + (tl[q] - X2lo[pr * D + q]);
+      const f32x2* c = coef2 + pr * NC;
+      f32x2 qf = f32x2{0.0f, 0.0f};
       int t = 0;
 #pragma unroll
       for (int a = 0; a < D; ++a) {
-        float r = c[t++] * dl[a];
+        f32x2 r = c[t++] * dl[a];
 #pragma unroll
-        for (int bb = a + 1; bb < D; ++bb) r = fmaf(c[t++], dl[bb], r);
-        qf = fmaf(dl[a], r, qf);
+        for (int bb = a + 1; bb < D; ++bb)
+          r = __builtin_elementwise_fma(c[t++], dl[bb], r);
+        qf = __builtin_elementwise_fma(dl[a], r, qf);
       }
-      a16 += __builtin_amdgcn_exp2f(lc[n] - qf);
+      const f32x2 e = lc2[pr] - qf;
+      a2 += f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
     }
-    acc += static_cast<double>(a16);
+    acc += static_cast<double>(a2.x + a2.y);
   }
   if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
 }
@@ -948,8 +977,9 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
 size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N) {
   // the fp64 layout, then X32[N][8] | X32lo[N][8] | coef32[N][36] | lc32[N]
   // | pts32[M][8] | pts32lo[M][8]
+  // (N padded to even: particle pairs)
   return abc_local_logpdf_workspace_bytes(M, N) +
-         static_cast<size_t>(N) * 4 * 53 + static_cast<size_t>(M) * 4 * 16 + 512;
+         static_cast<size_t>(N + 1) * 4 * 53 + static_cast<size_t>(M) * 4 * 16 + 512;
 }
 
 int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
@@ -967,6 +997,8 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   int split;
   int64_t nchunk;
   local_plan(M, N, split, nchunk);
+  nchunk += nchunk & 1;  // even: particle pairs never straddle two chunks
+  const int64_t Np = N + (N & 1);
   char* base = static_cast<char*>(ws);
   double* logsumw = reinterpret_cast<double*>(base);
   unsigned long long* lc_max_key = reinterpret_cast<unsigned long long*>(base + 8);
@@ -977,10 +1009,10 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   int* fix_rows = reinterpret_cast<int*>(part + static_cast<int64_t>(split) * M);
   float* X32 = reinterpret_cast<float*>(
       base + ((abc_local_logpdf_workspace_bytes(M, N) + 255) / 256) * 256);
-  float* X32lo = X32 + N * 8;
-  float* coef32 = X32lo + N * 8;
-  float* lc32 = coef32 + N * 36;
-  float* pts32 = lc32 + N;
+  float* X32lo = X32 + Np * 8;
+  float* coef32 = X32lo + Np * 8;
+  float* lc32 = coef32 + Np * 36;
+  float* pts32 = lc32 + Np;
   float* pts32lo = pts32 + M * 8;
   ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
   hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
@@ -991,14 +1023,17 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   // lost to fp32 underflow (< 2^-126 each) are then < 2^-40 of the sum
   const double thresh = 8.673617379884035e-19;
 #define L(DD)                                                                    \
-  hipLaunchKernelGGL((local_pack32_kernel<DD>), dim3(ceil_div(N, 256)), dim3(256), \
+  hipLaunchKernelGGL((local_pack32_kernel<DD>), dim3(ceil_div(Np, 256)), dim3(256), \
                      0, st, X, coef, lc, lc_max_key, N, X32, X32lo, coef32,    \
                      lc32);                                                      \
   hipLaunchKernelGGL((local_pts32_kernel<DD>), dim3(ceil_div(M, 256)), dim3(256),  \
                      0, st, pts, M, X, pts32, pts32lo);                          \
   hipLaunchKernelGGL((local_pdf32_kernel<DD>), dim3(grid), dim3(256), 0, st,       \
-                     pts32, pts32lo, M, X32, X32lo, coef32, lc32, N, split,      \
-                     nchunk, part);                                              \
+                     pts32, pts32lo, M, reinterpret_cast<const f32x2*>(X32),     \
+                     reinterpret_cast<const f32x2*>(X32lo),                      \
+                     reinterpret_cast<const f32x2*>(coef32),                     \
+                     reinterpret_cast<const f32x2*>(lc32), N, split, nchunk,     \
+                     part);                                                      \
   hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),  \
                      0, st, part, M, split, lc_max_key, logsumw, out_logpdf,     \
                      n_fix, fix_rows, thresh);                                   \

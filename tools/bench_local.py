@@ -39,9 +39,9 @@ def main(N=200_000, d=6, k=50):
             lambda: K.local_logpdf(pts, X, w, invs, dets, precision=prec))
     a = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f32")
     b = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f64")
-    out["max_rel_f32_vs_f64"] = float((a - b).abs().max())
-    print({k_: round(v, 4) if isinstance(v, float) else v
-           for k_, v in out.items()}, flush=True)
+    out["max_rel_f32_vs_f64"] = float(torch.expm1(a - b).abs().max())
+    print({k_: (f"{v:.3e}" if k_.startswith("max_rel") else round(v, 4))
+           if isinstance(v, float) else v for k_, v in out.items()}, flush=True)
 
 
 if __name__ == "__main__":

@@ -904,6 +904,178 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
   }
 }
 
+// ---- hand-interleaved folded LDS-DMA pass (d > 8, opt-in ABC_KDE_MFMA_LDS2=2)
+// The VALU of one 32-row tile (per i-tile: 16 v_exp_f32, the 15-add tree and
+// the row add) is cut into slices placed in the gaps of the NEXT tile's MFMA
+// chain, one slice after each MFMA, with sched_barrier fences so the compiler
+// keeps exactly that order: an MFMA holds vector issue for 8 of its 32
+// cycles, and a slice of two exps and one add (20 issue cycles) runs in the
+// other 24 (MI355X_MICROARCH.md, MFMA gap fillers).  Per i-tile the 32 ops
+// are  e0 e8  e1 e9 a0  e2 e10 a1 ... e7 e15 a6  a7  b0..b3  c0 c1  d0  s
+// (a: v + 8, b: v + 4, c: v + 2, d: v + 1, s: the row add) -- the tree of
+// tile_sum, so the rows are bit-identical to the FOLD lds2 kernel's.
+struct TileSumState {
+  float e[16];
+};
+template <int O>
+__device__ __forceinline__ void tile_sum_op(const f32x16& acc, TileSumState& st,
+                                            float& sacc) {
+  if constexpr (O < 2) {
+    st.e[8 * O] = __builtin_amdgcn_exp2f(acc[8 * O]);
+  } else if constexpr (O < 23) {
+    // the exps of pair v one slice ahead of the add of pair v - 1, so no
+    // add waits on the transcendental it follows
+    constexpr int v = 1 + (O - 2) / 3, k = (O - 2) % 3;
+    if constexpr (k == 0) st.e[v] = __builtin_amdgcn_exp2f(acc[v]);
+    else if constexpr (k == 1) st.e[v + 8] = __builtin_amdgcn_exp2f(acc[v + 8]);
+    else st.e[v - 1] += st.e[v - 1 + 8];
+  } else if constexpr (O == 23) {
+    st.e[7] += st.e[15];
+  } else if constexpr (O < 28) {
+    st.e[O - 24] += st.e[O - 24 + 4];
+  } else if constexpr (O < 30) {
+    st.e[O - 28] += st.e[O - 28 + 2];
+  } else if constexpr (O == 30) {
+    st.e[0] += st.e[1];
+  } else {
+    sacc += st.e[0];
+  }
+}
+template <int G, int PER, int O = G * PER>
+__device__ __forceinline__ void tile_sum_slice(const f32x16& acc, TileSumState& st,
+                                               float& sacc) {
+  if constexpr (O < 32 && O < (G + 1) * PER) {
+    tile_sum_op<O>(acc, st, sacc);
+    tile_sum_slice<G, PER, O + 1>(acc, st, sacc);
+  }
+}
+// one gap's slice: gap g of the KT * IB gaps serves i-tile g / KT
+template <int KT, int IB, int G>
+__device__ __forceinline__ void gap_slice(const f32x16 (&acc)[IB],
+                                          TileSumState (&st)[IB],
+                                          float (&sacc)[IB]) {
+  constexpr int t = G / KT, gi = G % KT;
+  constexpr int PER = (32 + KT - 1) / KT;
+  if constexpr (t < IB) tile_sum_slice<gi, PER>(acc[t], st[t], sacc[t]);
+}
+
+// MFMA chain of one tile (folded) with the previous tile's VALU in its gaps
+template <int KT, int IB, bool VALU, int C = 0>
+__device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int lane,
+                                          const bf16x8 (&bq)[IB][KT],
+                                          f32x16 (&acc)[IB],
+                                          const f32x16 (&prev)[IB],
+                                          TileSumState (&st)[IB],
+                                          float (&sacc)[IB], bf16x8 (&a)[2]) {
+  if constexpr (C < KT) {
+    // fragment C + 2 is read while C's MFMAs run (a[C & 1] holds C)
+    bf16x8 nxt = a[(C + 1) & 1];
+    if constexpr (C + 2 < KT) nxt = Ab[tile * KT + C + 2][lane];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[C & 1], bq[t][C], acc[t],
+                                                       0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (VALU) {
+        if (t == 0) gap_slice<KT, IB, C * IB + 0>(prev, st, sacc);
+        if (t == 1) gap_slice<KT, IB, C * IB + 1>(prev, st, sacc);
+        if (t == 2) gap_slice<KT, IB, C * IB + 2>(prev, st, sacc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    a[C & 1] = nxt;
+    lds_chain<KT, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, st, sacc, a);
+  }
+}
+
+template <int KH, int KL, int IB>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2f_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT;
+  static_assert(IB <= 3, "gap_slice serves at most 3 i-tiles");
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    auto fill = [&](int buf, int jc) {
+      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+      for (int f = wave; f < CH; f += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            src + f * 64 + lane,
+            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+    };
+    __syncthreads();
+    if (nj > 0) fill(0, 0);
+    int buf = 0;
+    f32x16 accA[IB], accB[IB];
+    TileSumState st[IB];
+    float sprev[IB], scur[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) sprev[t] = scur[t] = 0.0f;
+    for (int jc = 0; jc < nj; jc += 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      const bf16x8(*Ab)[64] = As[buf];
+      bf16x8 a[2];
+#pragma unroll
+      for (int t = 0; t < IB; ++t) accA[t] = f32x16{};
+      a[0] = Ab[0][lane];
+      a[1] = Ab[1][lane];
+      if (jc == 0) {  // tile 0, nothing to retire yet
+        lds_chain<KT, IB, false>(Ab, 0, lane, bq, accA, accB, st, sprev, a);
+      } else {        // tile 0 || tile 1 of the previous chunk
+        lds_chain<KT, IB, true>(Ab, 0, lane, bq, accA, accB, st, sprev, a);
+#pragma unroll
+        for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) {
+        accB[t] = f32x16{};
+        scur[t] = 0.0f;
+      }
+      a[0] = Ab[KT][lane];
+      a[1] = Ab[KT + 1][lane];
+      // tile 1 || tile 0 of this chunk
+      lds_chain<KT, IB, true>(Ab, 1, lane, bq, accB, accA, st, scur, a);
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
+      buf ^= 1;
+    }
+    if (nj > 0) {  // retire the last tile
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<0>(accB[t], accB[t]);
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
 // The same pass with the A fragments of each 64-row chunk staged once per
 // block in LDS (double-buffered) and shared by the kWaves waves, which walk
 // the same j-segments.  Where the register version needs more than 256
@@ -1076,9 +1248,18 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   // LDS-DMA A with IB MFMAs per LDS fragment: the MFMA-bound shapes (d > 8)
   // (default at d > 8: d = 20 21.5 -> 20.4 ms, d = 12 18.6 -> 15.1, d = 24
   // 27.0 -> 23.8 at N = M = 262144, rows bit-identical; tools/kde_variants.py)
-  bool lds2 = D > 8;
-  if (const char* env = getenv("ABC_KDE_MFMA_LDS2")) lds2 = atoi(env) != 0;
+  // 2 (default at d > 8): the hand-interleaved folded form, d = 20 19.5 ->
+  // 17.3 ms at N = M = 262144, full-size error 6.3e-6 (split form: 1.5e-6);
+  // 1: the split form (kde_mfma_lds2_kernel); 0: the register kernel
+  int lds2 = D > 8 ? 2 : 0;
+  if (const char* env = getenv("ABC_KDE_MFMA_LDS2")) lds2 = atoi(env);
   if constexpr (D > 8) {
+    if (lds2 == 2) {
+      hipLaunchKernelGGL((kde_mfma_lds2f_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                         dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
+                         p.split, p.spb, p.jseg, partial);
+      return;
+    }
     if (lds2) {
       bool fold = false;
       if (const char* env = getenv("ABC_KDE_MFMA_FOLD")) fold = atoi(env) != 0;

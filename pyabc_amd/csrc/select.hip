@@ -84,6 +84,21 @@ struct WQState {
   int none;                     // alpha beyond the last knot
   int pad;
   double scale;                 // power-of-two fixed-point scale
+  // one-GPU compacted path (abc_wquantile_f64)
+  unsigned long long ccount;    // keys of the 24-bit bucket
+  unsigned long long kp_out;    // largest key below the bucket (0: none)
+  unsigned long long kn_out;    // smallest key above the bucket (~0: none)
+  int compacted;                // the bucket fits the candidate buffer
+  int need_mass;                // a neighbour lies outside the bucket
+};
+// 12-bit digit histograms and the candidate buffer follow the state
+constexpr int kWqWideBins = 4096;
+constexpr int kWqCand = 65536;
+struct WQWide {
+  unsigned long long hw[kWqWideBins];
+  unsigned long long hc[kWqWideBins];
+  unsigned long long ckey[kWqCand];
+  unsigned long long cw[kWqCand];
 };
 constexpr unsigned long long kKeyFlip = 0x8000000000000000ull;
 
@@ -106,6 +121,11 @@ __global__ void wq_reset_kernel(WQState* st) {
     st->w_less = 0;
     st->w_eq = 0;
     st->none = 0;
+    st->ccount = 0;
+    st->kp_out = 0;
+    st->kn_out = ~0ull;
+    st->compacted = 0;
+    st->need_mass = 0;
   }
 }
 
@@ -309,6 +329,347 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
   out[1] = key_f64(st->prefix);
   out[2] = static_cast<double>(st->w_less) / W;
   out[3] = static_cast<double>(st->w_eq) / W;
+}
+
+// ---------------------------------------------------------------------------
+// One-GPU weighted quantile in ten launches (abc_wquantile_f64): two 12-bit
+// digit passes over (d, w) -- the first also sums the fixed-point total --
+// then one pass that compacts the keys of the selected 24-bit bucket (with
+// their fixed-point masses) and finds the nearest keys outside it; a
+// single block finishes the remaining 40 key bits, the knot's mass and its
+// neighbours on the candidates.  Same integers as the sharded 8-bit select
+// (the knot key, exact fixed-point masses), so the same result bit for bit.
+__global__ __launch_bounds__(256) void wqc_hist_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    WQState* __restrict__ st, WQWide* __restrict__ wide, int shift,
+    unsigned long long mask, int first) {
+  __shared__ unsigned long long hw[kWqWideBins];
+  __shared__ unsigned hc[kWqWideBins];
+  __shared__ unsigned long long red[4];
+  for (int b = threadIdx.x; b < kWqWideBins; b += 256) {
+    hw[b] = 0;
+    hc[b] = 0;
+  }
+  __syncthreads();
+  const double wmax = __longlong_as_double(st->x.wmax_bits);
+  int E = 0;
+  frexp(static_cast<double>(n) * wmax, &E);
+  const double scale = wmax > 0.0 ? ldexp(1.0, 62 - E) : 0.0;
+  const unsigned long long prefix = st->prefix;
+  const int lane = threadIdx.x & 63;
+  unsigned long long tot = 0;
+  // every lane runs the same trip count (ballots): in the leading digit
+  // most keys share one bin (sign + exponent), and a wave whose active
+  // lanes agree adds its mass and count once instead of 64 LDS atomics
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * 256; i0 < n;
+       i0 += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t i = i0 + threadIdx.x;
+    unsigned long long fw = 0;
+    bool in = false;
+    int bin = 0;
+    if (i < n) {
+      fw = fixw(w ? w[i] : 1.0, scale);
+      tot += fw;
+      const uint64_t k = f64_key(d[i]);
+      in = ((k ^ prefix) & mask) == 0;
+      bin = static_cast<int>((k >> shift) & (kWqWideBins - 1));
+    }
+    const unsigned long long act = __ballot(in);
+    if (act == 0ull) continue;
+    const int leader = __ffsll(static_cast<long long>(act)) - 1;
+    const int lb = __shfl(bin, leader, 64);
+    const unsigned long long same = __ballot(in && bin == lb);
+    if (same == act) {
+      const unsigned long long sm = wave_sum(in ? fw : 0ull);
+      if (lane == leader) {
+        atomicAdd(&hw[lb], sm);
+        atomicAdd(&hc[lb], static_cast<unsigned>(__popcll(act)));
+      }
+    } else if (in) {
+      atomicAdd(&hw[bin], fw);
+      atomicAdd(&hc[bin], 1u);
+    }
+  }
+  if (first) {
+    tot = wave_sum(tot);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = tot;
+  }
+  __syncthreads();
+  if (first && threadIdx.x == 0) {
+    tot = red[0] + red[1] + red[2] + red[3];
+    if (tot) atomicAdd(&st->x.w_tot, tot);
+    if (blockIdx.x == 0) st->scale = scale;
+  }
+  for (int b = threadIdx.x; b < kWqWideBins; b += 256)
+    if (hc[b]) {
+      atomicAdd(&wide->hw[b], hw[b]);
+      atomicAdd(&wide->hc[b], static_cast<unsigned long long>(hc[b]));
+    }
+}
+
+// the 12-bit digit holding the remaining target (thread t owns 16 bins);
+// the first pass sets the target from the total, the second decides the
+// compaction (the bucket's key count against the buffer)
+__global__ __launch_bounds__(256) void wqc_select_kernel(
+    WQState* st, WQWide* wide, int shift, int first, double alpha) {
+  constexpr int PER = kWqWideBins / 256;
+  __shared__ unsigned long long sc[256];
+  __shared__ int found;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    found = -1;
+    if (first) {
+      const double tg = alpha * static_cast<double>(st->x.w_tot);
+      st->remaining = tg >= 18446744073709551615.0
+                          ? ~0ull : static_cast<unsigned long long>(tg);
+    }
+  }
+  unsigned long long v[PER], c[PER], tot = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = wide->hw[t * PER + j];
+    c[j] = wide->hc[t * PER + j];
+    tot += v[j];
+  }
+  sc[t] = tot;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const unsigned long long a = t >= o ? sc[t - o] : 0;
+    __syncthreads();
+    sc[t] += a;
+    __syncthreads();
+  }
+  unsigned long long run = sc[t] - tot;
+  const unsigned long long rem = st->remaining;
+  const int none = st->none;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const unsigned long long incl = run + v[j];
+    if (!none && c[j] > 0 && run <= rem && incl > rem) {
+      found = t * PER + j;
+      st->prefix |= static_cast<unsigned long long>(t * PER + j) << shift;
+      st->remaining = rem - run;
+      st->w_less += run;
+      if (!first) {
+        st->ccount = 0;
+        st->compacted = c[j] <= static_cast<unsigned long long>(kWqCand);
+      }
+    }
+    run = incl;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    wide->hw[t * PER + j] = 0;
+    wide->hc[t * PER + j] = 0;
+  }
+  __syncthreads();
+  if (t == 0 && found < 0 && !none) st->none = 1;
+}
+
+// keys of the selected 24-bit bucket (and their fixed masses) -> candidate
+// buffer; the largest key below and the smallest key above the bucket
+__global__ __launch_bounds__(256) void wqc_compact_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    WQState* st, WQWide* __restrict__ wide) {
+  const unsigned long long prefix = st->prefix;
+  const unsigned long long mask = ~0ull << 40;
+  const double scale = st->scale;
+  const int comp = st->compacted && !st->none;
+  const int lane = threadIdx.x & 63;
+  unsigned long long kp = 0, kn = ~0ull;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * 256; i0 < n;
+       i0 += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t i = i0 + threadIdx.x;
+    uint64_t k = 0;
+    bool in = false;
+    if (i < n) {
+      k = f64_key(d[i]);
+      const unsigned long long hi = k & mask;
+      in = hi == (prefix & mask);
+      if (hi < (prefix & mask) && k > kp) kp = k;
+      if (hi > (prefix & mask) && k < kn) kn = k;
+    }
+    if (!comp) continue;
+    const unsigned long long m = __ballot(in);
+    if (m == 0ull) continue;
+    const int leader = __ffsll(static_cast<long long>(m)) - 1;
+    unsigned long long base = 0;
+    if (lane == leader)
+      base = atomicAdd(&st->ccount, static_cast<unsigned long long>(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    if (in) {
+      const unsigned long long slot = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (slot < static_cast<unsigned long long>(kWqCand)) {
+        wide->ckey[slot] = k;
+        wide->cw[slot] = fixw(w ? w[i] : 1.0, scale);
+      }
+    }
+  }
+  block_atomic_max_u64<256>(&st->kp_out, kp);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->kn_out, kn);
+}
+
+// one block: the remaining 40 key bits by 8-bit digits over the candidates
+// (or, if the bucket did not fit, over the whole arrays), then the knot's
+// mass, its neighbours and their masses (need_mass: a neighbour outside the
+// bucket, whose mass wqc_mass_kernel sums).  Writes the WQXchg words the
+// sharded path produces, so wq_finalize_kernel applies unchanged.
+__global__ __launch_bounds__(1024) void wqc_finish_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    WQState* st, WQWide* __restrict__ wide) {
+  __shared__ unsigned long long hm[256];
+  __shared__ unsigned long long hcnt[256];
+  __shared__ unsigned long long sc[256];
+  __shared__ unsigned long long red[16];
+  __shared__ int found;
+  const int t = threadIdx.x;
+  const int none = st->none;
+  const int comp = st->compacted;
+  const double scale = st->scale;
+  const long long cnt = comp ? static_cast<long long>(st->ccount) : n;
+  auto key_at = [&](long long i) -> unsigned long long {
+    return comp ? wide->ckey[i] : f64_key(d[i]);
+  };
+  auto mass_at = [&](long long i) -> unsigned long long {
+    return comp ? wide->cw[i] : fixw(w ? w[i] : 1.0, scale);
+  };
+  unsigned long long eqw = 0;
+  for (int pass = 0; pass < 5 && !none; ++pass) {
+    const int shift = 32 - 8 * pass;
+    const unsigned long long mask = ~0ull << (shift + 8);
+    if (t < 256) {
+      hm[t] = 0;
+      hcnt[t] = 0;
+    }
+    if (t == 0) found = -1;
+    __syncthreads();
+    const unsigned long long prefix = st->prefix;
+    for (long long i = t; i < cnt; i += 1024) {
+      const unsigned long long k = key_at(i);
+      if (((k ^ prefix) & mask) == 0) {
+        const int bin = static_cast<int>((k >> shift) & 0xff);
+        atomicAdd(&hm[bin], mass_at(i));
+        atomicAdd(&hcnt[bin], 1ull);
+      }
+    }
+    __syncthreads();
+    if (t < 256) sc[t] = hm[t];
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      unsigned long long a = 0;
+      if (t < 256 && t >= o) a = sc[t - o];
+      __syncthreads();
+      if (t < 256) sc[t] += a;
+      __syncthreads();
+    }
+    const unsigned long long rem = st->remaining;
+    __syncthreads();
+    if (t < 256) {
+      const unsigned long long incl = sc[t], excl = incl - hm[t];
+      if (hcnt[t] > 0 && excl <= rem && incl > rem) {
+        found = t;
+        st->prefix = prefix | (static_cast<unsigned long long>(t) << shift);
+        st->remaining = rem - excl;
+        st->w_less += excl;
+        if (pass == 4) eqw = hm[t];
+      }
+    }
+    __syncthreads();
+    if (found < 0) {  // alpha past the last knot
+      if (t == 0) st->none = 1;
+      break;
+    }
+    if (pass == 4 && t == found) st->w_eq = eqw;
+    __syncthreads();
+  }
+  __syncthreads();
+  // neighbours of the knot (none: the largest key overall, as wq_neighbors)
+  const unsigned long long key = st->none ? ~0ull : st->prefix;
+  unsigned long long kp = 0, kn = ~0ull;
+  for (long long i = t; i < cnt; i += 1024) {
+    const unsigned long long k = key_at(i);
+    if (k < key && k > kp) kp = k;
+    if (k > key && k < kn) kn = k;
+  }
+  kp = wave_max(kp);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(kn, o, 64);
+    kn = b < kn ? b : kn;
+  }
+  if ((t & 63) == 0) red[t >> 6] = kp;
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 16; ++i) kp = red[i] > kp ? red[i] : kp;
+    red[0] = kp;
+  }
+  __syncthreads();
+  kp = red[0];
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = kn;
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 16; ++i) kn = red[i] < kn ? red[i] : kn;
+    red[0] = kn;
+  }
+  __syncthreads();
+  kn = red[0];
+  // outside the bucket only when the bucket holds none (compacted path)
+  const bool kp_in = !comp || kp != 0;
+  const bool kn_in = !comp || kn != ~0ull;
+  if (!kp_in) kp = st->kp_out;
+  if (!kn_in) kn = st->kn_out;
+  unsigned long long sp = 0, sn = 0;
+  for (long long i = t; i < cnt; i += 1024) {
+    const unsigned long long k = key_at(i);
+    if (kp_in && k == kp) sp += mass_at(i);
+    if (kn_in && k == kn) sn += mass_at(i);
+  }
+  sp = wave_sum(sp);
+  sn = wave_sum(sn);
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = sp;
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 16; ++i) sp += red[i];
+    red[0] = sp;
+  }
+  __syncthreads();
+  sp = red[0];
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = sn;
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 16; ++i) sn += red[i];
+    st->x.kprev_x = static_cast<long long>(kp ^ kKeyFlip);
+    st->x.knext_x = static_cast<long long>(kn ^ kKeyFlip);
+    st->x.wprev = kp_in ? sp : 0;
+    st->x.wnext = kn_in ? sn : 0;
+    st->need_mass = (kp_in ? 0 : 1) | (kn_in ? 0 : 2);
+  }
+}
+
+// masses of neighbours outside the compacted bucket (usually nothing to do)
+__global__ __launch_bounds__(256) void wqc_mass_kernel(
+    const double* __restrict__ d, const double* __restrict__ w, int64_t n,
+    WQState* st) {
+  const int need = st->need_mass;
+  if (!need) return;
+  const unsigned long long kp = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
+  const unsigned long long kn = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
+  const double scale = st->scale;
+  unsigned long long sp = 0, sn = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint64_t k = f64_key(d[i]);
+    if ((need & 1) && k == kp) sp += fixw(w ? w[i] : 1.0, scale);
+    if ((need & 2) && k == kn) sn += fixw(w ? w[i] : 1.0, scale);
+  }
+  block_atomic_add_u64<256>(&st->x.wprev, sp);
+  __syncthreads();
+  block_atomic_add_u64<256>(&st->x.wnext, sn);
 }
 
 // one step of the sharded select (see abc_wquantile_step_f64)
@@ -1008,7 +1369,9 @@ int abc_importance_weights_f64(const double* logpd, const double* prior,
   return kOk;
 }
 
-size_t abc_wquantile_workspace_bytes(void) { return sizeof(WQState) + 256; }
+size_t abc_wquantile_workspace_bytes(void) {
+  return ((sizeof(WQState) + 255) / 256) * 256 + sizeof(WQWide) + 256;
+}
 
 int abc_wquantile_step_f64(int step, const double* d, const double* w,
                            int64_t n_local, int64_t n_total, double alpha,
@@ -1055,13 +1418,26 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
   ABC_REQUIRE(ws_bytes >= abc_wquantile_workspace_bytes(),
               "wquantile: workspace too small");
   WQState* s = static_cast<WQState*>(ws);
-  static const int kSeq[] = {kWqReset, kWqWmax, kWqTotal, kWqTarget,
-                             10, 20, 11, 21, 12, 22, 13, 23, 14, 24, 15, 25,
-                             16, 26, 17, 27, kWqNeighbors, kWqMass, kWqFinish};
-  for (int step : kSeq) {
-    const int rc = wq_step(step, d, w, n, n, alpha, out4, s, st);
-    if (rc != kOk) return rc;
-  }
+  WQWide* wide = reinterpret_cast<WQWide*>(static_cast<char*>(ws) +
+                                           ((sizeof(WQState) + 255) / 256) * 256);
+  const unsigned g = stream_grid(n, 256, 1024);
+  ABC_HIP(hipMemsetAsync(wide->hw, 0, 2 * sizeof(wide->hw), st));
+  hipLaunchKernelGGL(wq_reset_kernel, dim3(1), dim3(kBins), 0, st, s);
+  hipLaunchKernelGGL(wq_wmax_kernel, dim3(g), dim3(256), 0, st, w, n, s);
+  hipLaunchKernelGGL(wqc_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s, wide,
+                     52, 0ull, 1);
+  hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 52, 1,
+                     alpha);
+  hipLaunchKernelGGL(wqc_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s, wide,
+                     40, ~0ull << 52, 0);
+  hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 40, 0,
+                     alpha);
+  hipLaunchKernelGGL(wqc_compact_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,
+                     wide);
+  hipLaunchKernelGGL(wqc_finish_kernel, dim3(1), dim3(1024), 0, st, d, w, n, s,
+                     wide);
+  hipLaunchKernelGGL(wqc_mass_kernel, dim3(g), dim3(256), 0, st, d, w, n, s);
+  hipLaunchKernelGGL(wq_finalize_kernel, dim3(1), dim3(1), 0, st, s, alpha, out4);
   ABC_LAUNCH_CHECK("wquantile kernels");
   return kOk;
 }

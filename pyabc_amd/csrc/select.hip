@@ -339,14 +339,18 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
 // single block finishes the remaining 40 key bits, the knot's mass and its
 // neighbours on the candidates.  Same integers as the sharded 8-bit select
 // (the knot key, exact fixed-point masses), so the same result bit for bit.
-__global__ __launch_bounds__(256) void wqc_hist_kernel(
+// 1024-thread blocks, one per CU: each block flushes its (up to 4096)
+// non-empty bins to the global histogram with device atomics, so few large
+// blocks (the flush of 1024 small blocks cost 55 us at N = 1e6)
+constexpr int kWqHistBlock = 1024;
+__global__ __launch_bounds__(kWqHistBlock) void wqc_hist_kernel(
     const double* __restrict__ d, const double* __restrict__ w, int64_t n,
     WQState* __restrict__ st, WQWide* __restrict__ wide, int shift,
     unsigned long long mask, int first) {
   __shared__ unsigned long long hw[kWqWideBins];
   __shared__ unsigned hc[kWqWideBins];
-  __shared__ unsigned long long red[4];
-  for (int b = threadIdx.x; b < kWqWideBins; b += 256) {
+  __shared__ unsigned long long red[kWqHistBlock / 64];
+  for (int b = threadIdx.x; b < kWqWideBins; b += kWqHistBlock) {
     hw[b] = 0;
     hc[b] = 0;
   }
@@ -361,8 +365,8 @@ __global__ __launch_bounds__(256) void wqc_hist_kernel(
   // every lane runs the same trip count (ballots): in the leading digit
   // most keys share one bin (sign + exponent), and a wave whose active
   // lanes agree adds its mass and count once instead of 64 LDS atomics
-  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * 256; i0 < n;
-       i0 += static_cast<int64_t>(gridDim.x) * 256) {
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kWqHistBlock; i0 < n;
+       i0 += static_cast<int64_t>(gridDim.x) * kWqHistBlock) {
     const int64_t i = i0 + threadIdx.x;
     unsigned long long fw = 0;
     bool in = false;
@@ -396,11 +400,12 @@ __global__ __launch_bounds__(256) void wqc_hist_kernel(
   }
   __syncthreads();
   if (first && threadIdx.x == 0) {
-    tot = red[0] + red[1] + red[2] + red[3];
+    tot = 0;
+    for (int i = 0; i < kWqHistBlock / 64; ++i) tot += red[i];
     if (tot) atomicAdd(&st->x.w_tot, tot);
     if (blockIdx.x == 0) st->scale = scale;
   }
-  for (int b = threadIdx.x; b < kWqWideBins; b += 256)
+  for (int b = threadIdx.x; b < kWqWideBins; b += kWqHistBlock)
     if (hc[b]) {
       atomicAdd(&wide->hw[b], hw[b]);
       atomicAdd(&wide->hc[b], static_cast<unsigned long long>(hc[b]));
@@ -1424,12 +1429,13 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
   ABC_HIP(hipMemsetAsync(wide->hw, 0, 2 * sizeof(wide->hw), st));
   hipLaunchKernelGGL(wq_reset_kernel, dim3(1), dim3(kBins), 0, st, s);
   hipLaunchKernelGGL(wq_wmax_kernel, dim3(g), dim3(256), 0, st, w, n, s);
-  hipLaunchKernelGGL(wqc_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s, wide,
-                     52, 0ull, 1);
+  const unsigned gh = stream_grid(n, kWqHistBlock, 256);
+  hipLaunchKernelGGL(wqc_hist_kernel, dim3(gh), dim3(kWqHistBlock), 0, st, d, w, n,
+                     s, wide, 52, 0ull, 1);
   hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 52, 1,
                      alpha);
-  hipLaunchKernelGGL(wqc_hist_kernel, dim3(g), dim3(256), 0, st, d, w, n, s, wide,
-                     40, ~0ull << 52, 0);
+  hipLaunchKernelGGL(wqc_hist_kernel, dim3(gh), dim3(kWqHistBlock), 0, st, d, w, n,
+                     s, wide, 40, ~0ull << 52, 0);
   hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 40, 0,
                      alpha);
   hipLaunchKernelGGL(wqc_compact_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,

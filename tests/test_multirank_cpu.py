@@ -77,3 +77,37 @@ def test_two_ranks_one_sql_run(tmp_path):
     c.close()
     assert [r[0] for r in runs] == [1, 2]
     assert n_pops == n_pops1 > 1
+
+
+def _forced_rank(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      ABC_COMM_FORCE="1")
+    sys.path.insert(0, ROOT)
+    import torch
+    from pyabc_amd.distributed import Comm
+    comm = Comm.from_env("gloo")
+    assert comm.active and comm.world == 1
+    assert Comm.current().active
+    x = torch.arange(12, dtype=torch.float64).reshape(6, 2)
+    out["rows"] = comm.all_gather_rows(x).numpy().tolist()
+    out["ints"] = comm.all_gather_ints(5)
+    out["lists"] = comm.all_gather_int_lists([1, 2, 3])
+    out["sum"] = comm.all_reduce_ints([4, 7])
+    comm.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_forced_one_rank_group_runs_collectives():
+    """ABC_COMM_FORCE=1 under a one-rank process group: the communicator is
+    active and every collective runs (the RCCL self-test's host path) with
+    the identity result."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_forced_rank, args=(port, out), nprocs=1, join=True)
+        res = dict(out)
+    assert res["rows"] == np.arange(12.0).reshape(6, 2).tolist()
+    assert res["ints"] == [5]
+    assert res["lists"] == [[1, 2, 3]]
+    assert res["sum"] == [4, 7]

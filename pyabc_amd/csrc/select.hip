@@ -85,7 +85,7 @@ struct WQState {
   int pad;
   double scale;                 // power-of-two fixed-point scale
   // one-GPU compacted path (abc_wquantile_f64)
-  unsigned long long ccount;    // keys of the 24-bit bucket
+  unsigned long long ccount;    // keys of the 22-bit bucket
   unsigned long long kp_out;    // largest key below the bucket (0: none)
   unsigned long long kn_out;    // smallest key above the bucket (~0: none)
   int compacted;                // the bucket fits the candidate buffer
@@ -94,6 +94,10 @@ struct WQState {
 // 12-bit digit histograms and the candidate buffer follow the state
 constexpr int kWqWideBins = 4096;
 constexpr int kWqCand = 65536;
+// digits of the one-GPU path: 12 + 10 key bits on the full arrays (the
+// second digit narrower: each block flushes at most 1024 non-empty bins),
+// then 8, 8, 8, 8, 8, 2 on the candidates of the 22-bit bucket
+constexpr int kWqCompactShift = 42;
 struct WQWide {
   unsigned long long hw[kWqWideBins];
   unsigned long long hc[kWqWideBins];
@@ -332,11 +336,11 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
 }
 
 // ---------------------------------------------------------------------------
-// One-GPU weighted quantile in ten launches (abc_wquantile_f64): two 12-bit
-// digit passes over (d, w) -- the first also sums the fixed-point total --
-// then one pass that compacts the keys of the selected 24-bit bucket (with
-// their fixed-point masses) and finds the nearest keys outside it; a
-// single block finishes the remaining 40 key bits, the knot's mass and its
+// One-GPU weighted quantile in ten launches (abc_wquantile_f64): a 12-bit
+// and a 10-bit digit pass over (d, w) -- the first also sums the fixed-point
+// total -- then one pass that compacts the keys of the selected 22-bit
+// bucket (with their fixed-point masses) and finds the nearest keys outside
+// it; a single block finishes the remaining 42 key bits, the knot's mass and its
 // neighbours on the candidates.  Same integers as the sharded 8-bit select
 // (the knot key, exact fixed-point masses), so the same result bit for bit.
 // 1024-thread blocks, one per CU: each block flushes its (up to 4096)
@@ -345,7 +349,7 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
 constexpr int kWqHistBlock = 1024;
 __global__ __launch_bounds__(kWqHistBlock) void wqc_hist_kernel(
     const double* __restrict__ d, const double* __restrict__ w, int64_t n,
-    WQState* __restrict__ st, WQWide* __restrict__ wide, int shift,
+    WQState* __restrict__ st, WQWide* __restrict__ wide, int shift, int bits,
     unsigned long long mask, int first) {
   __shared__ unsigned long long hw[kWqWideBins];
   __shared__ unsigned hc[kWqWideBins];
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(kWqHistBlock) void wqc_hist_kernel(
       tot += fw;
       const uint64_t k = f64_key(d[i]);
       in = ((k ^ prefix) & mask) == 0;
-      bin = static_cast<int>((k >> shift) & (kWqWideBins - 1));
+      bin = static_cast<int>((k >> shift) & ((1u << bits) - 1u));
     }
     const unsigned long long act = __ballot(in);
     if (act == 0ull) continue;
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(kWqHistBlock) void wqc_hist_kernel(
     }
 }
 
-// the 12-bit digit holding the remaining target (thread t owns 16 bins);
+// the (12- or 10-bit) digit holding the remaining target (thread t owns 16 bins);
 // the first pass sets the target from the total, the second decides the
 // compaction (the bucket's key count against the buffer)
 __global__ __launch_bounds__(256) void wqc_select_kernel(
@@ -472,13 +476,13 @@ __global__ __launch_bounds__(256) void wqc_select_kernel(
   if (t == 0 && found < 0 && !none) st->none = 1;
 }
 
-// keys of the selected 24-bit bucket (and their fixed masses) -> candidate
+// keys of the selected 22-bit bucket (and their fixed masses) -> candidate
 // buffer; the largest key below and the smallest key above the bucket
 __global__ __launch_bounds__(256) void wqc_compact_kernel(
     const double* __restrict__ d, const double* __restrict__ w, int64_t n,
     WQState* st, WQWide* __restrict__ wide) {
   const unsigned long long prefix = st->prefix;
-  const unsigned long long mask = ~0ull << 40;
+  const unsigned long long mask = ~0ull << kWqCompactShift;
   const double scale = st->scale;
   const int comp = st->compacted && !st->none;
   const int lane = threadIdx.x & 63;
@@ -516,7 +520,7 @@ __global__ __launch_bounds__(256) void wqc_compact_kernel(
   block_atomic_min_u64<256>(&st->kn_out, kn);
 }
 
-// one block: the remaining 40 key bits by 8-bit digits over the candidates
+// one block: the remaining 42 key bits (8-bit digits, a 2-bit last) over the candidates
 // (or, if the bucket did not fit, over the whole arrays), then the knot's
 // mass, its neighbours and their masses (need_mass: a neighbour outside the
 // bucket, whose mass wqc_mass_kernel sums).  Writes the WQXchg words the
@@ -541,9 +545,10 @@ __global__ __launch_bounds__(1024) void wqc_finish_kernel(
     return comp ? wide->cw[i] : fixw(w ? w[i] : 1.0, scale);
   };
   unsigned long long eqw = 0;
-  for (int pass = 0; pass < 5 && !none; ++pass) {
-    const int shift = 32 - 8 * pass;
-    const unsigned long long mask = ~0ull << (shift + 8);
+  for (int pass = 0; pass < 6 && !none; ++pass) {
+    const int shift = pass < 5 ? kWqCompactShift - 8 * (pass + 1) : 0;
+    const int nb = pass < 5 ? 8 : 2;
+    const unsigned long long mask = ~0ull << (shift + nb);
     if (t < 256) {
       hm[t] = 0;
       hcnt[t] = 0;
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(1024) void wqc_finish_kernel(
     for (long long i = t; i < cnt; i += 1024) {
       const unsigned long long k = key_at(i);
       if (((k ^ prefix) & mask) == 0) {
-        const int bin = static_cast<int>((k >> shift) & 0xff);
+        const int bin = static_cast<int>((k >> shift) & ((1u << nb) - 1u));
         atomicAdd(&hm[bin], mass_at(i));
         atomicAdd(&hcnt[bin], 1ull);
       }
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(1024) void wqc_finish_kernel(
         st->prefix = prefix | (static_cast<unsigned long long>(t) << shift);
         st->remaining = rem - excl;
         st->w_less += excl;
-        if (pass == 4) eqw = hm[t];
+        if (pass == 5) eqw = hm[t];
       }
     }
     __syncthreads();
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(1024) void wqc_finish_kernel(
       if (t == 0) st->none = 1;
       break;
     }
-    if (pass == 4 && t == found) st->w_eq = eqw;
+    if (pass == 5 && t == found) st->w_eq = eqw;
     __syncthreads();
   }
   __syncthreads();
@@ -1431,13 +1436,13 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
   hipLaunchKernelGGL(wq_wmax_kernel, dim3(g), dim3(256), 0, st, w, n, s);
   const unsigned gh = stream_grid(n, kWqHistBlock, 256);
   hipLaunchKernelGGL(wqc_hist_kernel, dim3(gh), dim3(kWqHistBlock), 0, st, d, w, n,
-                     s, wide, 52, 0ull, 1);
+                     s, wide, 52, 12, 0ull, 1);
   hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 52, 1,
                      alpha);
   hipLaunchKernelGGL(wqc_hist_kernel, dim3(gh), dim3(kWqHistBlock), 0, st, d, w, n,
-                     s, wide, 40, ~0ull << 52, 0);
-  hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide, 40, 0,
-                     alpha);
+                     s, wide, kWqCompactShift, 10, ~0ull << 52, 0);
+  hipLaunchKernelGGL(wqc_select_kernel, dim3(1), dim3(256), 0, st, s, wide,
+                     kWqCompactShift, 0, alpha);
   hipLaunchKernelGGL(wqc_compact_kernel, dim3(g), dim3(256), 0, st, d, w, n, s,
                      wide);
   hipLaunchKernelGGL(wqc_finish_kernel, dim3(1), dim3(1024), 0, st, d, w, n, s,

@@ -50,7 +50,8 @@ def cpu_baseline(gens, model, x0, d, seconds):
     timed."""
     from oracle import cpu_baseline as cb
     return cb.run(gens, model.A_host, x0.cpu().numpy(), np.full(d, -5.0),
-                  np.full(d, 10.0), model.sigma, 2.0, seconds=seconds)
+                  np.full(d, 10.0), model.sigma, 2.0, seconds=seconds,
+                  kde_dims=sorted({d, 20}))
 
 
 def kde_traffic():
@@ -290,12 +291,28 @@ def main():
             "value": cb["rate"], "unit": "accepted particles/s",
             "cores": cb["workers"], "kind": "port",
             "cpu_model": cb["cpu_model"], "host_cpus": cb["host_cpus"],
+            "physical_cores": cb["physical_cores"],
+            "cpu_share": cb["cpu_share"],
+            "value_all_physical_cores_ideal": cb[
+                "rate_all_physical_cores_ideal"],
+            "kde_pairs_per_s": cb.get("kde_pairs_per_s_1core"),
+            "kde_pairs_per_s_ideal_all_cores": cb.get(
+                "kde_pairs_per_s_ideal_all_cores"),
+            "kde_pairs_basis": f"one core, the reference's MVN.pdf of one "
+                               f"particle against N_prev="
+                               f"{cb.get('kde_n_prev')} (eigh + whitening + "
+                               f"exp-sum, multivariatenormal.py:102-125); "
+                               f"ideal = x physical cores",
+            "tN_fit": cb.get("tN_fit"),
             "per_generation": cb["per_generation"],
             "eps": [g[3] for g in gens],
             "sample": f"the timed schedule's generations {pick} (of "
                       f"{K_}; eps {[round(g[3], 3) for g in gens]}), "
                       f"{cb['seconds_per_generation']:.1f} s each on "
-                      f"{cb['workers']} spawned workers (1 BLAS thread each; "
+                      f"{cb['workers']} spawned workers (min of the "
+                      f"{cb['physical_cores']} physical cores and this "
+                      f"process's {cb['cpu_share']}-CPU share; 1 BLAS thread "
+                      f"each; "
                       f"{cb['accepted']} accepted of {cb['evaluations']} "
                       f"evaluations); value = harmonic mean of the "
                       f"per-generation rates (N_prev={N}, d={d}, S={S}): the "

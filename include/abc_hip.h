@@ -183,8 +183,10 @@ int abc_kde_logsum_f64(const double* Ynew, const double* Yprev,
  * also writes lw2max and the grid g to gscale; ws >= 128 B).  Bfr: new-row
  * fragments (abc_kde_mfma_new_bytes, abc_kde_mfma_new_rows padded rows) and
  * the fp64 whitened rows Ynew [M][D], built by abc_kde_pack_new_mfma from
- * theta.  Rows whose fp32-exponent sum underflows 2^-60 and rows beyond the
- * grid range are re-evaluated exactly in fp64 from Ynew and P.
+ * theta.  Rows whose fp32-exponent sum falls below 2^-32 (of the largest
+ * weight's scale) and rows beyond the grid range are re-evaluated exactly in
+ * fp64 from Ynew and P; their count is the int32 at byte
+ * abc_kde_segments(npad) * M * 8 of the workspace after the call.
  * Workspace: abc_kde_workspace_bytes.
  *                                          multivariatenormal.py:102-125 */
 size_t abc_kde_mfma_prev_bytes(int64_t npad, int d);

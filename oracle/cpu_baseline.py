@@ -24,6 +24,23 @@ generation; a generation's rate is the sum over workers of accepted
 particles / busy time, and the baseline is their harmonic mean -- the rate
 of running each generation to the same population size, as the GPU's value
 is measured.
+
+Core count (n_procs = the physical cores).  The
+physical cores are counted from /proc/cpuinfo (distinct (physical id, core
+id) pairs).  On the GPU box one process may use only its share of the host
+(16 CPUs per GPU; nproc shows the whole machine), so the measured leg runs
+min(physical cores, that share) workers and the line also carries the
+per-worker rate scaled to every physical core, labelled as an ideal
+(linear) extrapolation.  Two more figures follow BASELINE.md section 2:
+
+* KDE pairs/s of the reference's direct pass (``MVN.pdf`` of one particle
+  against N_prev = 1e6, d = 8 and d = 20: scipy's eigh, whitening and
+  exp-sum, multivariatenormal.py:102-125) on ONE core, and the same times
+  the physical cores ("ideal");
+* the generation-time model t(N) = a N + b N^2 fitted to the sampler's rate
+  at N_prev in {1e4, 3e4, 1e5} (sub-populations of the last timed
+  generation, same epsilon), evaluated at the headline N and labelled
+  extrapolated, beside the rate measured directly at that N.
 """
 import multiprocessing as mp
 import os
@@ -32,17 +49,22 @@ import time
 import numpy as np
 
 
-def _worker(paths, seconds, seed, out_q):
+def _worker(tasks, seed, out_q):
+    """``tasks``: (npz path, seconds, n_sub) -- one generation each; n_sub
+    > 0 runs it on the first n_sub particles of the previous population
+    (weights renormalised, the same covariance and epsilon)."""
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import ref_cpu as ref
     rng = np.random.default_rng(seed)
     res = []
-    for path in paths:     # one slice per generation of the GPU's schedule
+    for path, seconds, n_sub in tasks:
         with np.load(path, allow_pickle=False) as f:
             X, w, cov = f["X"], f["w"], f["cov"]
             A_model, x0, lo, sc = f["A_model"], f["x0"], f["lo"], f["sc"]
             eps, sigma, p = float(f["eps"]), float(f["sigma"]), float(f["p"])
+        if n_sub:
+            X, w = X[:n_sub], w[:n_sub] / w[:n_sub].sum()
         A = ref.svd_factor(cov)
         fw = np.ones_like(x0)
         d = X.shape[1]
@@ -64,6 +86,54 @@ def _worker(paths, seconds, seed, out_q):
     out_q.put(res)
 
 
+def _kde_worker(n_prev, dims, reps, out_q):
+    """One core: seconds per reference ``MVN.pdf`` call of one particle
+    against an N_prev population (the per-acceptance KDE of smc.py:722-733)."""
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import ref_cpu as ref
+    rng = np.random.default_rng(7)
+    out = {}
+    for d in dims:
+        X = rng.normal(size=(n_prev, d))
+        w = rng.uniform(0.5, 1.5, n_prev)
+        w /= w.sum()
+        cov = ref.mvn_fit_cov(X, w)
+        th = X[:1] + 0.1
+        ref.kde_transition_pd(th, X, w, cov)      # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ref.kde_transition_pd(th, X, w, cov)
+        out[d] = (time.perf_counter() - t0) / reps
+    out_q.put(out)
+
+
+def physical_cores():
+    """Distinct (physical id, core id) pairs of /proc/cpuinfo."""
+    cores, phys = set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    cores.add((phys, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return len(cores) or (os.cpu_count() or 1)
+
+
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by the box's
+    per-GPU share (the harness exports it as OMP_NUM_THREADS / MAX_JOBS)."""
+    n = len(os.sched_getaffinity(0))
+    for k in ("ABC_CPU_SHARE", "MAX_JOBS", "OMP_NUM_THREADS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return min(n, int(v))
+    return n
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -75,17 +145,30 @@ def cpu_model():
     return "unknown"
 
 
+def _spawn(ctx, q, target, argsets):
+    procs = [ctx.Process(target=target, args=a + (q,)) for a in argsets]
+    for pr in procs:
+        pr.start()
+    res = [q.get() for _ in procs]
+    for pr in procs:
+        pr.join()
+    return res
+
+
 def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
-        tmpdir="/tmp"):
+        tmpdir="/tmp", fit_sizes=(10_000, 30_000, 100_000), fit_seconds=1.5,
+        kde_dims=(8, 20), kde_n_prev=1_000_000):
     """The CPU path over the GPU's own generations: ``gens`` is a list of
     (X, w, cov, eps) -- previous population, its fitted covariance and the
     generation's epsilon -- each run for seconds / len(gens) on every
     worker.  Returns a dict: per-generation accepted/s summed over workers,
     their schedule rate (the harmonic mean: the rate of running every
     generation to the same population size, as the GPU value is), workers,
-    accepted, evaluations, wall seconds."""
+    physical cores, the ideal all-core rate, the t(N) = aN + bN^2 fit, the
+    one-core KDE pairs/s, accepted, evaluations, wall seconds."""
+    phys = physical_cores()
     if workers is None:
-        workers = min(16, os.cpu_count() or 1)
+        workers = max(1, min(phys, cpu_share()))
     paths = []
     for g, (X, w, cov, eps) in enumerate(gens):
         path = os.path.join(tmpdir, f"abc_cpu_baseline_{os.getpid()}_{g}.npz")
@@ -95,22 +178,46 @@ def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
     per = seconds / len(gens)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(paths, per, 1000 + i, q))
-             for i in range(workers)]
     t0 = time.perf_counter()
-    for pr in procs:
-        pr.start()
-    res = [q.get() for _ in procs]
-    for pr in procs:
-        pr.join()
+    res = _spawn(ctx, q, _worker, [([(pa, per, 0) for pa in paths], 1000 + i)
+                                   for i in range(workers)])
     wall = time.perf_counter() - t0
-    for path in paths:
-        os.remove(path)
     rates = [sum(r[g][0] / r[g][2] for r in res) for g in range(len(gens))]
     acc = [sum(r[g][0] for r in res) for g in range(len(gens))]
     ev = [sum(r[g][1] for r in res) for g in range(len(gens))]
     sched = len(rates) / sum(1.0 / max(r, 1e-12) for r in rates)
-    return dict(rate=sched, per_generation=rates, workers=workers,
-                accepted=acc, evaluations=ev, wall=wall,
-                seconds_per_generation=per, cpu_model=cpu_model(),
-                host_cpus=os.cpu_count())
+    out = dict(rate=sched, per_generation=rates, workers=workers,
+               physical_cores=phys, cpu_share=cpu_share(),
+               rate_all_physical_cores_ideal=sched / workers * phys,
+               accepted=acc, evaluations=ev, wall=wall,
+               seconds_per_generation=per, cpu_model=cpu_model(),
+               host_cpus=os.cpu_count())
+    # t(N) = a N + b N^2 from sub-populations of the last generation
+    n_full = gens[-1][0].shape[0]
+    sizes = [n for n in fit_sizes if n < n_full]
+    if len(sizes) >= 2:
+        fr = _spawn(ctx, q, _worker,
+                    [([(paths[-1], fit_seconds, n) for n in sizes], 2000 + i)
+                     for i in range(workers)])
+        rate_n = [sum(r[k][0] / r[k][2] for r in fr) for k in range(len(sizes))]
+        tgen = [n / max(rn, 1e-12) for n, rn in zip(sizes, rate_n)]
+        Amat = np.array([[n, n * n] for n in sizes], dtype=np.float64)
+        (a, b), *_ = np.linalg.lstsq(Amat, np.array(tgen), rcond=None)
+        t_ext = a * n_full + b * n_full ** 2
+        out["tN_fit"] = dict(
+            sizes=sizes, rate=rate_n, t_generation_s=tgen, a=float(a),
+            b=float(b), n=n_full, t_generation_extrapolated_s=float(t_ext),
+            rate_extrapolated=float(n_full / t_ext),
+            rate_measured_last_generation=rates[-1],
+            label="extrapolated: t(N) = a N + b N^2 fitted at the sizes "
+                  "above with the measured workers")
+    if kde_dims:
+        kd = _spawn(ctx, q, _kde_worker, [(kde_n_prev, tuple(kde_dims), 3)])[0]
+        out["kde_pairs_per_s_1core"] = {
+            f"d{d}": kde_n_prev / t for d, t in kd.items()}
+        out["kde_pairs_per_s_ideal_all_cores"] = {
+            f"d{d}": kde_n_prev / t * phys for d, t in kd.items()}
+        out["kde_n_prev"] = kde_n_prev
+    for path in paths:
+        os.remove(path)
+    return out

@@ -324,18 +324,32 @@ def local_k(k, k_fraction, n, d, min_k=10):
     return max([k_, min_k, d])
 
 
-def local_covs(X, w, nbr, scaling=1.0, eps=1e-3):
-    """LocalTransition._cov / _cov_and_inv (local_transition.py:112-139)."""
+def knn_rows(X, k, rows):
+    """knn_indices for the particles ``rows`` only (sorted by distance)."""
+    X = np.asarray(X, dtype=np.float64)
+    kk = min(k + 1, X.shape[0])
+    out = np.empty((len(rows), kk - 1), dtype=np.int64)
+    for r, i in enumerate(rows):
+        d2 = np.sum((X - X[i]) ** 2, axis=1)
+        out[r] = np.argsort(d2, kind="stable")[:kk][1:]
+    return out
+
+
+def local_covs(X, w, nbr, scaling=1.0, eps=1e-3, rows=None):
+    """LocalTransition._cov / _cov_and_inv (local_transition.py:112-139).
+    ``rows``: evaluate only these particles (``nbr`` then holds their
+    neighbour rows, in the same order)."""
     X = np.asarray(X, dtype=np.float64)
     w = np.asarray(w, dtype=np.float64)
     n, d = X.shape
-    covs = np.empty((n, d, d))
-    invs = np.empty((n, d, d))
-    dets = np.empty(n)
-    for i in range(n):
+    rows = np.arange(n) if rows is None else np.asarray(rows)
+    covs = np.empty((len(rows), d, d))
+    invs = np.empty((len(rows), d, d))
+    dets = np.empty(len(rows))
+    for r, i in enumerate(rows):
         if nbr.shape[1] >= 1:
-            deltas = X[nbr[i]] - X[i]
-            lw = w[nbr[i]]
+            deltas = X[nbr[r]] - X[i]
+            lw = w[nbr[r]]
             c = weighted_cov(deltas, lw / lw.sum())
         else:
             c = weighted_cov(np.abs(X), np.array([1.0]))
@@ -347,9 +361,9 @@ def local_covs(X, w, nbr, scaling=1.0, eps=1e-3):
         while det <= 0:
             c = c + np.identity(d) * eps
             det = np.linalg.det(c)
-        covs[i] = c
-        invs[i] = np.linalg.inv(c)
-        dets[i] = det
+        covs[r] = c
+        invs[r] = np.linalg.inv(c)
+        dets[r] = det
     return covs, invs, dets
 
 

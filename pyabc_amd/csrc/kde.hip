@@ -285,7 +285,11 @@ __global__ __launch_bounds__(256) void kde_finalize_kernel(
   }
 }
 
-// exact two-pass evaluation for rows whose fixed-offset sum underflowed
+// exact two-pass evaluation for rows whose fixed-offset sum underflowed.
+// One block per row (grid-stride over the device-side count): 1024 blocks,
+// so up to 4 rows per CU run at once and a launch with few or no fixup rows
+// costs only the empty blocks' exit.
+constexpr int kFixupBlocks = 1024;
 template <typename T, int D>
 __global__ __launch_bounds__(256) void kde_fixup_kernel(
     const T* __restrict__ Ynew, const T* __restrict__ P, int64_t npad,
@@ -484,7 +488,7 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
                      log_const, out_logpd, n_fix, fix_rows,
                      KdeCfg<T>::underflow);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
-  hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(64), dim3(256), 0, stream,
+  hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(kFixupBlocks), dim3(256), 0, stream,
                      Ynew, P, npad, lw2max, log_const, n_fix, fix_rows,
                      out_logpd);
   ABC_LAUNCH_CHECK("kde_fixup_kernel");
@@ -724,7 +728,7 @@ int kde_finish_mfma(const double* partial, int64_t M, int nseg,
   switch (padded_dim(d)) {
 #define CASE(DD)                                                              \
   case DD:                                                                    \
-    hipLaunchKernelGGL((kde_fixup_kernel<double, DD>), dim3(64), dim3(256), 0, \
+    hipLaunchKernelGGL((kde_fixup_kernel<double, DD>), dim3(kFixupBlocks), dim3(256), 0, \
                        stream, Ynew, P, npad, lw2max, log_const, n_fix,       \
                        fix_rows, out_logpd);                                  \
     break;

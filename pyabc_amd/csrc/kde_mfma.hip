@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
 // bounded by ~8e-8 log2(N / S) for a row sum S; rows with S < 2^-32 (dominant
 // exponents beyond ~32) take the exact fp64 fixup (kMfmaFixupSum), so the
 // bound is ~4e-6 at N = 1e6 (measured: tests/test_gpu_fullsize.py, DESIGN
-// section 4).  The opt-in LDS / DMA variants keep the split order.
+// section 4).  At d > 8 (MFMA-bound) the accumulation stays split.
 constexpr int kFoldKL = 4;
 
 // one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
@@ -351,83 +351,11 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
   }
 }
 
-// VALU instructions of one step's sum (16 exps + the tree + the row add,
-// plus the 16 hi + lo adds when not folded): the sched_group_barrier share
-template <int KL>
-constexpr int step_valu() { return KL <= kFoldKL ? 32 : 48; }
-
-// Ablation forms of one step (tuning diagnostics only, ABC_KDE_MFMA_ABL):
-// 1 no exp, 2 no MFMA, 3 neither (adds only), 4 MFMA only.  The results are
-// meaningless; they time the pipes separately.
-template <int ABL, int KH, int KL>
-__device__ __forceinline__ void abl_step(const bf16x8* a, const bf16x8* b,
-                                         f32x16& hi, f32x16& lo) {
-  if constexpr (ABL == 5) {
-    // fold: the lo chain first, then the exact hi products on top of it as
-    // the MFMA's C operand (accuracy probe; saves the VALU hi + lo add)
-    lo = f32x16{};
-#pragma unroll
-    for (int c = 0; c < KL; ++c)
-      lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0, 0, 0);
-    hi = lo;
-#pragma unroll
-    for (int c = 0; c < KH; ++c)
-      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
-  } else if constexpr (ABL == 6) {
-    // fold the other way: the exact hi products first, then the lo chain
-    // accumulated on top of them (rounding at |e|, not at the hi partials)
-    hi = f32x16{};
-#pragma unroll
-    for (int c = 0; c < KH; ++c)
-      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
-#pragma unroll
-    for (int c = 0; c < KL; ++c)
-      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], hi, 0, 0, 0);
-  } else if constexpr (ABL == 2 || ABL == 3) {
-    asm volatile("" : "+v"(hi), "+v"(lo));
-  } else {
-    mfma_step<KH, KL>(a, b, hi, lo);
-  }
-}
-// (the ablated sum is consumed by an empty asm and replaced by 1, so no row
-// reaches the exact fixup)
-template <int ABL, int KL>
-__device__ __forceinline__ float abl_sum(const f32x16& hi, const f32x16& lo) {
-  if constexpr (ABL == 0) return tile_sum<KL>(hi, lo);
-  if constexpr (ABL == 5 || ABL == 6) {
-    float e[16];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v]);
-#pragma unroll
-    for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-      for (int v = 0; v < w; ++v) e[v] += e[v + w];
-    return e[0];
-  }
-  float r;
-  if constexpr (ABL == 2) {
-    r = tile_sum_split(hi, lo);
-  } else if constexpr (ABL == 4) {
-    r = hi[0] + lo[0];
-  } else {
-    float e[16];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) e[v] = hi[v] + lo[v];
-#pragma unroll
-    for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-      for (int v = 0; v < w; ++v) e[v] += e[v + w];
-    r = e[0];
-  }
-  asm volatile("" ::"v"(r));
-  return 1.0f;
-}
-
 // main pass.  Block (rb, s): wave w owns i-tiles (rb*kWaves + w)*IB + t and
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB, bool PIPE, bool SCHED, int ABL = 0>
+template <int KH, int KL, int IB, bool PIPE>
 __device__ __forceinline__ void kde_mfma_body(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -475,31 +403,17 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
         f32x16 hi[2], lo[2];
-        abl_step<ABL, KH, KL>(a[0], bq[0], hi[0], lo[0]);
+        mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           if (q + 1 < 2 * IB)
-            abl_step<ABL, KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
+            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
                               hi[(q + 1) & 1], lo[(q + 1) & 1]);
           if (q + 1 == IB) {  // last MFMA reading tile 0 is issued
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += abl_sum<ABL, KL>(hi[q & 1], lo[q & 1]);
-          if constexpr (SCHED) {
-            // interleave: each MFMA of step q+1 followed by a share of step
-            // q's VALU (16 exp, 16 tree/row adds, 16 hi + lo adds unless folded)
-            constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;
-            if (q + 1 < 2 * IB) {
-#pragma unroll
-              for (int m = 0; m < KT; ++m) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
-              }
-            } else {
-              __builtin_amdgcn_sched_group_barrier(0x002, step_valu<KL>(), 0);
-            }
-          }
+          sacc[q % IB] += tile_sum<KL>(hi[q & 1], lo[q & 1]);
         }
       } else {
 #pragma unroll
@@ -507,8 +421,8 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
-          abl_step<ABL, KH, KL>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += abl_sum<ABL, KL>(hi, lo);
+          mfma_step<KH, KL>(a[q / IB], bq[q % IB], hi, lo);
+          sacc[q % IB] += tile_sum<KL>(hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -527,281 +441,12 @@ __device__ __forceinline__ void kde_mfma_body(
   }
 }
 
-template <int KH, int KL, int IB, bool PIPE, bool SCHED = false>
+template <int KH, int KL, int IB, bool PIPE>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  kde_mfma_body<KH, KL, IB, PIPE, SCHED>(Bfr, M, Afr, npad, split, spb, jseg,
+  kde_mfma_body<KH, KL, IB, PIPE>(Bfr, M, Afr, npad, split, spb, jseg,
                                          partial);
-}
-
-template <int KH, int KL, int ABL>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_abl_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  kde_mfma_body<KH, KL, 3, true, true, ABL>(Bfr, M, Afr, npad, split, spb,
-                                            jseg, partial);
-}
-
-// The same pass software-pipelined ACROSS 64-row chunks: the MFMAs of step
-// q+1 -- for the last step of a chunk, step 0 of the next chunk -- are
-// issued interleaved with the VALU of step q (sched_group_barrier: one MFMA,
-// then a share of the 48 VALU instructions), so no step's exp/add block
-// runs without matrix work beside it.  A row's arithmetic and summation
-// order are those of kde_mfma_kernel: the rows are bit-identical.
-template <int KH, int KL, int IB>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_sw_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  constexpr int KT = KH + KL;
-  constexpr int NS = 2 * IB;                  // steps per 64-row chunk
-  constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;  // VALU per gap
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
-  const int64_t t0 = (rb * kWaves + wave) * IB;
-
-  bf16x8 bq[IB][KT];
-#pragma unroll
-  for (int t = 0; t < IB; ++t)
-#pragma unroll
-    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
-
-  for (int gi = 0; gi < spb; ++gi) {
-    const int seg = s * spb + gi;
-    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
-    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
-    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64 + lane;
-    double S[IB];
-#pragma unroll
-    for (int t = 0; t < IB; ++t) S[t] = 0.0;
-    if (nj > 0) {
-      bf16x8 a[2][KT];
-      f32x16 hi[2], lo[2];
-#pragma unroll
-      for (int c = 0; c < KT; ++c) a[0][c] = Aseg[c * 64];
-#pragma unroll
-      for (int c = 0; c < KT; ++c) a[1][c] = Aseg[(KT + c) * 64];
-      mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
-      for (int jc = 0; jc < nj; jc += 64) {
-        const bool more = jc + 64 < nj;
-        // next chunk's tiles (a re-read of this chunk's on the last one)
-        const bf16x8* __restrict__ an =
-            Aseg + ((more ? jc + 64 : jc) >> 5) * KT * 64;
-        float sacc[IB];
-#pragma unroll
-        for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-          if (q + 1 < NS)
-            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
-                              hi[(q + 1) & 1], lo[(q + 1) & 1]);
-          else if (more)  // step 0 of the next chunk (tile 0 loaded below)
-            mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
-          if (q + 1 == IB) {  // last MFMA reading tile 0 issued
-#pragma unroll
-            for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
-          }
-          if (q + 2 == NS) {  // last MFMA reading tile 1 issued
-#pragma unroll
-            for (int c = 0; c < KT; ++c) a[1][c] = an[(KT + c) * 64];
-          }
-          sacc[q % IB] += tile_sum<KL>(hi[q & 1], lo[q & 1]);
-          if (q + 1 < NS || more) {
-#pragma unroll
-            for (int m = 0; m < KT; ++m) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
-            }
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < IB; ++t) {
-      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
-      const int64_t i = (t0 + t) * 32 + lane;
-      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
-    }
-  }
-}
-
-// L1-relief form: the A fragments of each 64-row chunk are copied ONCE per
-// block into LDS by LDS-DMA (global_load_lds_dwordx4: no staging registers,
-// double-buffered, one barrier per chunk) and every wave of the block reads
-// them from LDS (128 B/clk/CU) instead of each wave pulling its own 10 KiB
-// per chunk through the vector L1 (64 B/clk/CU: the MFMA path alone ran
-// 114 ms at N = M = 1e6, d = 8, L1-bound, tools/kde_variants.py ablations).
-// NW waves per block share one copy; each keeps IB i-tiles of B in
-// registers.  Per-lane arithmetic and summation order are those of
-// kde_mfma_body: rows are bit-identical.
-template <int KH, int KL, int IB, int NW, bool SCHED, int ABL = 0>
-__global__ __launch_bounds__(64 * NW) void kde_mfma_dmab_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  constexpr int KT = KH + KL;
-  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
-  __shared__ bf16x8 As[2][CH][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
-  const int64_t t0 = (rb * NW + wave) * IB;
-
-  bf16x8 bq[IB][KT];
-#pragma unroll
-  for (int t = 0; t < IB; ++t)
-#pragma unroll
-    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
-
-  for (int gi = 0; gi < spb; ++gi) {
-    const int seg = s * spb + gi;
-    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
-    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
-    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
-    double S[IB];
-#pragma unroll
-    for (int t = 0; t < IB; ++t) S[t] = 0.0;
-    // fragment f of a chunk = contiguous 1 KiB at Aseg + (chunk*2*KT + f)*64
-    auto fill = [&](int buf, int jc) {
-      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
-      for (int f = wave; f < CH; f += NW)
-        __builtin_amdgcn_global_load_lds(
-            src + f * 64 + lane,
-            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
-    };
-    __syncthreads();  // the previous segment's readers are done with As
-    if (nj > 0) fill(0, 0);
-    int buf = 0;
-    for (int jc = 0; jc < nj; jc += 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // chunk jc landed (each wave waited for its own pieces) and every wave
-      // is done with chunk jc - 64, whose buffer is refilled now
-      __syncthreads();
-      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
-      const bf16x8(*Ab)[64] = As[buf];
-      float sacc[IB];
-#pragma unroll
-      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
-      bf16x8 a[2][KT];
-#pragma unroll
-      for (int c = 0; c < KT; ++c) a[0][c] = Ab[c][lane];
-#pragma unroll
-      for (int c = 0; c < KT; ++c) a[1][c] = Ab[KT + c][lane];
-      f32x16 hi[2], lo[2];
-      abl_step<ABL, KH, KL>(a[0], bq[0], hi[0], lo[0]);
-#pragma unroll
-      for (int q = 0; q < 2 * IB; ++q) {
-        if (q + 1 < 2 * IB)
-          abl_step<ABL, KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
-                            hi[(q + 1) & 1], lo[(q + 1) & 1]);
-        sacc[q % IB] += abl_sum<ABL, KL>(hi[q & 1], lo[q & 1]);
-        if constexpr (SCHED) {
-          constexpr int VPG = (step_valu<KL>() + KT - 1) / KT;
-          if (q + 1 < 2 * IB) {
-#pragma unroll
-            for (int m = 0; m < KT; ++m) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x002, VPG, 0);
-            }
-          } else {
-            __builtin_amdgcn_sched_group_barrier(0x002, step_valu<KL>(), 0);
-          }
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
-      buf ^= 1;
-    }
-#pragma unroll
-    for (int t = 0; t < IB; ++t) {
-      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
-      const int64_t i = (t0 + t) * 32 + lane;
-      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
-    }
-  }
-}
-
-// Occupancy form for large d (MFMA-bound): one i-tile per wave, the A
-// fragments of each 64-row chunk copied once per block into LDS by LDS-DMA
-// (global_load_lds_dwordx4, no staging registers; double-buffered, one
-// barrier per chunk) and read back one fragment ahead of its MFMA (sched
-// groups DS_READ 1 / MFMA 1), so a wave holds only its B fragments, one
-// accumulator pair and the exp block: three waves per SIMD at d = 20
-// instead of one, and the MFMA chain of one wave runs beside the VALU of
-// another.  Per-lane arithmetic and order are those of kde_mfma_kernel at
-// IB = 1: rows are bit-identical.
-template <int KH, int KL>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_dma_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  constexpr int KT = KH + KL;
-  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
-  __shared__ bf16x8 As[2][CH][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
-  const int64_t t0 = rb * kWaves + wave;
-
-  bf16x8 bq[KT];
-#pragma unroll
-  for (int c = 0; c < KT; ++c) bq[c] = Bfr[(t0 * KT + c) * 64 + lane];
-
-  for (int gi = 0; gi < spb; ++gi) {
-    const int seg = s * spb + gi;
-    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
-    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
-    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
-    double S = 0.0;
-    // fragment f of a chunk = (tile f / KT, slot chunk f % KT): contiguous
-    // 1 KiB at Aseg + (chunk * 2 * KT + f) * 64; wave w copies f = w, w+4..
-    auto fill = [&](int buf, int jc) {
-      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
-      for (int f = wave; f < CH; f += kWaves)
-        __builtin_amdgcn_global_load_lds(
-            src + f * 64 + lane,
-            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
-    };
-    __syncthreads();  // the previous segment's readers are done with As
-    if (nj > 0) fill(0, 0);
-    int buf = 0;
-    for (int jc = 0; jc < nj; jc += 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // chunk jc landed (every wave waited for its own pieces) and every
-      // wave finished chunk jc - 64, whose buffer is refilled next
-      __syncthreads();
-      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
-      float sacc = 0.0f;
-#pragma unroll
-      for (int tile = 0; tile < 2; ++tile) {
-        f32x16 hi = f32x16{}, lo = f32x16{};
-#pragma unroll
-        for (int c = 0; c < KH; ++c) {
-          hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(As[buf][tile * KT + c][lane],
-                                                       bq[c], hi, 0, 0, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
-#pragma unroll
-        for (int c = 0; c < KL; ++c) {
-          lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              As[buf][tile * KT + KH + c][lane], bq[KH + c], lo, 0, 0, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
-        sacc += tile_sum_split(hi, lo);
-      }
-      S += static_cast<double>(sacc);
-      buf ^= 1;  // the next top barrier also ends every read of this buffer
-    }
-    const double tot = S + __shfl_xor(S, 32, 64);
-    const int64_t i = t0 * 32 + lane;
-    if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
-  }
 }
 
 // MFMA-bound form for d > 8.  Per 32x32 tile a wave runs KT = KH + KL
@@ -818,7 +463,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_dma_kernel(
 // arithmetic and summation order are those of kde_mfma_body (split hi / lo
 // accumulators, tile 0 then tile 1 of each chunk): the rows are
 // bit-identical to kde_mfma_kernel's.
-template <int KH, int KL, int IB, bool FOLD>
+template <int KH, int KL, int IB>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -876,7 +521,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
           const bf16x8 a = Ab[tile * KT + c][lane];
 #pragma unroll
           for (int t = 0; t < IB; ++t) {
-            if (c < KH || FOLD)
+            if (c < KH)
               hi[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t][c], hi[t],
                                                               0, 0, 0);
             else
@@ -889,7 +534,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
         }
 #pragma unroll
         for (int t = 0; t < IB; ++t)
-          sacc[t] += FOLD ? tile_sum<0>(hi[t], lo[t]) : tile_sum_split(hi[t], lo[t]);
+          sacc[t] += tile_sum_split(hi[t], lo[t]);
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
@@ -904,97 +549,135 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
   }
 }
 
-// ---- hand-interleaved folded LDS-DMA pass (d > 8, opt-in ABC_KDE_MFMA_LDS2=2)
-// The VALU of one 32-row tile (per i-tile: 16 v_exp_f32, the 15-add tree and
-// the row add) is cut into slices placed in the gaps of the NEXT tile's MFMA
-// chain, one slice after each MFMA, with sched_barrier fences so the compiler
-// keeps exactly that order: an MFMA holds vector issue for 8 of its 32
-// cycles, and a slice of two exps and one add (20 issue cycles) runs in the
-// other 24 (MI355X_MICROARCH.md, MFMA gap fillers).  Per i-tile the 32 ops
-// are  e0 e8  e1 e9 a0  e2 e10 a1 ... e7 e15 a6  a7  b0..b3  c0 c1  d0  s
-// (a: v + 8, b: v + 4, c: v + 2, d: v + 1, s: the row add) -- the tree of
-// tile_sum, so the rows are bit-identical to the FOLD lds2 kernel's.
-struct TileSumState {
-  float e[16];
-};
+// ---- hand-interleaved LDS-DMA passes (d > 8) --------------------------------
+// The VALU of one 32-row tile is cut into slices placed in the gaps of the
+// NEXT tile's MFMA chain, one slice after each MFMA, with sched_barrier
+// fences so the compiler keeps exactly that order: an MFMA holds vector
+// issue for 8 of its 32 cycles, and the slice runs in the other 24
+// (MI355X_MICROARCH.md, MFMA gap fillers).  Every op works in place on the
+// retiring tile's accumulators (no separate exp registers).
+//
+// Sum ops of one i-tile (32): the exps of pair v are issued one slice ahead
+// of the add of pair v - 1, so no add waits on the transcendental it follows:
+//   e0 e8  e1 e9 a0  e2 e10 a1 ... e7 e15 a6  a7  b0..b3  c0 c1  d0  s
+// (a: v += v + 8, b: v + 4, c: v + 2, d: v + 1, s: the row add) -- the tree
+// of tile_sum, so the rows are bit-identical to the plain passes'.
 template <int O>
-__device__ __forceinline__ void tile_sum_op(const f32x16& acc, TileSumState& st,
-                                            float& sacc) {
+__device__ __forceinline__ void sum_op(f32x16& x, float& sacc) {
   if constexpr (O < 2) {
-    st.e[8 * O] = __builtin_amdgcn_exp2f(acc[8 * O]);
+    x[8 * O] = __builtin_amdgcn_exp2f(x[8 * O]);
   } else if constexpr (O < 23) {
-    // the exps of pair v one slice ahead of the add of pair v - 1, so no
-    // add waits on the transcendental it follows
     constexpr int v = 1 + (O - 2) / 3, k = (O - 2) % 3;
-    if constexpr (k == 0) st.e[v] = __builtin_amdgcn_exp2f(acc[v]);
-    else if constexpr (k == 1) st.e[v + 8] = __builtin_amdgcn_exp2f(acc[v + 8]);
-    else st.e[v - 1] += st.e[v - 1 + 8];
+    if constexpr (k == 0) x[v] = __builtin_amdgcn_exp2f(x[v]);
+    else if constexpr (k == 1) x[v + 8] = __builtin_amdgcn_exp2f(x[v + 8]);
+    else x[v - 1] += x[v - 1 + 8];
   } else if constexpr (O == 23) {
-    st.e[7] += st.e[15];
+    x[7] += x[15];
   } else if constexpr (O < 28) {
-    st.e[O - 24] += st.e[O - 24 + 4];
+    x[O - 24] += x[O - 24 + 4];
   } else if constexpr (O < 30) {
-    st.e[O - 28] += st.e[O - 28 + 2];
+    x[O - 28] += x[O - 28 + 2];
   } else if constexpr (O == 30) {
-    st.e[0] += st.e[1];
+    x[0] += x[1];
   } else {
-    sacc += st.e[0];
+    sacc += x[0];
   }
-}
-template <int G, int PER, int O = G * PER>
-__device__ __forceinline__ void tile_sum_slice(const f32x16& acc, TileSumState& st,
-                                               float& sacc) {
-  if constexpr (O < 32 && O < (G + 1) * PER) {
-    tile_sum_op<O>(acc, st, sacc);
-    tile_sum_slice<G, PER, O + 1>(acc, st, sacc);
-  }
-}
-// one gap's slice: gap g of the KT * IB gaps serves i-tile g / KT
-template <int KT, int IB, int G>
-__device__ __forceinline__ void gap_slice(const f32x16 (&acc)[IB],
-                                          TileSumState (&st)[IB],
-                                          float (&sacc)[IB]) {
-  constexpr int t = G / KT, gi = G % KT;
-  constexpr int PER = (32 + KT - 1) / KT;
-  if constexpr (t < IB) tile_sum_slice<gi, PER>(acc[t], st[t], sacc[t]);
 }
 
-// MFMA chain of one tile (folded) with the previous tile's VALU in its gaps
-template <int KT, int IB, bool VALU, int C = 0>
+// Split accumulation (hi and lo accumulators, e = hi + lo rounded once).
+// The lo accumulators are single-buffered: the next chain's first lo MFMA of
+// i-tile t comes after its KH * IB + t hi MFMAs, so the retiring tile's
+// 16 IB  hi += lo  adds (i-tile by i-tile) go in the first GA = KH*IB+IB-1
+// gaps, and the 32 IB sum ops (i-tiles interleaved op by op) in the rest.
+template <int KT, int KH, int IB>
+struct SplitPlan {
+  static constexpr int NG = KT * IB;
+  static constexpr int GA = KH * IB + IB - 1;
+  static constexpr int NA = 16 * IB;
+  static constexpr int NS = 32 * IB;
+  static constexpr int a0(int g) { return g * NA / GA; }
+  static constexpr int s0(int g) { return (g - GA) * NS / (NG - GA); }
+};
+template <int KT, int KH, int IB, int Q, int QE>
+__device__ __forceinline__ void split_add_ops(f32x16 (&h)[IB],
+                                              const f32x16 (&l)[IB]) {
+  if constexpr (Q < QE) {
+    h[Q / 16][Q % 16] += l[Q / 16][Q % 16];
+    split_add_ops<KT, KH, IB, Q + 1, QE>(h, l);
+  }
+}
+template <int IB, int Q, int QE>
+__device__ __forceinline__ void split_sum_ops(f32x16 (&h)[IB], float (&sacc)[IB]) {
+  if constexpr (Q < QE) {
+    sum_op<Q / IB>(h[Q % IB], sacc[Q % IB]);
+    split_sum_ops<IB, Q + 1, QE>(h, sacc);
+  }
+}
+template <int KT, int KH, int IB, int G>
+__device__ __forceinline__ void split_gap_ops(f32x16 (&h)[IB], const f32x16 (&l)[IB],
+                                              float (&sacc)[IB]) {
+  using P = SplitPlan<KT, KH, IB>;
+  if constexpr (G < P::GA) {
+    split_add_ops<KT, KH, IB, P::a0(G), P::a0(G + 1)>(h, l);
+  } else {
+    split_sum_ops<IB, P::s0(G), P::s0(G + 1)>(h, sacc);
+  }
+}
+
+// MFMA chain of one tile with the previous tile's VALU in its gaps.  acc:
+// this tile's hi accumulators; prev: the retiring tile's; lo: the lo
+// accumulators (read as the retiring tile's lo by the first gaps, then
+// overwritten by this chain).
+template <int KT, int KH, int IB, bool VALU, int C = 0>
 __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int lane,
                                           const bf16x8 (&bq)[IB][KT],
-                                          f32x16 (&acc)[IB],
-                                          const f32x16 (&prev)[IB],
-                                          TileSumState (&st)[IB],
-                                          float (&sacc)[IB], bf16x8 (&a)[2]) {
+                                          f32x16 (&acc)[IB], f32x16 (&prev)[IB],
+                                          f32x16 (&lo)[IB], float (&sacc)[IB],
+                                          bf16x8 (&a)[2]) {
   if constexpr (C < KT) {
     // fragment C + 2 is read while C's MFMAs run (a[C & 1] holds C)
     bf16x8 nxt = a[(C + 1) & 1];
     if constexpr (C + 2 < KT) nxt = Ab[tile * KT + C + 2][lane];
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[C & 1], bq[t][C], acc[t],
-                                                       0, 0, 0);
+      if (C >= KH)
+        lo[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            a[C & 1], bq[t][C], C == KH ? f32x16{} : lo[t], 0, 0, 0);
+      else
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VALU) {
-        if (t == 0) gap_slice<KT, IB, C * IB + 0>(prev, st, sacc);
-        if (t == 1) gap_slice<KT, IB, C * IB + 1>(prev, st, sacc);
-        if (t == 2) gap_slice<KT, IB, C * IB + 2>(prev, st, sacc);
+        // t is a compile-time constant after unrolling; each branch names
+        // its gap index
+#define ABC_GAP(TT) \
+  if (t == TT) split_gap_ops<KT, KH, IB, C * IB + TT>(prev, lo, sacc);
+        ABC_GAP(0)
+        ABC_GAP(1)
+        ABC_GAP(2)
+#undef ABC_GAP
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     a[C & 1] = nxt;
-    lds_chain<KT, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, st, sacc, a);
+    lds_chain<KT, KH, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, lo, sacc,
+                                        a);
   }
 }
 
+// The d > 8 default: the split accumulation of kde_mfma_lds2_kernel with
+// the VALU hand-placed in the MFMA gaps; rows bit-identical to it (and to
+// the register kernel).  d = 20, N = M = 262144: 19.3 (lds2) -> 18.0 ms.
+// (The folded accumulation in the same schedule ran 16.8 ms but its error
+// reached 6.3e-6 at N = M = 1e6 against 1.5e-6 -- DESIGN.md section 4 --
+// and was dropped.)
 template <int KH, int KL, int IB>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2f_kernel(
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
   constexpr int CH = 2 * KT;
-  static_assert(IB <= 3, "gap_slice serves at most 3 i-tiles");
+  static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1026,8 +709,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2f_kernel(
     __syncthreads();
     if (nj > 0) fill(0, 0);
     int buf = 0;
-    f32x16 accA[IB], accB[IB];
-    TileSumState st[IB];
+    f32x16 accA[IB], accB[IB], lo[IB];
     float sprev[IB], scur[IB];
 #pragma unroll
     for (int t = 0; t < IB; ++t) sprev[t] = scur[t] = 0.0f;
@@ -1037,129 +719,31 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2f_kernel(
       if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
       const bf16x8(*Ab)[64] = As[buf];
       bf16x8 a[2];
-#pragma unroll
-      for (int t = 0; t < IB; ++t) accA[t] = f32x16{};
       a[0] = Ab[0][lane];
       a[1] = Ab[1][lane];
       if (jc == 0) {  // tile 0, nothing to retire yet
-        lds_chain<KT, IB, false>(Ab, 0, lane, bq, accA, accB, st, sprev, a);
+        lds_chain<KT, KH, IB, false>(Ab, 0, lane, bq, accA, accB, lo, sprev, a);
       } else {        // tile 0 || tile 1 of the previous chunk
-        lds_chain<KT, IB, true>(Ab, 0, lane, bq, accA, accB, st, sprev, a);
+        lds_chain<KT, KH, IB, true>(Ab, 0, lane, bq, accA, accB, lo, sprev, a);
 #pragma unroll
         for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
       }
 #pragma unroll
-      for (int t = 0; t < IB; ++t) {
-        accB[t] = f32x16{};
-        scur[t] = 0.0f;
-      }
+      for (int t = 0; t < IB; ++t) scur[t] = 0.0f;
       a[0] = Ab[KT][lane];
       a[1] = Ab[KT + 1][lane];
       // tile 1 || tile 0 of this chunk
-      lds_chain<KT, IB, true>(Ab, 1, lane, bq, accB, accA, st, scur, a);
+      lds_chain<KT, KH, IB, true>(Ab, 1, lane, bq, accB, accA, lo, scur, a);
 #pragma unroll
       for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
       buf ^= 1;
     }
     if (nj > 0) {  // retire the last tile
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<0>(accB[t], accB[t]);
+      for (int t = 0; t < IB; ++t)
+        sprev[t] += tile_sum_split(accB[t], lo[t]);
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < IB; ++t) {
-      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
-      const int64_t i = (t0 + t) * 32 + lane;
-      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
-    }
-  }
-}
-
-// The same pass with the A fragments of each 64-row chunk staged once per
-// block in LDS (double-buffered) and shared by the kWaves waves, which walk
-// the same j-segments.  Where the register version needs more than 256
-// VGPRs (d > 8: one wave per SIMD, MFMA chain and VALU back to back) this
-// frees the a[2][KT] registers, and L2 serves each fragment once per block
-// instead of once per wave.  Per-lane arithmetic and order are those of
-// kde_mfma_kernel<.., PIPE = false>: the two give bit-identical rows.
-template <int KH, int KL, int IB>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  constexpr int KT = KH + KL;
-  constexpr int CH = 2 * KT * 64;  // fragments of one 64-row chunk
-  constexpr int PER = (CH + 64 * kWaves - 1) / (64 * kWaves);
-  __shared__ bf16x8 As[2][CH];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
-  const int64_t t0 = (rb * kWaves + wave) * IB;
-
-  bf16x8 bq[IB][KT];
-#pragma unroll
-  for (int t = 0; t < IB; ++t)
-#pragma unroll
-    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
-
-  for (int gi = 0; gi < spb; ++gi) {
-    const int seg = s * spb + gi;
-    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
-    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
-    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
-    double S[IB];
-#pragma unroll
-    for (int t = 0; t < IB; ++t) S[t] = 0.0;
-    bf16x8 stage[PER];
-    if (nj > 0) {
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int idx = threadIdx.x + q * 64 * kWaves;
-        if (idx < CH) As[0][idx] = Aseg[idx];
-      }
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int jc = 0; jc < nj; jc += 64) {
-      const bool more = jc + 64 < nj;
-      if (more) {  // next chunk into registers; written after this compute
-        const bf16x8* __restrict__ an = Aseg + ((jc + 64) >> 5) * KT * 64;
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const int idx = threadIdx.x + q * 64 * kWaves;
-          if (idx < CH) stage[q] = an[idx];
-        }
-      }
-      const bf16x8* __restrict__ Ab = As[buf];
-      float sacc[IB];
-#pragma unroll
-      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 2 * IB; ++q) {
-        const int tile = q / IB, it = q % IB;
-        f32x16 hi = f32x16{}, lo = f32x16{};
-#pragma unroll
-        for (int c = 0; c < KH; ++c)
-          hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              Ab[(tile * KT + c) * 64 + lane], bq[it][c], hi, 0, 0, 0);
-#pragma unroll
-        for (int c = 0; c < KL; ++c)
-          lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              Ab[(tile * KT + KH + c) * 64 + lane], bq[it][KH + c], lo, 0, 0, 0);
-        sacc[it] += tile_sum_split(hi, lo);
-      }
-#pragma unroll
-      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
-      if (more) {
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const int idx = threadIdx.x + q * 64 * kWaves;
-          if (idx < CH) As[buf ^ 1][idx] = stage[q];
-        }
-      }
-      __syncthreads();
-      buf ^= 1;
     }
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
@@ -1224,127 +808,51 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib) {
   return p;
 }
 
+// Runtime knobs (tuning only; tests/test_gpu_kernels.py
+// test_kde_mfma_launch_knobs_bit_identical checks that each leaves every row
+// unchanged): ABC_KDE_MFMA_SPLIT (j-segment blocks per row block),
+// ABC_KDE_MFMA_IB (i-tiles per wave), ABC_KDE_MFMA_PIPE (software
+// pipelining of the register kernel), ABC_KDE_MFMA_LDS2 at d > 8 (0: the
+// register kernel, 1: LDS-DMA A fragments).
+int env_int(const char* name, int dflt) {
+  const char* env = getenv(name);
+  return env ? atoi(env) : dflt;
+}
+
 template <int D, int IB>
 void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
                  const bf16x8* Afr, int64_t npad, double* partial,
                  hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
-  // software pipelining pays at D <= 8 (VALU-bound); at larger D the
-  // MFMA chain dominates and the lower register count wins (bench_kde sweep)
-  bool pipe = D <= 8;
-  if (const char* env = getenv("ABC_KDE_MFMA_PIPE")) pipe = atoi(env) != 0;
-  bool lds = false;
-  if (const char* env = getenv("ABC_KDE_MFMA_LDS")) lds = atoi(env) != 0;
-  // sched_group_barrier interleave of step q+1's MFMAs with step q's VALU:
-  // 156.4 -> 151.2 ms at N = M = 1e6, d = 8 with SLP-packed adds, but with
-  // plain adds (no SLP, Makefile) the hardware's own interleave is faster:
-  // 143.4 (sched) vs 139.2 ms (tools/kde_ab.py); slower at d = 4 and 20
-  bool sched = false;
-  if (const char* env = getenv("ABC_KDE_MFMA_SCHED")) sched = atoi(env) != 0;
-  bool sw = false;
-  if (const char* env = getenv("ABC_KDE_MFMA_SW")) sw = atoi(env) != 0;
-  int dmab = 0;  // LDS-DMA shared A: 1 = 4 waves per block, 2 = 8 waves
-  if (const char* env = getenv("ABC_KDE_MFMA_DMAB")) dmab = atoi(env);
-  // LDS-DMA A with IB MFMAs per LDS fragment: the MFMA-bound shapes (d > 8)
-  // (default at d > 8: d = 20 21.5 -> 20.4 ms, d = 12 18.6 -> 15.1, d = 24
-  // 27.0 -> 23.8 at N = M = 262144, rows bit-identical; tools/kde_variants.py)
-  // 2 (default at d > 8): the hand-interleaved folded form, d = 20 19.5 ->
-  // 17.3 ms at N = M = 262144, full-size error 6.3e-6 (split form: 1.5e-6);
-  // 1: the split form (kde_mfma_lds2_kernel); 0: the register kernel
-  int lds2 = D > 8 ? 2 : 0;
-  if (const char* env = getenv("ABC_KDE_MFMA_LDS2")) lds2 = atoi(env);
+  const dim3 block(64 * kWaves);
   if constexpr (D > 8) {
+    // 2: hand-interleaved split pass; 1: LDS-DMA A fragments, compiler
+    // schedule (d = 20: 21.5 -> 20.4 ms at N = M = 262144 against the
+    // register kernel); 0: the register kernel.  Rows bit-identical.
+    const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
     if (lds2 == 2) {
-      hipLaunchKernelGGL((kde_mfma_lds2f_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                         dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                         p.split, p.spb, p.jseg, partial);
+      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         p.spb, p.jseg, partial);
       return;
     }
-    if (lds2) {
-      bool fold = false;
-      if (const char* env = getenv("ABC_KDE_MFMA_FOLD")) fold = atoi(env) != 0;
-      if (fold)
-        hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
-                           dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr,
-                           npad, p.split, p.spb, p.jseg, partial);
-      else
-        hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
-                           dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr,
-                           npad, p.split, p.spb, p.jseg, partial);
+    if (lds2 != 0) {
+      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         p.spb, p.jseg, partial);
       return;
     }
   }
-  if constexpr (D <= 8) {
-    if (dmab == 1 || dmab == 2) {
-#define DMAB(NW, SC)                                                           \
-  hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, NW, SC>),  \
-                     dim3(grid / (NW / kWaves)), dim3(64 * NW), 0, st, Bfr, M, \
-                     Afr, npad, p.split, p.spb, p.jseg, partial)
-      int abl = 0;
-      if (const char* env = getenv("ABC_KDE_MFMA_ABL")) abl = atoi(env);
-      if (abl == 4) {  // MFMA + LDS-DMA only (diagnostic)
-        hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, 4,
-                                                 false, 4>),
-                           dim3(grid), dim3(256), 0, st, Bfr, M, Afr, npad,
-                           p.split, p.spb, p.jseg, partial);
-        return;
-      }
-      if (abl == 2) {  // exp + adds only (diagnostic)
-        hipLaunchKernelGGL((kde_mfma_dmab_kernel<Mk<D>::KH, Mk<D>::KL, IB, 4,
-                                                 false, 2>),
-                           dim3(grid), dim3(256), 0, st, Bfr, M, Afr, npad,
-                           p.split, p.spb, p.jseg, partial);
-        return;
-      }
-      if (dmab == 2 && (p.row_blocks & 1) == 0) {
-        if (sched) DMAB(8, true);
-        else DMAB(8, false);
-      } else {  // 8-wave blocks need an even row-block count
-        if (sched) DMAB(4, true);
-        else DMAB(4, false);
-      }
-#undef DMAB
-      return;
-    }
-  }
-  if constexpr (D == 8 && IB == 3) {
-    int abl = 0;
-    if (const char* env = getenv("ABC_KDE_MFMA_ABL")) abl = atoi(env);
-    if (abl >= 1 && abl <= 6) {
-#define ABLK(A)                                                                \
-  hipLaunchKernelGGL((kde_mfma_abl_kernel<Mk<D>::KH, Mk<D>::KL, A>), dim3(grid), \
-                     dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,     \
-                     p.spb, p.jseg, partial)
-      if (abl == 1) ABLK(1);
-      else if (abl == 5) ABLK(5);
-      else if (abl == 6) ABLK(6);
-      else if (abl == 2) ABLK(2);
-      else if (abl == 3) ABLK(3);
-      else ABLK(4);
-#undef ABLK
-      return;
-    }
-  }
-  if (sw)
-    hipLaunchKernelGGL((kde_mfma_sw_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                       p.split, p.spb, p.jseg, partial);
-  else if (sched)
-    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, true>),
-                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                       p.split, p.spb, p.jseg, partial);
-  else if (lds)
-    hipLaunchKernelGGL((kde_mfma_lds_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                       p.split, p.spb, p.jseg, partial);
-  else if (pipe)
+  // software pipelining pays at D <= 8 (VALU-bound); at larger D the MFMA
+  // chain dominates and the lower register count wins (bench_kde sweep)
+  if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
-                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                       p.split, p.spb, p.jseg, partial);
+                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                       p.spb, p.jseg, partial);
   else
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
-                       dim3(grid), dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad,
-                       p.split, p.spb, p.jseg, partial);
+                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                       p.spb, p.jseg, partial);
 }
 
 template <int D>
@@ -1352,19 +860,14 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
                      const bf16x8* Afr, const double* P, int64_t npad, int d,
                      const double* lw2max, double log_const, double* out,
                      void* ws, size_t ws_bytes, hipStream_t st) {
-  // i-tiles per wave: Mk<D>::IB (the row padding unit) or half of it
+  // i-tiles per wave: Mk<D>::IB (the row padding unit) or a divisor of it
   // (tuning override ABC_KDE_MFMA_IB); a row's arithmetic is the same
   constexpr int IBF = Mk<D>::IB;
   constexpr int IBH = IBF > 1 ? IBF / 2 : 1;
   constexpr int IB2 = IBF == 3 ? 2 : IBF;  // the third choice at D <= 8
   int ib = IBF;
-  if (const char* env = getenv("ABC_KDE_MFMA_IB")) {
-    const int v = atoi(env);
-    if (v == IBH || v == IB2) ib = v;
-  }
-  bool dma = false;
-  if (const char* env = getenv("ABC_KDE_MFMA_DMA")) dma = atoi(env) != 0;
-  if (dma) ib = 1;
+  const int v = env_int("ABC_KDE_MFMA_IB", IBF);
+  if (v == IBH || v == IB2) ib = v;
   const MPlan p = make_mplan<D>(M, npad, ib);
   const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
@@ -1375,12 +878,7 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.nseg * M) * 8);
   int* fix_rows = n_fix + 4;
   ABC_HIP(hipMemsetAsync(n_fix, 0, 16, st));
-  if (dma)
-    hipLaunchKernelGGL((kde_mfma_dma_kernel<Mk<D>::KH, Mk<D>::KL>),
-                       dim3(static_cast<unsigned>(p.row_blocks * p.split)),
-                       dim3(64 * kWaves), 0, st, Bfr, M, Afr, npad, p.split,
-                       p.spb, p.jseg, partial);
-  else if (ib == IBF)
+  if (ib == IBF)
     launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, st);
   else if (ib == IB2)
     launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, partial, st);

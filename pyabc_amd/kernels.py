@@ -270,6 +270,8 @@ class PackedPopulation:
             return out
         wsb = nat.lib().abc_kde_workspace_bytes(M, self.npad, self.d)
         ws = WS.get(wsb, "kde")
+        # the fixup-row counter follows the [nseg][M] fp64 partials
+        self._fix_at = (ws, nat.lib().abc_kde_segments(self.npad) * M * 8)
         if self.precision == "mfma":
             if not isinstance(Y, WhitenedRows):
                 raise TypeError("mfma KDE pass takes rows from whiten()")
@@ -285,6 +287,16 @@ class PackedPopulation:
 
     def logpdf(self, theta):
         return self.logpdf_whitened(self.whiten(theta))
+
+    def fixup_rows(self):
+        """Rows the last fp32 / MFMA pass of this population handed to the
+        exact fp64 fixup (sum below the pass's threshold, or beyond the
+        grid); synchronises with the stream.  Valid until the next KDE call
+        reuses the workspace."""
+        ws, off = getattr(self, "_fix_at", (None, 0))
+        if ws is None or self.precision == "f64":
+            return 0
+        return int(ws[off:off + 4].view(torch.int32).item())
 
 
 def importance_weights(logpd, prior=None, prior_const=1.0):

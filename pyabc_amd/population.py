@@ -144,6 +144,7 @@ class ColumnarPopulation:
     def __init__(self, theta, w, d, names, stats_T=None, stat_keys=None,
                  m=0, normalize=True):
         self._pending = None      # host offload in flight (to_host)
+        self._offload_lock = threading.Lock()
         self.theta = theta
         self.d = d
         self.names = list(names)
@@ -199,9 +200,15 @@ class ColumnarPopulation:
                    if t is not None and t.is_cuda)
 
     def _finish_offload(self):
-        fut, self._pending = self._pending, None
-        for n, t in fut.result().items():
-            self.__dict__["_" + n] = t
+        # readers may race (the History writer thread, the caller): the
+        # first one installs the host columns, the others find _pending gone
+        with self.__dict__.setdefault("_offload_lock", threading.Lock()):
+            fut = self.__dict__.get("_pending")
+            if fut is None:
+                return
+            for n, t in fut.result().items():
+                self.__dict__["_" + n] = t
+            self.__dict__["_pending"] = None
 
     def get_model_probabilities(self):
         return self._model_probabilities

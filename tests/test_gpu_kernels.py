@@ -76,6 +76,9 @@ def test_kde_underflow_rows_fixup(K, precision):
     theta = np.concatenate([X[:50] + 0.01, X[:20] + 6.0])   # far rows
     pp = _packed(K, X, w, cov, precision)
     lp = host(pp.logpdf(dev(theta)))
+    if precision != "f64":
+        # the 20 far rows (and no near row) went through the exact fixup
+        assert pp.fixup_rows() == 20
     U, rank, log_pdet = ref.psd_whitening(cov)
     ls = ref.kde_logsum(theta @ U, X @ U, np.log(w))
     expect = ls - 0.5 * (rank * ref.LOG_2PI + log_pdet)
@@ -145,6 +148,42 @@ def test_kde_mfma_rows_independent_of_launch(K):
     for lo, hi in [(0, 1), (17, 1234), (1500, 3000), (2999, 3000)]:
         part = host(pp.logpdf(dev(theta[lo:hi])))
         np.testing.assert_array_equal(part, full[lo:hi])
+
+
+KNOBS = {
+    4: [("ABC_KDE_MFMA_PIPE", "0"), ("ABC_KDE_MFMA_IB", "1"),
+        ("ABC_KDE_MFMA_IB", "2"), ("ABC_KDE_MFMA_SPLIT", "4")],
+    8: [("ABC_KDE_MFMA_PIPE", "0"), ("ABC_KDE_MFMA_IB", "1"),
+        ("ABC_KDE_MFMA_IB", "2"), ("ABC_KDE_MFMA_SPLIT", "1"),
+        ("ABC_KDE_MFMA_SPLIT", "8")],
+    20: [("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_LDS2", "0"),
+         ("ABC_KDE_MFMA_IB", "1"), ("ABC_KDE_MFMA_SPLIT", "2"),
+         ("ABC_KDE_MFMA_PIPE", "1")],
+}
+
+
+@pytest.mark.parametrize("d", sorted(KNOBS))
+def test_kde_mfma_launch_knobs_bit_identical(K, d, monkeypatch):
+    """Every runtime knob of abc_kde_logpdf_mfma (kde_mfma.hip launch_mfma)
+    is a launch-shape choice: the rows are bit-identical under each."""
+    rng = np.random.default_rng(20 + d)
+    N, M = 20000, 2500
+    X = rng.normal(size=(N, d))
+    w = rng.uniform(0.5, 1.5, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = np.concatenate([X[rng.integers(0, N, M - 500)]
+                            + 0.2 * rng.normal(size=(M - 500, d)),
+                            1.7 * X[:500]])          # low-density rows too
+    pp = _packed(K, X, w, cov, "mfma")
+    base = host(pp.logpdf(dev(theta)))
+    want = ref.kde_transition_pd(theta[:64], X, w, cov)
+    assert np.max(np.abs(np.exp(base[:64]) / want - 1)) < 1e-5
+    for key, val in KNOBS[d]:
+        monkeypatch.setenv(key, val)
+        got = host(pp.logpdf(dev(theta)))
+        monkeypatch.delenv(key)
+        np.testing.assert_array_equal(got, base, err_msg=f"{key}={val}")
 
 
 # ------------------------------------------------------------ (a1) fit

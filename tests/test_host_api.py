@@ -275,3 +275,31 @@ def test_gather_segments_gloo(world):
         assert ints == [s * 10 + 1 for s in range(world)]
         assert lists == [[s, s + 5] for s in range(world)]
         assert red == [sum(range(world)), 2 * world]
+
+
+def test_columnar_offload_finish_is_thread_safe():
+    """Two readers of an offloaded population racing on the first column
+    access: both get the host columns, nothing raises."""
+    import concurrent.futures as cf
+    import threading
+    import time
+    from pyabc_amd.population import ColumnarPopulation
+    th = torch.arange(12, dtype=torch.float64).reshape(6, 2)
+    w = torch.full((6,), 1 / 6, dtype=torch.float64)
+    d = torch.arange(6, dtype=torch.float64)
+    pop = ColumnarPopulation(th, w, d, ["a", "b"], normalize=False)
+    gate = threading.Event()
+
+    def slow_copy():
+        gate.wait(5)
+        time.sleep(0.05)
+        return {"theta": th.clone(), "w": w.clone(), "d": d.clone(),
+                "stats_T": None}
+    with cf.ThreadPoolExecutor(4) as ex:
+        pop._pending = ex.submit(slow_copy)
+        readers = [ex.submit(lambda: pop.theta.sum().item()) for _ in range(2)]
+        readers.append(ex.submit(lambda: pop.w.sum().item()))
+        gate.set()
+        got = [r.result(timeout=10) for r in readers]
+    assert got[0] == got[1] == float(th.sum())
+    assert pop._pending is None

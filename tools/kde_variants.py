@@ -3,8 +3,8 @@ that every variant's rows are bit-identical to the default's.
 
     python tools/kde_variants.py d N [name=ENV:VAL,ENV:VAL ...]
 
-Without variant arguments a fixed occupancy sweep is run (IB / PIPE / SCHED /
-DMAB, see kde_mfma.hip launch_mfma)."""
+Without variant arguments the tuning knobs of kde_mfma.hip launch_mfma are
+swept (IB / PIPE / SPLIT / LDS2); each must leave every row unchanged."""
 import math
 import os
 import sys
@@ -16,22 +16,17 @@ sys.path.insert(0, ".")
 from pyabc_amd import kernels as K  # noqa: E402
 from oracle import ref_cpu as ref  # noqa: E402
 
-KEYS = ("ABC_KDE_MFMA_IB", "ABC_KDE_MFMA_PIPE", "ABC_KDE_MFMA_SCHED",
-        "ABC_KDE_MFMA_SW", "ABC_KDE_MFMA_DMA",
-        "ABC_KDE_MFMA_LDS", "ABC_KDE_MFMA_SPLIT", "ABC_KDE_MFMA_VPG",
-        "ABC_KDE_MFMA_ABL", "ABC_KDE_MFMA_DMAB")
+KEYS = ("ABC_KDE_MFMA_IB", "ABC_KDE_MFMA_PIPE", "ABC_KDE_MFMA_SPLIT",
+        "ABC_KDE_MFMA_LDS2", "ABC_KDE_MFMA_FOLD")
 
 SWEEP = [
     ("default", {}),
-    ("ib3_pipe", {"ABC_KDE_MFMA_SCHED": "0"}),
-    ("ib3_nopipe", {"ABC_KDE_MFMA_PIPE": "0", "ABC_KDE_MFMA_SCHED": "0"}),
-    ("ib2_pipe", {"ABC_KDE_MFMA_IB": "2", "ABC_KDE_MFMA_SCHED": "0"}),
-    ("ib2_nopipe", {"ABC_KDE_MFMA_IB": "2", "ABC_KDE_MFMA_PIPE": "0",
-                    "ABC_KDE_MFMA_SCHED": "0"}),
-    ("ib2_sched", {"ABC_KDE_MFMA_IB": "2"}),
-    ("ib1_pipe", {"ABC_KDE_MFMA_IB": "1", "ABC_KDE_MFMA_SCHED": "0"}),
-    ("dmab4", {"ABC_KDE_MFMA_DMAB": "1"}),
-    ("dmab8", {"ABC_KDE_MFMA_DMAB": "2", "ABC_KDE_MFMA_SCHED": "0"}),
+    ("pipe0", {"ABC_KDE_MFMA_PIPE": "0"}),
+    ("ib2", {"ABC_KDE_MFMA_IB": "2"}),
+    ("ib1", {"ABC_KDE_MFMA_IB": "1"}),
+    ("lds2_1", {"ABC_KDE_MFMA_LDS2": "1"}),
+    ("lds2_0", {"ABC_KDE_MFMA_LDS2": "0"}),
+    ("split8", {"ABC_KDE_MFMA_SPLIT": "8"}),
 ]
 
 

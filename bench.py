@@ -67,59 +67,97 @@ def kde_traffic():
 
 
 def kde_pmc(d):
-    """Per-tile instruction counts of kde_mfma_kernel from the committed
+    """Per-tile instruction counts of the MFMA KDE kernel from the committed
     rocprofv3 PMC passes (tools/kde_pmc.py), if they were taken at this d."""
-    path = os.path.join(ROOT, "profiles", "r02_kde_pmc.json")
-    if not os.path.exists(path):
+    for tag in ("r03", "r02"):
+        path = os.path.join(ROOT, "profiles", f"{tag}_kde_pmc.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                t = json.load(f)
+            if t.get("d") == d:
+                return t, path
+    return None, None
+
+
+PROBE_MIX = {8: 0, 20: 1}   # tools/probes/issue_probe.hip variants
+
+
+def issue_probe(d, waves_per_simd=2):
+    """Live ceiling of the KDE kernel's per-tile instruction mix on THIS GPU
+    (tools/probes/issue_probe.hip: the mix with no memory traffic, VALU in
+    the MFMA gaps, at the kernel's 2 waves per SIMD): ns per tile and SIMD,
+    or None when the probe library is not built or has no mix for d."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "probes", "libabc_probe.so")
+    v = PROBE_MIX.get(d)
+    if v is None or not os.path.exists(path):
         return None
-    with open(path) as f:
-        t = json.load(f)
-    return t if t.get("d") == d else None
+    lib = ctypes.CDLL(path)
+    lib.abc_probe_kde_mix.restype = ctypes.c_double
+    lib.abc_probe_kde_mix.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    torch.cuda.synchronize()
+    ns = lib.abc_probe_kde_mix(v, waves_per_simd, 100000)
+    return ns if ns > 0 else None
 
 
 def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
                  pairs_per_launch, tiles_per_launch):
-    """Roofline of the dominant kernel (kde_mfma_kernel).
+    """Roofline of the dominant kernel (the MFMA KDE pass).
 
     The pass is bound by the SIMD's instruction issue: per 32x32 tile of
     pairs a wave issues MFMAs (the d-dimensional exponent on the matrix
-    cores) and VALU (v_exp_f32, row-sum add; plus the hi+lo add when the
-    accumulation is not folded, d > 8).  The ceiling is
-    the instruction mix COUNTED by PMC (profiles/r02_kde_pmc.json: per-tile
-    SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32, SQ_INSTS_MFMA) priced at the
-    guide's per-instruction SIMD issue cycles (plain or packed VALU 4,
-    transcendental 8,
-    MFMA issue 8 / matrix pipe 32) at the 2.4 GHz peak clock on 1024 SIMDs:
+    cores) and VALU (v_exp_f32, row-sum tree; plus the hi+lo add when the
+    accumulation is split, d > 8).  The ceiling is MEASURED live: the probe
+    (tools/probes/issue_probe.hip) runs that per-tile mix -- PMC-counted,
+    profiles/r0*_kde_pmc.json -- with no memory traffic and the VALU spread
+    over the MFMA gaps, at the kernel's occupancy (2 waves per SIMD) on
+    every SIMD of this GPU, so clock and dual-wave issue are those the chip
+    really sustains:
 
-        t_ceiling = tiles * max(4 (V - T) + 8 T + 8 F, 32 F) / (1024 * 2.4e9)
+        t_ceiling = tiles / 1024 SIMDs * t_probe(per tile per SIMD)
 
-    frac = t_ceiling / t_launch (<= 1).  achieved / peak are the same ratio
-    in SURVEY 8(d)'s algorithmic unit (3d+4 FLOP per pair).  The FP32
-    vector-peak figure of a VALU-only pass is reported beside it as
-    ``valu_equiv`` (it exceeds 1: the MFMA does the d-dimensional part)."""
-    pmc = kde_pmc(d)
+    frac = t_ceiling / t_launch.  achieved / peak are the same ratio in
+    SURVEY 8(d)'s algorithmic unit (3d+4 FLOP per pair).  The static
+    pricing of the same mix at the guide's single-wave issue costs and
+    2.4 GHz is kept beside it (``static_issue``), and the FP32 vector-peak
+    figure of a VALU-only pass as ``valu_equiv`` (it exceeds 1: the MFMA
+    does the d-dimensional part)."""
+    pmc, pmc_path = kde_pmc(d)
     pairs_per_s = pairs_per_launch / avg_launch_s
     fpp = 3 * d + 4
+    D = K.padded_dim(d)
+    KL = (7 * D + 4 + 15) // 16
     if pmc is not None:
         pt = pmc["per_tile"]
         V, T, F = (pt["SQ_INSTS_VALU"], pt.get("SQ_INSTS_VALU_TRANS_F32", 0.0),
                    pt["SQ_INSTS_MFMA"])
-        src = "profiles/r02_kde_pmc.json (rocprofv3 --pmc, per-tile counts)"
+        src = f"{os.path.relpath(pmc_path, ROOT)} (rocprofv3 --pmc, per-tile)"
     else:   # static count of the kernel's per-tile code (DESIGN.md §4)
-        D = K.padded_dim(d)
-        KL = (7 * D + 4 + 15) // 16
         F = (D + 6 + 15) // 16 + KL
         # folded accumulation (KL <= 4): no hi + lo add (kde_mfma.hip)
         V, T = (32.0 if KL <= 4 else 48.0), 16.0
         src = "static per-tile instruction count (no PMC file for this d)"
     cyc = max(4 * (V - T) + 8 * T + 8 * F, 32 * F)
-    t_ceil = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
+    t_static = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
+    ns_probe = issue_probe(d)
+    if ns_probe is not None:
+        t_ceil = tiles_per_launch * ns_probe * 1e-9 / 1024
+        basis = ("live issue probe on this GPU (tools/probes/issue_probe.hip: "
+                 "the kernel's per-tile mix, no memory traffic, VALU in the "
+                 "MFMA gaps, 2 waves per SIMD) x tiles / 1024 SIMDs; "
+                 f"mix counts: {src}; algorithmic {fpp} FLOP/pair")
+    else:
+        t_ceil = t_static
+        basis = ("SIMD issue ceiling of the instruction mix (VALU 4, TRANS 8, "
+                 "MFMA 8 issue / 32 pipe cycles per wave64 instruction, 1024 "
+                 f"SIMDs at 2.4 GHz; probe library not built); {src}; "
+                 f"algorithmic {fpp} FLOP/pair")
     frac = t_ceil / avg_launch_s
     peak_tf = achieved_tf / frac
     mfma_tf = 32768 * F * tiles_per_launch / avg_launch_s / 1e12
     return {
-        "bound": "valu",
-        "kernel": "kde_mfma_kernel (exact-grid bf16 pieces: "
+        "bound": "issue (MFMA + VALU)",
+        "kernel": "MFMA KDE pass (exact-grid bf16 pieces: "
                   "v_mfma_f32_32x32x16_bf16 for the d-dim exponent -- at "
                   "d <= 8 hi and lo in one accumulator -- then v_exp_f32 + "
                   "the row-sum add per pair on the VALU)",
@@ -129,13 +167,12 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "frac": frac,
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "peak_basis": "SIMD issue ceiling of the PMC-counted instruction mix "
-                      "(VALU 4, TRANS 8, MFMA 8 issue / 32 pipe cycles per "
-                      "wave64 instruction, 1024 SIMDs at 2.4 GHz), expressed "
-                      f"in algorithmic {fpp} FLOP/pair; {src}",
-        "ceiling_cycles_per_tile": cyc,
-        "measured_cycles_per_tile": avg_launch_s * 1024 * CLOCK_HZ
-        / tiles_per_launch,
+        "peak_basis": basis,
+        "probe_ns_per_tile_per_simd": ns_probe,
+        "ceiling_ms": t_ceil * 1e3,
+        "static_issue": {"cycles_per_tile": cyc,
+                         "ceiling_ms": t_static * 1e3,
+                         "frac": t_static / avg_launch_s},
         "flops_per_pair": fpp,
         "avg_launch_ms": avg_launch_s * 1e3,
         "pairs_per_launch": pairs_per_launch,

@@ -471,7 +471,8 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
   constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform: the LDS-DMA fill loop and its M0 address stay scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = blockIdx.x % split;
   const int64_t rb = blockIdx.x / split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
@@ -680,7 +681,8 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
   static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform: the LDS-DMA fill loop and its M0 address stay scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int s = blockIdx.x % split;
   const int64_t rb = blockIdx.x / split;
   const int64_t t0 = (rb * kWaves + wave) * IB;

@@ -1,0 +1,115 @@
+// Issue-ceiling probe for the MFMA KDE pass (measurement infrastructure,
+// not part of libabc_hip.so; bench.py loads it to price its roofline).
+//
+// One "step" is the per-(32x32 tile, i-tile) instruction mix of the KDE
+// kernels with NO memory traffic: NM v_mfma_f32_32x32x16_bf16 on one
+// accumulator (random bf16 operands), NE v_exp_f32 and NA v_add_f32 on
+// independent registers, the VALU spread evenly over the MFMA gaps in
+// program order (the best placement a schedule can reach).  The kernel is
+// launched with WPS waves per SIMD (the KDE kernels' occupancy) on every
+// SIMD of the chip, so the measured time per step and SIMD is the
+// throughput ceiling of that mix at the clock the chip holds under it:
+//
+//   t_ceiling(launch) = tiles / 1024 SIMDs * ns_per_step
+//
+// Mixes (PMC-counted per tile, profiles/r0*_kde_pmc*.json):
+//   0: d <= 8, folded accumulation   -- 5 MFMA, 16 exp, 23 other VALU
+//   1: d = 20, split accumulation    -- 11 MFMA, 16 exp, 40 other VALU
+//
+//   hipcc --offload-arch=gfx950 -O3 -shared -fPIC issue_probe.hip \
+//         -o libabc_probe.so
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define ABC_EXP(a) asm volatile("v_exp_f32 %0, %0" : "+v"(a));
+#define ABC_ADD(a, s) asm volatile("v_add_f32 %0, %0, %1" : "+v"(a) : "v"(s));
+
+template <int NM, int NE, int NA>
+__global__ __launch_bounds__(256) void mix_kernel(float* out, int iters) {
+  // random-looking bf16 operands (all-zero operands raise the clock)
+  uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
+  bf16x8 a, b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h ^= h >> 13; h *= 0x5bd1e995u;
+    a[e] = static_cast<short>(0x3C00 | (h & 0x7F));
+    b[e] = static_cast<short>(0xBC00 | ((h >> 8) & 0x7F));
+  }
+  f32x16 acc = {};
+  float v[16];
+  const float s = 1e-7f * (threadIdx.x & 7);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = -1e-3f * (threadIdx.x + k);
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+#pragma unroll
+      for (int k = m * NE / NM; k < (m + 1) * NE / NM; ++k) ABC_EXP(v[k & 15])
+#pragma unroll
+      for (int k = m * NA / NM; k < (m + 1) * NA / NM; ++k)
+        ABC_ADD(v[(k + 5) & 15], s)
+    }
+  }
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += v[k] + acc[k];
+  out[blockIdx.x * 256 + threadIdx.x] = t;
+}
+
+template <int NM, int NE, int NA>
+double time_mix(int waves_per_simd, int iters, int cus, float* out) {
+  const int blocks = cus * waves_per_simd;  // 4 waves per block, 1 per SIMD
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; ++rep) {  // rep 0 warms the clock
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((mix_kernel<NM, NE, NA>), dim3(blocks), dim3(256), 0, 0,
+                       out, iters);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep > 0 && ms < best) best = ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  // every SIMD runs waves_per_simd waves of iters steps
+  return best * 1e6 / (static_cast<double>(waves_per_simd) * iters);
+}
+
+}  // namespace
+
+extern "C" {
+
+// ns per step per SIMD of mix `variant` at `waves_per_simd` waves per SIMD
+// (< 0 on error).  Blocks: one per CU per wave slot.
+double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1.0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    return -1.0;
+  if (waves_per_simd < 1 || waves_per_simd > 8 || iters < 1) return -1.0;
+  float* out = nullptr;
+  if (hipMalloc(&out, static_cast<size_t>(cus) * 8 * 256 * 4) != hipSuccess)
+    return -1.0;
+  double ns = -1.0;
+  switch (variant) {
+    case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
+    case 1: ns = time_mix<11, 16, 40>(waves_per_simd, iters, cus, out); break;
+    default: break;
+  }
+  (void)hipFree(out);
+  return ns;
+}
+
+}  // extern "C"

@@ -102,7 +102,9 @@ def main():
                 "unit": "pairs", "per_unit": 3 * d + 4, "bound": "valu_issue",
                 "achieved": ach, "peak": rl["peak"], "ach_unit": "TFLOP/s",
                 "frac": rl["frac"], "units_per_s": pairs / t,
-                "ceiling_cycles_per_tile": rl["ceiling_cycles_per_tile"],
+                "ceiling_ms": rl["ceiling_ms"],
+                "probe_ns_per_tile_per_simd": rl["probe_ns_per_tile_per_simd"],
+                "static_cycles_per_tile": rl["static_issue"]["cycles_per_tile"],
                 "valu_equiv_frac_fp32": rl["valu_equiv"]["frac"],
                 "mfma_bf16_frac": rl["mfma_bf16"]["frac"],
                 "N": N, "M": N, "d": d}), flush=True)

@@ -19,6 +19,7 @@
 // fp64 terms under one global offset, exact fixup for underflowing rows.
 #include "common.hpp"
 #include "philox.hpp"
+#include "spatial.hpp"
 
 namespace abc {
 
@@ -59,18 +60,47 @@ __device__ inline float knn_filter_bound(double tau, int d, double A) {
   return __double2float_ru(T);
 }
 
+// Tiled prep (spatial.hpp): fp32 centred coordinates in Morton order (one
+// wave per tile of 64 sorted positions, padding positions at kFar), the
+// tile's bounding box of those fp32 values, and the coordinate bound A.
+constexpr float kFar = 1e30f;  // (kFar - x)^2 overflows to +inf
+
 template <int D>
 __global__ __launch_bounds__(256) void knn_prep_kernel(
-    const double* __restrict__ X, int64_t N, float* __restrict__ Xf,
+    const double* __restrict__ X, int64_t N, const int32_t* __restrict__ perm,
+    int T, float* __restrict__ Xs, float* __restrict__ tbox,
     unsigned long long* __restrict__ amax) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int t = static_cast<int>((static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) >> 6);
+  const int64_t s = static_cast<int64_t>(t) * kTile + lane;
+  const bool valid = t < T && s < N;
   double m = 0.0;
-  if (i < N) {
+  float xf[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xf[q] = kFar;
+  if (valid) {
+    const int64_t n = perm[s];
 #pragma unroll
     for (int q = 0; q < D; ++q) {
-      const double v = X[i * D + q] - X[q];
-      Xf[i * D + q] = static_cast<float>(v);
+      const double v = X[n * D + q] - X[q];
+      xf[q] = static_cast<float>(v);
       m = fmax(m, fabs(v));
+    }
+  }
+  if (t < T) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      Xs[s * D + q] = xf[q];
+      float lo = valid ? xf[q] : INFINITY, hi = valid ? xf[q] : -INFINITY;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, o, 64));
+        hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+      }
+      if (lane == 0) {
+        tbox[(static_cast<int64_t>(t) * 2) * D + q] = lo;
+        tbox[(static_cast<int64_t>(t) * 2 + 1) * D + q] = hi;
+      }
     }
   }
   block_atomic_max_u64<256>(
@@ -191,104 +221,135 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
   return __shfl(tk, lk, 64);
 }
 
-// One wave per R rows, no block barriers: every lane streams one candidate
-// per step (fp32 centred coordinates, prefetched one step ahead) against the
-// wave's rows (packed-fp32 pairs in VGPRs); lanes passing the fp32 filter
-// append the candidate INDEX to the row's LDS buffer; a full buffer is
-// re-ranked by exact fp64 distance in registers (reg_bitonic) and cut back
-// to k, which sets tau.  Buffers hold indices only (H*64*4 B per row).
-// The per-step test is ONE compare per row: lanes past N carry coordinates
-// whose d2f is +inf, rows past rhi a threshold of -inf, and the row itself
-// (d2f = 0) is dropped by the exact ranking (knn_sort_cut), so the common
-// step -- no lane passes for any row -- is R compares, R ballots and one
-// branch.
+// One wave per R rows (R consecutive rows of the Morton order), no block
+// barriers.  Candidates stream tile by tile (64 sorted positions, one per
+// lane; fp32 centred coordinates) against the wave's rows (packed-fp32
+// pairs in VGPRs); lanes passing the fp32 filter append the candidate's
+// ORIGINAL index to the row's LDS buffer; a full buffer is re-ranked by exact
+// fp64 distance in registers (reg_bitonic) and cut back to k, which sets tau.
+// Tiles: first the wave's home tile and its two neighbours (they fill the
+// buffers and set tau), then all others in order, 64 at a time: lane l
+// tests tile tb + l against every row (box distance with the filter's own
+// rounded operations, spatial.hpp) and only tiles some row could take a
+// candidate from are streamed.  The skipped tiles hold no candidate the
+// filter would pass, so sets, order and distances are those of the full
+// scan.  The per-step test is ONE compare per row: padding positions carry
+// coordinates whose d2f is +inf, rows past the list a threshold of -inf, and
+// the row itself (d2f = 0) is dropped by the exact ranking (knn_sort_cut).
+template <int D, int H, int R>
+__device__ inline void knn_step(const float* __restrict__ Xs,
+                                const int32_t* __restrict__ perm,
+                                const double* __restrict__ X, int t,
+                                const f32x2 (&xrf)[R / 2][D], float (&Tf)[R],
+                                int (&cnt)[R], const int64_t (&row)[R],
+                                int (&buf)[R][H * 64], int k, double A,
+                                int lane) {
+  constexpr int CAP = H * 64;
+  const int64_t j = static_cast<int64_t>(t) * kTile + lane;
+  float xj[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xj[q] = Xs[j * D + q];
+  float d2f[R];
+#pragma unroll
+  for (int p = 0; p < R / 2; ++p) {
+    f32x2 acc = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const f32x2 df = xrf[p][q] - f32x2{xj[q], xj[q]};
+      acc = __builtin_elementwise_fma(df, df, acc);
+    }
+    d2f[2 * p] = acc.x;
+    d2f[2 * p + 1] = acc.y;
+  }
+  uint64_t m[R];
+  uint64_t any = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    m[r] = __ballot(d2f[r] < Tf[r]);
+    any |= m[r];
+  }
+  if (!any) return;
+  const int jo = perm[j];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (!m[r]) continue;
+    bool cand = d2f[r] < Tf[r];
+    if (cnt[r] + __popcll(m[r]) > CAP) {
+      const double tau = knn_sort_cut<D, H>(X, row[r], buf[r], cnt[r], k, lane,
+                                            nullptr, nullptr);
+      cnt[r] = k;
+      Tf[r] = knn_filter_bound(tau, D, A);
+      cand = cand && d2f[r] < Tf[r];
+      m[r] = __ballot(cand);
+    }
+    if (cand) buf[r][cnt[r] + __popcll(m[r] & ((1ull << lane) - 1ull))] = jo;
+    cnt[r] += __popcll(m[r]);
+  }
+}
+
 template <int D, int H, int R>
 __global__ __launch_bounds__(64) void knn_kernel(
-    const double* __restrict__ X, const float* __restrict__ Xf,
-    const unsigned long long* __restrict__ amax, int64_t N, int k,
-    int64_t rlo, int64_t rhi, int32_t* __restrict__ nbr,
-    double* __restrict__ nbr_d2) {
-  // query rows [rlo, rhi) against all N; row r's output is row r - rlo
+    const double* __restrict__ X, const float* __restrict__ Xs,
+    const int32_t* __restrict__ perm, const float* __restrict__ tbox, int T,
+    const unsigned long long* __restrict__ amax, int k,
+    const int32_t* __restrict__ rows, const int* __restrict__ nrows_p,
+    int64_t rlo, int32_t* __restrict__ nbr, double* __restrict__ nbr_d2) {
+  // rows[] = sorted positions of the query rows; row r's output is row r - rlo
   constexpr int CAP = H * 64;
   __shared__ int buf[R][CAP];
   const int lane = threadIdx.x;
-  const int64_t row0 = rlo + static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t nrows = *nrows_p;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * R;
+  if (w0 >= nrows) return;
   const double A = __longlong_as_double(static_cast<long long>(*amax));
-  constexpr float kFar = 1e30f;  // (kFar - x)^2 overflows to +inf
 
   f32x2 xrf[R / 2][D];   // rows in pairs for packed fp32 math
-#pragma unroll
-  for (int p = 0; p < R / 2; ++p) {
-    const int64_t ra = row0 + 2 * p < rhi ? row0 + 2 * p : rhi - 1;
-    const int64_t rb = row0 + 2 * p + 1 < rhi ? row0 + 2 * p + 1 : rhi - 1;
-#pragma unroll
-    for (int q = 0; q < D; ++q) xrf[p][q] = f32x2{Xf[ra * D + q], Xf[rb * D + q]};
-  }
+  float xr[R][D];
+  int64_t row[R];
   float Tf[R];
   int cnt[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    Tf[r] = row0 + r < rhi ? INFINITY : -INFINITY;
+    const int64_t li = w0 + r < nrows ? w0 + r : nrows - 1;
+    const int64_t sp = rows[li];
+    row[r] = perm[sp];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xr[r][q] = Xs[sp * D + q];
+    Tf[r] = w0 + r < nrows ? INFINITY : -INFINITY;
     cnt[r] = 0;
   }
-  float nx[D];
 #pragma unroll
-  for (int q = 0; q < D; ++q) nx[q] = lane < N ? Xf[lane * D + q] : kFar;
+  for (int p = 0; p < R / 2; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) xrf[p][q] = f32x2{xr[2 * p][q], xr[2 * p + 1][q]};
 
-  for (int64_t base = 0; base < N; base += 64) {
-    const int64_t j = base + lane;
-    float xj[D];
+  const int home = static_cast<int>(rows[w0] / kTile);
+  const int wlo = home > 0 ? home - 1 : 0;
+  const int whi = home + 1 < T ? home + 1 : T - 1;
+  for (int t = wlo; t <= whi; ++t)
+    knn_step<D, H, R>(Xs, perm, X, t, xrf, Tf, cnt, row, buf, k, A, lane);
+  for (int tb = 0; tb < T; tb += 64) {
+    const int t = tb + lane;
+    bool need = false;
+    if (t < T && (t < wlo || t > whi)) {
+      const float* lo = tbox + static_cast<int64_t>(t) * 2 * D;
 #pragma unroll
-    for (int q = 0; q < D; ++q) xj[q] = nx[q];
-    const int64_t jn = j + 64;
-#pragma unroll
-    for (int q = 0; q < D; ++q) nx[q] = jn < N ? Xf[jn * D + q] : kFar;
-    float d2f[R];
-#pragma unroll
-    for (int p = 0; p < R / 2; ++p) {
-      f32x2 acc = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        const f32x2 df = xrf[p][q] - f32x2{xj[q], xj[q]};
-        acc = __builtin_elementwise_fma(df, df, acc);
-      }
-      d2f[2 * p] = acc.x;
-      d2f[2 * p + 1] = acc.y;
+      for (int r = 0; r < R; ++r) need = need || box_dist2<D>(xr[r], lo, lo + D) < Tf[r];
     }
-    uint64_t m[R];
-    uint64_t any = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      m[r] = __ballot(d2f[r] < Tf[r]);
-      any |= m[r];
-    }
-    if (!any) continue;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (!m[r]) continue;
-      const int64_t row = row0 + r;
-      bool cand = d2f[r] < Tf[r];
-      if (cnt[r] + __popcll(m[r]) > CAP) {
-        const double tau = knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane,
-                                              nullptr, nullptr);
-        cnt[r] = k;
-        Tf[r] = knn_filter_bound(tau, D, A);
-        cand = cand && d2f[r] < Tf[r];
-        m[r] = __ballot(cand);
-      }
-      if (cand) buf[r][cnt[r] + __popcll(m[r] & ((1ull << lane) - 1ull))] =
-          static_cast<int>(j);
-      cnt[r] += __popcll(m[r]);
+    uint64_t mask = __ballot(need);
+    while (mask) {
+      const int tt = tb + __builtin_ctzll(mask);
+      mask &= mask - 1;
+      knn_step<D, H, R>(Xs, perm, X, tt, xrf, Tf, cnt, row, buf, k, A, lane);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int64_t row = row0 + r;
-    if (row < rhi)
-      knn_sort_cut<D, H>(X, row, buf[r], cnt[r], k, lane, nbr + (row - rlo) * k,
-                         nbr_d2 ? nbr_d2 + (row - rlo) * k : nullptr);
+    if (w0 + r < nrows)
+      knn_sort_cut<D, H>(X, row[r], buf[r], cnt[r], k, lane, nbr + (row[r] - rlo) * k,
+                         nbr_d2 ? nbr_d2 + (row[r] - rlo) * k : nullptr);
   }
 }
 
@@ -763,6 +824,70 @@ void convert(const S* src, int64_t n, D* dst, hipStream_t st) {
 }
 inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
+// Workspace of the spatial index (spatial.hpp) over n points padded to
+// whole tiles: header (ext keys, counters) | keys_in[n] | keys_out[n] |
+// vals_in[n] | perm[T*64] | tbox[T][2][8] | sort temp.
+struct SpatialWs {
+  unsigned long long* ext;  // [16]: per-dim min keys, then max keys
+  int* count;
+  uint64_t* keys_in;
+  uint64_t* keys_out;
+  int32_t* vals_in;
+  int32_t* perm;
+  float* tbox;
+  void* temp;
+  size_t temp_bytes;
+  int T;
+};
+
+static size_t spatial_ws_bytes(int64_t n) {
+  const int64_t T = ceil_div(n > 0 ? n : 1, kTile);
+  return 256 + 2 * al256(static_cast<size_t>(n) * 8) + al256(static_cast<size_t>(n) * 4) +
+         al256(static_cast<size_t>(T) * kTile * 4) + al256(static_cast<size_t>(T) * 2 * 8 * 4) +
+         al256(sort_pairs_temp_bytes(n));
+}
+
+static SpatialWs spatial_ws(void* ws, int64_t n) {
+  SpatialWs v;
+  char* q = static_cast<char*>(ws);
+  v.T = static_cast<int>(ceil_div(n > 0 ? n : 1, kTile));
+  v.ext = reinterpret_cast<unsigned long long*>(q);
+  v.count = reinterpret_cast<int*>(q + 128);
+  q += 256;
+  v.keys_in = reinterpret_cast<uint64_t*>(q);
+  q += al256(static_cast<size_t>(n) * 8);
+  v.keys_out = reinterpret_cast<uint64_t*>(q);
+  q += al256(static_cast<size_t>(n) * 8);
+  v.vals_in = reinterpret_cast<int32_t*>(q);
+  q += al256(static_cast<size_t>(n) * 4);
+  v.perm = reinterpret_cast<int32_t*>(q);
+  q += al256(static_cast<size_t>(v.T) * kTile * 4);
+  v.tbox = reinterpret_cast<float*>(q);
+  q += al256(static_cast<size_t>(v.T) * 2 * 8 * 4);
+  v.temp = q;
+  v.temp_bytes = al256(sort_pairs_temp_bytes(n));
+  return v;
+}
+
+// Morton order of X (spatial.hpp): ext, keys, sort -> keys_out / perm (the
+// padding positions of the last tile map to particle 0).
+template <int D>
+static int spatial_sort_population(const double* X, int64_t N, SpatialWs& v,
+                                   hipStream_t st) {
+  ABC_HIP(hipMemsetAsync(v.ext, 0xff, 64, st));
+  ABC_HIP(hipMemsetAsync(v.ext + 8, 0, 64 + 8, st));
+  hipLaunchKernelGGL((sp_extent_kernel<D>), dim3(stream_grid(N, 256, 64)), dim3(256),
+                     0, st, X, N, v.ext);
+  hipLaunchKernelGGL((sp_key_kernel<D>), dim3(ceil_div(N, 256)), dim3(256), 0, st,
+                     X, N, X, v.ext, v.keys_in, v.vals_in);
+  ABC_HIP(sort_pairs(v.temp, v.temp_bytes, v.keys_in, v.keys_out, v.vals_in, v.perm,
+                     N, morton_bits(D) * D, st));
+  const int64_t pad = static_cast<int64_t>(v.T) * kTile - N;
+  if (pad > 0) ABC_HIP(hipMemsetAsync(v.perm + N, 0, pad * 4, st));
+  return kOk;
+}
+
+
 }  // namespace abc
 
 using namespace abc;
@@ -796,8 +921,10 @@ int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
 
 size_t abc_knn_workspace_bytes(int64_t N, int k) {
   (void)k;
-  // fp32 centred coordinates [N][8] + the coordinate bound A
-  return static_cast<size_t>(N > 0 ? N : 1) * 8 * 4 + 256;
+  // amax | rows[N] | fp32 sorted coordinates [T*64][8] | spatial index
+  const int64_t T = ceil_div(N > 0 ? N : 1, kTile);
+  return 256 + al256(static_cast<size_t>(N > 0 ? N : 1) * 4) +
+         al256(static_cast<size_t>(T) * kTile * 8 * 4) + spatial_ws_bytes(N > 0 ? N : 1);
 }
 
 int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
@@ -812,26 +939,32 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
   if (nrows == 0) return kOk;
   ABC_REQUIRE(X && nbr && ws, "knn: null pointer");
   ABC_REQUIRE(ws_bytes >= abc_knn_workspace_bytes(N, k), "knn: workspace too small");
-  unsigned long long* amax = static_cast<unsigned long long*>(ws);
-  float* Xf = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
+  ABC_REQUIRE(d >= 1 && d <= 8, "knn: unsupported d=%d (d <= 8)", d);
+  char* q = static_cast<char*>(ws);
+  unsigned long long* amax = reinterpret_cast<unsigned long long*>(q);
+  q += 256;
+  int32_t* rows = reinterpret_cast<int32_t*>(q);
+  q += al256(static_cast<size_t>(N) * 4);
+  const int64_t T = ceil_div(N, kTile);
+  float* Xs = reinterpret_cast<float*>(q);
+  q += al256(static_cast<size_t>(T) * kTile * 8 * 4);
+  SpatialWs v = spatial_ws(q, N);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
-  const unsigned pg = static_cast<unsigned>(ceil_div(N, 256));
-  int rows = kKnnRows;  // rows per wave (tuning override ABC_KNN_ROWS=16)
-  if (const char* env = getenv("ABC_KNN_ROWS")) rows = atoi(env) == 16 ? 16 : 8;
-  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, rows));
+  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, kKnnRows));
   const int64_t rlo = row0, rhi = row0 + nrows;
-#define KNN(DD, H, R)                                                           \
-  hipLaunchKernelGGL((knn_kernel<DD, H, R>), dim3(grid), dim3(64), 0, st, X,    \
-                     Xf, amax, N, k, rlo, rhi, nbr, nbr_d2)
-#define L(DD)                                                                   \
-  {                                                                             \
-    hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(pg), dim3(256), 0, st, X, N, \
-                       Xf, amax);                                               \
-    if (k <= 64) {                                                              \
-      if (rows == 16) KNN(DD, 2, 16); else KNN(DD, 2, 8);                       \
-    } else {                                                                    \
-      if (rows == 16) KNN(DD, 4, 16); else KNN(DD, 4, 8);                       \
-    }                                                                           \
+#define KNN(DD, H)                                                               \
+  hipLaunchKernelGGL((knn_kernel<DD, H, kKnnRows>), dim3(grid), dim3(64), 0, st, \
+                     X, Xs, v.perm, v.tbox, v.T, amax, k, rows, v.count, rlo, nbr, \
+                     nbr_d2)
+#define L(DD)                                                                    \
+  {                                                                              \
+    const int rc = spatial_sort_population<DD>(X, N, v, st);                     \
+    if (rc != kOk) return rc;                                                    \
+    hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(ceil_div(T, 4)), dim3(256), 0, \
+                       st, X, N, v.perm, v.T, Xs, v.tbox, amax);                 \
+    hipLaunchKernelGGL(sp_rows_in_range_kernel, dim3(ceil_div(N, 256)), dim3(256), \
+                       0, st, v.perm, N, rlo, rhi, rows, v.count);               \
+    if (k <= 64) KNN(DD, 2); else KNN(DD, 4);                                    \
   }
   switch (d) {
     case 1: L(1) break;
@@ -842,9 +975,6 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
     case 6: L(6) break;
     case 7: L(7) break;
     case 8: L(8) break;
-    default:
-      set_error("knn: unsupported d=%d (d <= 8)", d);
-      return kUnsupported;
   }
 #undef L
 #undef KNN

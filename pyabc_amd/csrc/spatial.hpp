@@ -1,0 +1,148 @@
+// Spatial index of a particle population for the LocalTransition kNN
+// (cKDTree(X).query(X, k + 1), local_transition.py:82-83).
+//
+// The population is put in Morton order (d coordinates quantised to
+// b = min(21, 63 / d) bits each on the population's bounding box, keys
+// radix-sorted with their indices) and cut into tiles of 64 consecutive
+// particles.  A tile carries the bounding box of its fp32 centred
+// coordinates (x - X[0], the same rounding the kNN filter computes with).
+// The kNN skips a tile for a query row when the box distance, computed with
+// the filter's own rounded operations (rounding is monotone), is not below
+// the row's filter threshold: no candidate in the tile could pass the
+// filter, so the neighbour sets are those of the full scan.  (The same
+// bound does not pay for the density pass: in 6-D the k = 50 local kernels
+// are as wide as the population -- a numpy simulation of C4 needs 97.6 % of
+// the tiles per row at a 2^-40 loss bound)
+#pragma once
+
+#include "common.hpp"
+
+namespace abc {
+
+constexpr int kTile = 64;  // particles per tile (one per lane)
+
+size_t sort_pairs_temp_bytes(int64_t n);
+hipError_t sort_pairs(void* temp, size_t temp_bytes, const uint64_t* keys_in,
+                      uint64_t* keys_out, const int32_t* vals_in,
+                      int32_t* vals_out, int64_t n, int end_bit, hipStream_t st);
+
+__host__ __device__ inline int morton_bits(int d) {
+  const int b = 63 / d;
+  return b < 21 ? b : 21;
+}
+
+// Quantisation frame: per dimension the extent of (x - X[0]) over the
+// population as ordered fp64 keys, min in [q], max in [8 + q].
+template <int D>
+__global__ __launch_bounds__(256) void sp_extent_kernel(
+    const double* __restrict__ X, int64_t N,
+    unsigned long long* __restrict__ ext) {
+  __shared__ unsigned long long red[2 * D][4];
+  uint64_t mn[D], mx[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    mn[q] = ~0ull;
+    mx[q] = 0ull;
+  }
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < N;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const uint64_t k = f64_key(X[i * D + q] - X[q]);
+      mn[q] = k < mn[q] ? k : mn[q];
+      mx[q] = k > mx[q] ? k : mx[q];
+    }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t a = __shfl_xor(mn[q], o, 64), b = __shfl_xor(mx[q], o, 64);
+      mn[q] = a < mn[q] ? a : mn[q];
+      mx[q] = b > mx[q] ? b : mx[q];
+    }
+    if (lane == 0) {
+      red[q][wid] = mn[q];
+      red[D + q][wid] = mx[q];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * D) {
+    const int c = threadIdx.x;
+    unsigned long long v = red[c][0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+      v = c < D ? (red[c][w] < v ? red[c][w] : v) : (red[c][w] > v ? red[c][w] : v);
+    if (c < D)
+      atomicMin(ext + c, v);
+    else
+      atomicMax(ext + 8 + (c - D), v);
+  }
+}
+
+// Morton key of the points P[n][D] in the frame of X (clamped to the grid).
+template <int D>
+__global__ __launch_bounds__(256) void sp_key_kernel(
+    const double* __restrict__ P, int64_t n, const double* __restrict__ X,
+    const unsigned long long* __restrict__ ext, uint64_t* __restrict__ keys,
+    int32_t* __restrict__ vals) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  constexpr int B = 63 / D < 21 ? 63 / D : 21;
+  const double cells = static_cast<double>((1u << B) - 1);
+  uint64_t c[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    const double lo = key_f64(ext[q]), hi = key_f64(ext[8 + q]);
+    const double span = hi - lo;
+    double v = span > 0.0 ? (P[i * D + q] - X[q] - lo) * (cells / span) : 0.0;
+    v = v > 0.0 ? (v < cells ? v : cells) : 0.0;  // NaN -> 0
+    c[q] = static_cast<uint64_t>(v);
+  }
+  uint64_t key = 0;
+#pragma unroll
+  for (int b = B - 1; b >= 0; --b)
+#pragma unroll
+    for (int q = 0; q < D; ++q) key = (key << 1) | ((c[q] >> b) & 1u);
+  keys[i] = key;
+  vals[i] = static_cast<int32_t>(i);
+}
+
+// Order-preserving-within-block compaction of the sorted positions whose
+// original index lies in [rlo, rhi) (the rank's row share).  Blocks append
+// in arbitrary order; the passes' results do not depend on the row order.
+__global__ __launch_bounds__(256) void sp_rows_in_range_kernel(
+    const int32_t* __restrict__ perm, int64_t N, int64_t rlo, int64_t rhi,
+    int32_t* __restrict__ out, int* __restrict__ count) {
+  __shared__ int wcnt[4];
+  __shared__ int base;
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const bool in = s < N && perm[s] >= rlo && perm[s] < rhi;
+  const uint64_t m = __ballot(in);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) wcnt[wid] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    base = atomicAdd(count, wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3]);
+  __syncthreads();
+  int off = base;
+  for (int w = 0; w < wid; ++w) off += wcnt[w];
+  if (in) out[off + __popcll(m & ((1ull << lane) - 1ull))] = static_cast<int32_t>(s);
+}
+
+// Squared distance lower bound of a point to a box with the fp32 operations
+// of the passes (gap per dimension, fma chain): monotone in the gap.
+template <int D>
+__device__ inline float box_dist2(const float (&x)[D], const float* __restrict__ lo,
+                                  const float* __restrict__ hi) {
+  float s = 0.0f;
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    const float g = fmaxf(fmaxf(lo[q] - x[q], x[q] - hi[q]), 0.0f);
+    s = __builtin_fmaf(g, g, s);
+  }
+  return s;
+}
+
+}  // namespace abc

@@ -653,6 +653,58 @@ def test_local_logpdf_f32_vs_exact(K, d, offset):
     np.testing.assert_allclose(np.exp(got - exact), 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("d", [3, 6])
+def test_local_logpdf_f32_rows_independent(K, d):
+    """The fp32 pass cuts the particle range into chunks that depend on N
+    only: a row's bits do not depend on which rows share its call (a subset
+    in another order, a single row, duplicated rows), as the row-sharded
+    generation needs."""
+    rng = np.random.default_rng(90 + d)
+    n, k = 20_000, 30
+    X = rng.normal(size=(n, d))
+    w = rng.uniform(0.1, 1.0, size=n)
+    nbr, _ = K.knn(dev(X), k)
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    pts = np.concatenate([X[rng.integers(0, n, 3000)] +
+                          0.2 * rng.normal(size=(3000, d)),
+                          rng.normal(size=(100, d)) * 4])
+    full = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, "f32"))
+    sub = rng.permutation(len(pts))[:777]
+    part = host(K.local_logpdf(dev(pts[sub]), dev(X), dev(w), invs, dets, "f32"))
+    np.testing.assert_array_equal(part, full[sub])
+    one = host(K.local_logpdf(dev(pts[sub[:1]]), dev(X), dev(w), invs, dets, "f32"))
+    np.testing.assert_array_equal(one, full[sub[:1]])
+    dup = np.repeat(pts[:50], 3, axis=0)
+    got = host(K.local_logpdf(dev(dup), dev(X), dev(w), invs, dets, "f32"))
+    np.testing.assert_array_equal(got, np.repeat(full[:50], 3))
+    exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
+    np.testing.assert_allclose(np.exp(full - exact), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("d", [2, 6])
+def test_knn_rows_tiled_equal_full(K, d):
+    """Row ranges of the tiled kNN (the rank shares of the sharded fit) give
+    the rows of the full call, and both equal an fp64 brute force on a
+    sample of rows."""
+    rng = np.random.default_rng(70 + d)
+    n, k = 30_000, 50
+    X = rng.normal(size=(n, d)) * np.linspace(0.5, 2.0, d)
+    nbr, d2 = K.knn(dev(X), k)
+    nbr, d2 = host(nbr), host(d2)
+    for lo, m in [(0, 1), (12_345, 4321), (n - 77, 77)]:
+        nb, dd = K.knn_rows(dev(X), k, lo, m)
+        np.testing.assert_array_equal(host(nb), nbr[lo:lo + m])
+        np.testing.assert_array_equal(host(dd), d2[lo:lo + m])
+    rows = rng.choice(n, 200, replace=False)
+    diff = X[None, :, :] - X[rows, None, :]
+    D2 = np.zeros((len(rows), n))
+    for q in range(d):
+        D2 = D2 + diff[:, :, q] * diff[:, :, q]
+    D2[np.arange(len(rows)), rows] = np.inf
+    order = np.lexsort((np.broadcast_to(np.arange(n), D2.shape), D2), axis=1)
+    np.testing.assert_array_equal(nbr[rows], order[:, :k])
+
+
 @pytest.mark.parametrize("d,spread", [(6, 1e3), (3, 1e4), (8, 3e3)])
 def test_local_logpdf_f32_wide_population(K, d, spread):
     """A population whose extent is >= 1e3 local bandwidths (small k, far

@@ -24,21 +24,24 @@ def timed(fn, reps=3):
     return min(ts)
 
 
-def main(N=200_000, d=6, k=50):
+def main(N=200_000, d=6, k=50, scale=1.0):
     g = torch.Generator(device="cuda").manual_seed(3)
-    X = torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
+    X = scale * torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
     w = torch.rand(N, dtype=torch.float64, device="cuda", generator=g)
     w /= w.sum()
     nbr, _ = K.knn(X, k)
     covs, invs, dets = K.local_cov(X, w, nbr)
-    pts = X + 0.1
+    # evaluation points as the C4 generation draws them: the production
+    # LocalTransition proposal (X[idx] + Cholesky(C_idx) z, Philox)
+    cdf = K.resample_cdf(w)
+    pts, _, _ = K.propose_local(X, cdf, covs, 11, 0, 0, N)
     out = {"knn_ms": timed(lambda: K.knn(X, k)),
            "local_cov_ms": timed(lambda: K.local_cov(X, w, nbr))}
     for prec in ("f32", "f64"):
         out[f"pdf_{prec}_ms"] = timed(
             lambda: K.local_logpdf(pts, X, w, invs, dets, precision=prec))
-    a = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f32")
-    b = K.local_logpdf(pts[:4096], X, w, invs, dets, precision="f64")
+    a = K.local_logpdf(pts, X, w, invs, dets, precision="f32")
+    b = K.local_logpdf(pts, X, w, invs, dets, precision="f64")
     out["max_rel_f32_vs_f64"] = float(torch.expm1(a - b).abs().max())
     print({k_: (f"{v:.3e}" if k_.startswith("max_rel") else round(v, 4))
            if isinstance(v, float) else v for k_, v in out.items()}, flush=True)
@@ -46,3 +49,5 @@ def main(N=200_000, d=6, k=50):
 
 if __name__ == "__main__":
     main()
+    main(N=200_000, d=4, k=50)
+    main(N=50_000, d=8, k=50)

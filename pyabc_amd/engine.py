@@ -171,7 +171,8 @@ def pnorm_host(x, x0, fw, p):
                         for a, b, f in zip(x, x0, fw)), 1 / p)
 
 
-def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps):
+def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps,
+                        band=None):
     """Host re-decision of the guard band (acceptor.py:241-242).
 
     The kernel squares with ``t*t`` and roots with ``sqrt``; the reference
@@ -181,11 +182,16 @@ def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps):
     the flagged band around eps could be decided differently.  Those
     columns -- normally none -- are copied to the host, re-evaluated with
     :func:`pnorm_host`, and their distance and accept bit overwritten, so
-    the accept mask equals the reference's.  Returns the band's size."""
+    the accept mask equals the reference's.  ``band`` = (positions, count)
+    of the flagged columns when the caller has compacted them already.
+    Returns the band's size."""
     if guard is None or B == 0:
         return 0
-    gpos, gcount = K.compact(guard[:B])
-    n = int(gcount.item())
+    if band is None:
+        gpos, gcount = K.compact(guard[:B])
+        n = int(gcount.item())
+    else:
+        gpos, n = band
     if n == 0:
         return 0
     sel = gpos[:n]
@@ -198,6 +204,21 @@ def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps):
     return n
 
 
+def decide(acceptance, stats, nv, seed, stream, eval_off):
+    """One round's acceptance with ONE host read: distances / flags, the
+    order-preserving positions of the accepted columns, and the accepted
+    and guard-band counts as host ints -> (d, acc, guard, accw, apos,
+    n_acc, n_guard)."""
+    if hasattr(acceptance, "decide"):
+        return acceptance.decide(stats, nv, seed, stream, eval_off)
+    d, acc, guard, accw = acceptance(stats, nv, seed, stream, eval_off)
+    apos, acount = K.compact(acc)
+    g = guard[:nv].sum(dtype=torch.int64).view(1) if guard is not None \
+        else torch.zeros(1, dtype=torch.int64, device=acount.device)
+    n_acc, n_guard = torch.cat([acount.view(1), g]).cpu().tolist()
+    return d, acc, guard, accw, apos, int(n_acc), int(n_guard)
+
+
 class PNormAcceptance:
     """Uniform acceptance d <= eps of a p-norm distance
     (distance/distance.py:76-102, acceptor/acceptor.py:235-244), with the
@@ -208,15 +229,38 @@ class PNormAcceptance:
         self._host = None
         self.n_redecided = 0
 
+    def _host_params(self):
+        if self._host is None:
+            self._host = (self.x0.cpu().tolist(), self.fw.cpu().tolist())
+        return self._host
+
     def __call__(self, stats, nv, seed, stream, eval_off):
         d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
                                          self.eps, B=nv)
-        if self._host is None:
-            self._host = (self.x0.cpu().tolist(), self.fw.cpu().tolist())
+        x0h, fwh = self._host_params()
         self.n_redecided += redecide_guard_band(
-            stats, nv, d, acc, guard, self._host[0], self._host[1], self.p,
-            self.eps)
+            stats, nv, d, acc, guard, x0h, fwh, self.p, self.eps)
         return d, acc, guard, None
+
+    def decide(self, stats, nv, seed, stream, eval_off):
+        """:func:`decide` for the p-norm: the accepted and the guard-band
+        columns are compacted together and their counts read in one host
+        sync; the (rare) band is then re-decided and the accepted columns
+        compacted again."""
+        x0h, fwh = self._host_params()
+        d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
+                                         self.eps, B=nv)
+        gpos, gcount = K.compact(guard[:nv])
+        apos, acount = K.compact(acc)
+        n_acc, n_guard = torch.cat([acount.view(1), gcount.view(1)]).cpu(
+        ).tolist()
+        if n_guard:
+            self.n_redecided += redecide_guard_band(
+                stats, nv, d, acc, guard, x0h, fwh, self.p, self.eps,
+                band=(gpos, int(n_guard)))
+            apos, acount = K.compact(acc)
+            n_acc = acount.item()
+        return d, acc, guard, None, apos, int(n_acc), int(n_guard)
 
 
 class StochasticAcceptance:
@@ -398,17 +442,18 @@ class GenerationEngine:
                 apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
                 nas = list(nvs)
             elif nv:
-                d, acc, guard, accw = acceptance(
-                    stats, nv, self.seed, self._stream(t, stream_base + 4),
-                    my_eval)
-                apos, acount = K.compact(acc)
-                nas = comm.all_gather_ints(acount)                  # sync 2
+                d, acc, guard, accw, apos, acount, gcount = decide(
+                    acceptance, stats, nv, self.seed,
+                    self._stream(t, stream_base + 4), my_eval)      # sync 2
+                nas = comm.all_gather_ints(acount)
             else:
                 d = guard = apos = None
                 nas = comm.all_gather_ints(0)
+            if acceptance is None or not nv:
+                gcount = 0
             rounds.append(dict(theta=theta, stats=stats, d=d, apos=apos,
                                guard=guard, accw=accw, acc=acc, nvs=nvs,
-                               nas=nas, acc0=n_acc))
+                               nas=nas, acc0=n_acc, gcount=gcount))
             raw_off += R * B
             eval_off += sum(nvs)
             n_acc += sum(nas)
@@ -460,7 +505,8 @@ class GenerationEngine:
                     ra_loc.append(rd["acc"][:last].to(F64) if rd["acc"]
                                   is not None else torch.ones(
                                       last, dtype=F64, device=self.dev))
-                n_guard += int(rd["guard"][:last].sum().item())
+                if rd["gcount"]:     # no flag in the round: no host read
+                    n_guard += int(rd["guard"][:last].sum().item())
         n_eval, n_guard = comm.all_reduce_ints([n_eval_loc, n_guard])
         if n_eval > cap:
             # the n-th acceptance lies past the evaluation cap: the reference
@@ -487,7 +533,7 @@ class GenerationEngine:
             rec_theta = self._gather(rth_loc, (self.d,), last_counts)
             rec_d = self._gather(rd_loc, (), last_counts)
             rec_acc = self._gather(ra_loc, (), last_counts)
-        torch.cuda.synchronize()
+        # host time (the device work of the selection overlaps the KDE pass)
         tm["select"] = time.perf_counter() - t0 - tm["propose_sim_dist"]
         t1 = time.perf_counter()
         if fit is None:
@@ -530,6 +576,10 @@ class GenerationEngine:
         """Stat-major [S, cols] version of :meth:`_gather` (contiguous)."""
         S = self.model.n_stats
         if not self.comm.active:
+            if len(pieces) == 1:
+                # one round: the column slice itself (row stride = the
+                # round's batch; the kernels take (pointer, ld), no copy)
+                return pieces[0]
             return torch.cat(pieces, 1) if pieces else torch.empty(
                 (S, 0), dtype=F64, device=self.dev)
         rows = self._gather([x.t() for x in pieces], (S,), counts)

@@ -49,6 +49,20 @@ def _contig(t, dtype):
     return t.contiguous()
 
 
+def _stat_major(stats_T):
+    """(tensor, ld, n) of a stat-major [S, n] fp64 matrix for the kernels'
+    (pointer, ld) convention: a column slice of a larger matrix (rows
+    contiguous, row stride ld >= n) is passed as is -- no copy -- and
+    anything else is made contiguous."""
+    if stats_T.dtype != F64:
+        raise TypeError(f"expected {F64}, got {stats_T.dtype}")
+    S, n = stats_T.shape
+    if S > 1 and stats_T.stride(1) == 1 and stats_T.stride(0) >= n:
+        return stats_T, stats_T.stride(0), n
+    t = stats_T.contiguous()
+    return t, max(n, 1), n
+
+
 # ---------------------------------------------------------------------------
 # RNG / proposals (a2)
 # ---------------------------------------------------------------------------
@@ -329,8 +343,9 @@ def scale_inplace(x, divisor_dev):
 # ---------------------------------------------------------------------------
 def pnorm_distance(stats_T, x0, fw, p, eps=math.inf, B=None, with_accept=True,
                    d_out=None, acc_out=None, guard_out=None):
-    S, ld = stats_T.shape
-    B = ld if B is None else B
+    S = stats_T.shape[0]
+    stats_T, ld, n = _stat_major(stats_T)
+    B = n if B is None else B
     d = torch.empty(B, dtype=F64, device=_dev()) if d_out is None else d_out
     acc = guard = None
     if with_accept:
@@ -344,8 +359,9 @@ def pnorm_distance(stats_T, x0, fw, p, eps=math.inf, B=None, with_accept=True,
 
 
 def column_median_mad(data_T, n=None, mad=True):
-    S, ld = data_T.shape
-    n = ld if n is None else n
+    S = data_T.shape[0]
+    data_T, ld, n0 = _stat_major(data_T)
+    n = n0 if n is None else n
     med = torch.empty(S, dtype=F64, device=_dev())
     madv = torch.empty(S, dtype=F64, device=_dev()) if mad else None
     wsb = nat.lib().abc_column_select_workspace_bytes(S)
@@ -356,8 +372,9 @@ def column_median_mad(data_T, n=None, mad=True):
 
 
 def column_std(data_T, n=None):
-    S, ld = data_T.shape
-    n = ld if n is None else n
+    S = data_T.shape[0]
+    data_T, ld, n0 = _stat_major(data_T)
+    n = n0 if n is None else n
     mean = torch.empty(S, dtype=F64, device=_dev())
     std = torch.empty(S, dtype=F64, device=_dev())
     wsb = nat.lib().abc_column_std_workspace_bytes(n, S)
@@ -546,8 +563,9 @@ def stochastic_kernel(stats_T, x0, prm, kind, c, B=None, pdf_norm=None,
     """Log-densities of an independent normal / Laplace kernel per column of
     stat-major ``stats_T`` ([S, ld]); with ``pdf_norm`` also the fused
     stochastic acceptance.  Returns (pd, accept, accw, guard)."""
-    S, ld = stats_T.shape
-    B = ld if B is None else B
+    S = stats_T.shape[0]
+    stats_T, ld, n = _stat_major(stats_T)
+    B = n if B is None else B
     pd = torch.empty(B, dtype=F64, device=_dev())
     acc = accw = guard = None
     if pdf_norm is not None:

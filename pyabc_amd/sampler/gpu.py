@@ -142,6 +142,7 @@ class GPUBatchSampler(Sampler):
         self.comm = comm
         self._engines = {}
         self.last_timers = {}
+        self.timer_log = []     # per-call engine timers (tools/bench_configs.py)
         self.fallback_reason = None
 
     def _engine(self, spec):
@@ -220,6 +221,7 @@ class GPUBatchSampler(Sampler):
             rec = DeviceStats(res.rec_stats_T, keys)
         self.nr_evaluations_ = int(res.n_eval)
         self.last_timers = dict(eng.timers)
+        self.timer_log.append(self.last_timers)
         pop = ColumnarPopulation(res.theta, res.w, res.d, names,
                                  res.stats_T, keys)
         recp = None

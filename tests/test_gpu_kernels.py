@@ -348,6 +348,53 @@ def _sqrt_pow_disagree(rng, n):
     raise AssertionError("no sqrt/pow disagreement found")
 
 
+def test_stat_major_column_slices(K):
+    """Column slices of a stat-major matrix (the recorded statistics of one
+    round, first_m_sum_stats) go to the kernels as (pointer, row stride):
+    median / MAD, std, p-norm and stochastic-kernel results equal those of
+    the contiguous copy, bit for bit."""
+    rng = np.random.default_rng(5)
+    S, n, m = 7, 5000, 3111
+    full = dev(rng.normal(size=(S, n)) * rng.uniform(0.1, 10, size=(S, 1)))
+    view = full[:, :m]
+    assert not view.is_contiguous()
+    copy = view.contiguous()
+    for f in (K.column_median_mad, K.column_std):
+        for a, b in zip(f(view), f(copy)):
+            np.testing.assert_array_equal(host(a), host(b))
+    x0, fw = dev(rng.normal(size=S)), dev(rng.uniform(0.5, 2, size=S))
+    for a, b in zip(K.pnorm_distance(view, x0, fw, 2, 3.0),
+                    K.pnorm_distance(copy, x0, fw, 2, 3.0)):
+        np.testing.assert_array_equal(host(a), host(b))
+    prm = dev(rng.uniform(0.5, 2, size=S))
+    a = K.stochastic_kernel(view, x0, prm, K.KERNEL_NORMAL, 0.0)[0]
+    b = K.stochastic_kernel(copy, x0, prm, K.KERNEL_NORMAL, 0.0)[0]
+    np.testing.assert_array_equal(host(a), host(b))
+    one = full[:1, :m]                     # S = 1: any row stride
+    np.testing.assert_array_equal(host(K.column_median_mad(one)[0]),
+                                  np.median(host(copy)[:1], axis=1))
+
+
+def test_pnorm_decide_one_read(K):
+    """PNormAcceptance.decide (the engine's one-sync round) gives the
+    distances, accept mask, compacted positions and counts of the plain
+    call followed by a compaction, with the guard band re-decided."""
+    from pyabc_amd.engine import PNormAcceptance
+    rng = np.random.default_rng(8)
+    S, B = 20, 40000
+    stats = dev(rng.normal(size=(S, B)))
+    x0, fw = dev(np.zeros(S)), dev(np.ones(S))
+    eps = float(np.median(np.sqrt((host(stats) ** 2).sum(0))))
+    a = PNormAcceptance(x0, fw, 2, eps)
+    d1, acc1, g1, _ = a(stats, B, 0, 0, 0)
+    pos1, c1 = K.compact(acc1)
+    d2, acc2, g2, _, pos2, n2, ng2 = a.decide(stats, B, 0, 0, 0)
+    np.testing.assert_array_equal(host(d1), host(d2))
+    np.testing.assert_array_equal(host(acc1), host(acc2))
+    assert n2 == int(host(c1)[0]) and ng2 == int(host(g2).sum())
+    np.testing.assert_array_equal(host(pos1)[:n2], host(pos2)[:n2])
+
+
 @pytest.mark.parametrize("p", [2, 3])
 def test_guard_band_redecided_on_host(K, p):
     """A distance within 1 ulp of eps where the kernel's sqrt (or device

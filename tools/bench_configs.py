@@ -55,9 +55,12 @@ def run(name, abc, x0, names, theta_true=None, db=None, **run_kw):
     df, w = h.distribution_numpy(0, h.max_t)
     w = w / w.sum()
     mean = (df[names].values * w[:, None]).sum(0)
+    tl = getattr(abc.sampler, "timer_log", [])
+    tl = tl[-len(log):] if len(tl) >= len(log) else [{}] * len(log)
     gens = [dict(t=e["t"], eps=float(e["eps"]), n_sim=int(e["n_sim"]),
-                 sample_s=float(e["sample_seconds"]), batch=e["batch"])
-            for e in log]
+                 sample_s=float(e["sample_seconds"]), batch=e["batch"],
+                 timers={k: round(v * 1e3, 4) for k, v in tm.items()})
+            for e, tm in zip(log, tl)]
     n_pop = int(len(w))
     rates = [n_pop / g["sample_s"] for g in gens if g["t"] >= 1]
     out = dict(config=name, N=n_pop, generations=len(gens), wall_s=wall,

@@ -349,6 +349,21 @@ int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
                                 double sigma, uint64_t seed, uint64_t sid,
                                 uint64_t offset, double* out_T, int64_t ld,
                                 hipStream_t stream);
+/* Fused simulation + p-norm distance + uniform acceptance for rounds whose
+ * statistics are not kept: per proposal the column of
+ * abc_sim_linear_gaussian_f64 (same arithmetic, same Philox noise) goes
+ * straight into the abc_pnorm_distance_f64 chain without being stored;
+ * d_out / accept / guard are bit-identical to the two calls.
+ * Replaces model(par) + distance(x, x_0) + acceptor  smc.py:650-700,
+ *                                 distance/distance.py:76-102,
+ *                                 acceptor/acceptor.py:235-244 */
+int abc_sim_linear_gaussian_pnorm_f64(const double* theta, int64_t B, int d,
+                                      const double* A, const double* c, int S,
+                                      double sigma, uint64_t seed, uint64_t sid,
+                                      uint64_t offset, const double* x0,
+                                      const double* fw, double p, double eps,
+                                      double* d_out, uint8_t* accept,
+                                      uint8_t* guard, hipStream_t stream);
 int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
                               uint64_t seed, uint64_t sid, uint64_t offset,
                               double* out, hipStream_t stream);

@@ -65,6 +65,14 @@ class LinearGaussianModel(BatchModel):
         return K.sim_linear_gaussian(theta, A, c, self.sigma, seed, sid,
                                      offset)
 
+    def simulate_distance(self, theta, seed, sid, offset, x0, fw, p, eps):
+        """simulate + p-norm distance + d <= eps in one pass, statistics not
+        stored (their rows in the model's key order): (d, accept, guard),
+        bit-identical to simulate() followed by the distance kernel."""
+        A, c = self._tensors()
+        return K.sim_linear_gaussian_pnorm(theta, A, c, self.sigma, seed, sid,
+                                           offset, x0, fw, p, eps)
+
     def simulate_host(self, theta, rng):
         """numpy reference of the same model (for CPU baselines)."""
         theta = np.atleast_2d(theta)

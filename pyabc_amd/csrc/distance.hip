@@ -94,6 +94,65 @@ __global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
   }
 }
 
+// Fused simulation + distance for rounds whose statistics nobody keeps
+// (no recorded statistics, no stored population statistics): the column
+// y[., b] of sim_linear_gaussian_kernel is formed stat by stat in registers
+// -- the same fma sequence and the same Philox / Box-Muller noise -- and fed
+// straight into pnorm_kernel's key-ordered chain, so distances, accept and
+// guard flags are bit-identical to the two-kernel path while the 8 S bytes
+// per evaluation are neither written nor read back (test_sim_pnorm_fused).
+template <int PMODE>
+__global__ __launch_bounds__(256) void sim_lg_pnorm_kernel(
+    const double* __restrict__ theta, int64_t B, int d,
+    const double* __restrict__ A, const double* __restrict__ c, int S,
+    double sigma, uint64_t seed, uint64_t sid, uint64_t offset,
+    const double* __restrict__ x0, const double* __restrict__ fw, double p,
+    double eps, double* __restrict__ d_out, uint8_t* __restrict__ accept,
+    uint8_t* __restrict__ guard) {
+#pragma clang fp contract(off)  // as pnorm_kernel; the fmas are explicit
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double th[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) th[k] = k < d ? theta[b * d + k] : 0.0;
+  const uint64_t base = (offset + static_cast<uint64_t>(b)) * static_cast<uint64_t>(S);
+  float z4[4] = {0.f, 0.f, 0.f, 0.f};
+  uint64_t have = ~0ull;
+  double acc2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    double acc = c ? c[s] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < d) acc = fma(A[s * d + k], th[k], acc);
+    const uint64_t zi = base + s;
+    if ((zi >> 2) != have) {
+      box_muller4_f32(philox_block(seed, sid, zi >> 2), z4);
+      have = zi >> 2;
+    }
+    const double y = fma(sigma, static_cast<double>(z4[zi & 3]), acc);
+    const double t = fabs(fw[s] * (y - x0[s]));
+    if (PMODE == 1)
+      acc2 += t;
+    else if (PMODE == 2)
+      acc2 += t * t;
+    else if (PMODE == 3)
+      acc2 = fmax(acc2, t);
+    else
+      acc2 += pow(t, p);
+  }
+  double dist;
+  if (PMODE == 1 || PMODE == 3)
+    dist = acc2;
+  else if (PMODE == 2)
+    dist = sqrt(acc2);
+  else
+    dist = pow(acc2, 1.0 / p);
+  d_out[b] = dist;
+  if (accept) accept[b] = dist <= eps ? 1 : 0;
+  if (guard)
+    guard[b] = fabs(dist - eps) <= (PMODE == 0 ? 16.0 : 4.0) * ulp_of(eps) ? 1 : 0;
+}
+
 // quickstart model (doc/examples/parameter_inference.ipynb cell 2):
 // y = mean + 0.5 * N(0,1), one statistic
 __global__ __launch_bounds__(256) void sim_gaussian_mean_kernel(
@@ -151,6 +210,37 @@ int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
                      dim3(256), 0, st, theta, B, d, A, c, S, sigma, seed, sid,
                      offset, out_T, ld);
   ABC_LAUNCH_CHECK("sim_linear_gaussian_kernel");
+  return kOk;
+}
+
+int abc_sim_linear_gaussian_pnorm_f64(const double* theta, int64_t B, int d,
+                                      const double* A, const double* c, int S,
+                                      double sigma, uint64_t seed, uint64_t sid,
+                                      uint64_t offset, const double* x0,
+                                      const double* fw, double p, double eps,
+                                      double* d_out, uint8_t* accept,
+                                      uint8_t* guard, hipStream_t st) {
+  ABC_REQUIRE(d >= 1 && d <= 32 && S >= 1 && B >= 0,
+              "sim_linear_gaussian_pnorm: bad sizes (d <= 32)");
+  ABC_REQUIRE(p >= 1.0, "sim_linear_gaussian_pnorm: It must be p >= 1");
+  if (B == 0) return kOk;
+  ABC_REQUIRE(theta && A && x0 && fw && d_out,
+              "sim_linear_gaussian_pnorm: null pointer");
+  const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+#define L(PM)                                                                    \
+  hipLaunchKernelGGL(sim_lg_pnorm_kernel<PM>, dim3(g), dim3(256), 0, st, theta, B, \
+                     d, A, c, S, sigma, seed, sid, offset, x0, fw, p, eps, d_out, \
+                     accept, guard)
+  if (std::isinf(p))
+    L(3);
+  else if (p == 1.0)
+    L(1);
+  else if (p == 2.0)
+    L(2);
+  else
+    L(0);
+#undef L
+  ABC_LAUNCH_CHECK("sim_lg_pnorm_kernel");
   return kOk;
 }
 

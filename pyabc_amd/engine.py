@@ -242,19 +242,27 @@ class PNormAcceptance:
             stats, nv, d, acc, guard, x0h, fwh, self.p, self.eps)
         return d, acc, guard, None
 
-    def decide(self, stats, nv, seed, stream, eval_off):
+    def decide(self, stats, nv, seed, stream, eval_off, fused=None):
         """:func:`decide` for the p-norm: the accepted and the guard-band
         columns are compacted together and their counts read in one host
         sync; the (rare) band is then re-decided and the accepted columns
-        compacted again."""
+        compacted again.  ``fused`` = (d, acc, guard, simulate) when the
+        round ran the fused simulation + distance: ``stats`` is None and
+        the band's statistics come from ``simulate()`` (same Philox noise,
+        so the same columns)."""
         x0h, fwh = self._host_params()
-        d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
-                                         self.eps, B=nv)
+        if fused is None:
+            d, acc, guard = K.pnorm_distance(stats, self.x0, self.fw, self.p,
+                                             self.eps, B=nv)
+        else:
+            d, acc, guard, simulate = fused
         gpos, gcount = K.compact(guard[:nv])
         apos, acount = K.compact(acc)
         n_acc, n_guard = torch.cat([acount.view(1), gcount.view(1)]).cpu(
         ).tolist()
         if n_guard:
+            if stats is None:
+                stats = simulate()
             self.n_redecided += redecide_guard_band(
                 stats, nv, d, acc, guard, x0h, fwh, self.p, self.eps,
                 band=(gpos, int(n_guard)))
@@ -310,6 +318,9 @@ class GenerationEngine:
         self.max_batch = max_batch
         self.kde_precision = kde_precision
         self.record_stats = record_stats
+        # rounds whose statistics are not kept run the model's fused
+        # simulate_distance when it has one (bit-identical distances)
+        self.fuse_sim_distance = True
         self.acc_rate_est = 0.5
         self.valid_rate_est = 1.0
         self.timers = {}
@@ -427,10 +438,15 @@ class GenerationEngine:
                 theta = K.gather_rows(theta_all, vpos, nv) if nv else None
             nv = nvs[r]
             my_eval = eval_off + sum(nvs[:r])
-            if nv:
-                stats = self.model.simulate(
-                    theta, self.seed, self._stream(t, stream_base + 1),
-                    my_eval)
+            sim_sid = self._stream(t, stream_base + 1)
+            # statistics nobody keeps: simulation and distance in one pass
+            fuse = (nv and not keep_stats and not record
+                    and self.fuse_sim_distance
+                    and isinstance(acceptance, PNormAcceptance)
+                    and hasattr(self.model, "simulate_distance"))
+            if nv and not fuse:
+                stats = self.model.simulate(theta, self.seed, sim_sid,
+                                            my_eval)
             else:
                 stats = None
             accw = acc = None
@@ -441,6 +457,16 @@ class GenerationEngine:
                 guard = torch.zeros(nv, dtype=torch.uint8, device=self.dev)
                 apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
                 nas = list(nvs)
+            elif fuse:
+                a = acceptance
+                fd = self.model.simulate_distance(
+                    theta, self.seed, sim_sid, my_eval, a.x0, a.fw, a.p, a.eps)
+                th_, me_ = theta, my_eval
+                d, acc, guard, accw, apos, acount, gcount = a.decide(
+                    None, nv, self.seed, self._stream(t, stream_base + 4),
+                    my_eval, fused=fd + (lambda: self.model.simulate(
+                        th_, self.seed, sim_sid, me_),))            # sync 2
+                nas = comm.all_gather_ints(acount)
             elif nv:
                 d, acc, guard, accw, apos, acount, gcount = decide(
                     acceptance, stats, nv, self.seed,

@@ -541,6 +541,24 @@ def sim_linear_gaussian(theta, A, c, sigma, seed, sid, offset, out_T=None,
     return out_T
 
 
+def sim_linear_gaussian_pnorm(theta, A, c, sigma, seed, sid, offset, x0, fw,
+                              p, eps=math.inf, B=None):
+    """Fused simulation + p-norm distance + acceptance (no statistics
+    stored): (d, accept, guard), bit-identical to sim_linear_gaussian
+    followed by pnorm_distance."""
+    theta = _contig(theta, F64)
+    B = theta.shape[0] if B is None else B
+    S, d = A.shape
+    dist = torch.empty(B, dtype=F64, device=_dev())
+    acc = torch.empty(B, dtype=torch.uint8, device=_dev())
+    guard = torch.empty(B, dtype=torch.uint8, device=_dev())
+    call("abc_sim_linear_gaussian_pnorm_f64", ptr(theta), B, d, ptr(A), ptr(c),
+         S, float(sigma), seed, sid, offset, ptr(_contig(x0, F64)),
+         ptr(_contig(fw, F64)), float(p), float(eps), ptr(dist), ptr(acc),
+         ptr(guard), nat.stream())
+    return dist, acc, guard
+
+
 def sim_gaussian_mean(theta, sigma, seed, sid, offset, out=None, B=None):
     B = theta.shape[0] if B is None else B
     if out is None:

@@ -375,6 +375,56 @@ def test_stat_major_column_slices(K):
                                   np.median(host(copy)[:1], axis=1))
 
 
+@pytest.mark.parametrize("p", [1, 2, 3, math.inf])
+def test_sim_pnorm_fused(K, p):
+    """The fused simulation + distance kernel (no statistics stored) gives
+    the distances, accept and guard flags of abc_sim_linear_gaussian_f64
+    followed by abc_pnorm_distance_f64, bit for bit, with and without the
+    constant term c."""
+    rng = np.random.default_rng(31)
+    B, d, S = 20000, 8, 100
+    theta = dev(rng.uniform(-2, 2, size=(B, d)))
+    A = dev(rng.normal(size=(S, d)))
+    x0, fw = dev(rng.normal(size=S)), dev(rng.uniform(0.5, 2, size=S))
+    for c in (None, dev(rng.normal(size=S))):
+        stats = K.sim_linear_gaussian(theta, A, c, 0.5, 7, 13, 12345)
+        d1, a1, g1 = K.pnorm_distance(stats, x0, fw, p, 30.0)
+        eps = float(np.median(host(d1)))
+        d1, a1, g1 = K.pnorm_distance(stats, x0, fw, p, eps)
+        d2, a2, g2 = K.sim_linear_gaussian_pnorm(theta, A, c, 0.5, 7, 13, 12345,
+                                                 x0, fw, p, eps)
+        np.testing.assert_array_equal(host(d1), host(d2))
+        np.testing.assert_array_equal(host(a1), host(a2))
+        np.testing.assert_array_equal(host(g1), host(g2))
+
+
+def test_engine_fused_round_equals_unfused(K):
+    """A generation whose statistics are not kept (the bench's) runs the
+    fused simulate_distance; population, distances, weights, log-densities
+    and evaluation count equal the unfused engine's bit for bit."""
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.engine import DeviceMVNFit, GenerationEngine
+    model = LinearGaussianModel.benchmark(4, 30)
+    x0 = dev(model._x0)
+    fw = dev(np.ones(30))
+    out = []
+    for fuse in (False, True):
+        eng = GenerationEngine(model, np.full(4, -5.0), np.full(4, 10.0),
+                               seed=99)
+        eng.fuse_sim_distance = fuse
+        r0 = eng.sample_prior(0, 8000)
+        d0, _, _ = K.pnorm_distance(r0.stats_T, x0, fw, 2.0)
+        w0 = torch.full((8000,), 1 / 8000, dtype=torch.float64, device="cuda")
+        eps = float(np.quantile(host(d0), 0.3))
+        res = eng.sample_generation(1, 8000, DeviceMVNFit(r0.theta, w0), x0, fw,
+                                    eps)
+        out.append(res)
+    a, b = out
+    for f in ("theta", "d", "w", "logpd"):
+        np.testing.assert_array_equal(host(getattr(a, f)), host(getattr(b, f)))
+    assert a.n_eval == b.n_eval
+
+
 def test_pnorm_decide_one_read(K):
     """PNormAcceptance.decide (the engine's one-sync round) gives the
     distances, accept mask, compacted positions and counts of the plain
@@ -674,6 +724,29 @@ def test_column_median_mad_skewed(K, n):
     np.testing.assert_array_equal(host(med), np.median(data, axis=0))
     mad_ref = np.array([np.median(np.abs(data[:, k] - np.median(data[:, k])))
                         for k in range(S)])
+    np.testing.assert_array_equal(host(mad), mad_ref)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 16384, 16385, 300_001, 2_000_000])
+def test_column_median_mad_sampled_splitters(K, n):
+    """The sampled-splitter select (one read per order statistic) and its
+    radix fallback on column orders and value sets that defeat a strided
+    sample: sorted, reversed, sawtooth, constant, three values, a spike of
+    ties at the median, and plain normal data -- bit-exact np.median / MAD
+    for odd and even n."""
+    rng = np.random.default_rng(n)
+    cols = [np.sort(rng.normal(size=n)),
+            np.sort(rng.normal(size=n))[::-1],
+            np.tile(np.arange(97.0), n // 97 + 1)[:n] + 0.5 * (np.arange(n) % 2),
+            np.full(n, 3.25),
+            rng.integers(0, 3, size=n).astype(float),
+            np.where(rng.uniform(size=n) < 0.3, 0.0, rng.normal(size=n)),
+            rng.normal(size=n) * 1e-3 + 7.0]
+    data = np.stack(cols, axis=1)
+    med, mad = K.column_median_mad(dev(data.T))
+    want = np.median(data, axis=0)
+    np.testing.assert_array_equal(host(med), want)
+    mad_ref = np.median(np.abs(data - want[None, :]), axis=0)
     np.testing.assert_array_equal(host(mad), mad_ref)
 
 

@@ -250,7 +250,10 @@ int abc_column_std_ws_f64(const double* data_T, int64_t ld, int64_t n, int S,
 /* ---------------- (a7) weighted-quantile epsilon -------------------------
  * Replaces weighted_quantile                        weighted_statistics.py:26-43
  * used by QuantileEpsilon._update                   epsilon/epsilon.py:202-228
- * w may be NULL (uniform weights).  out4 = [eps, p_k, cs_{k-1}, w_k]. */
+ * w may be NULL (uniform weights).  out4 = [eps, p_k, cs_{k-1}, w_k].
+ * Tied points form one block of knots at the same p: alpha between the
+ * block's first and last knot gives p exactly; the block's end knots take
+ * its smallest weight (numpy's unstable argsort leaves their order open). */
 size_t abc_wquantile_workspace_bytes(void);
 int abc_wquantile_f64(const double* d, const double* w, int64_t n,
                       double alpha, double* out4, void* ws, size_t ws_bytes,
@@ -258,7 +261,7 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n,
 /* The same select as exchangeable steps, for a population sharded over
  * ranks ("the multi-GPU variant exposes its histogram pass so
  * RCCL can all-reduce between passes"; 8(e) epsilon).  Each rank runs the
- * step sequence 0, 1, 2, 3, 10, 20, 11, 21, ..., 17, 27, 30, 31, 32 on its
+ * step sequence 0, 1, 2, 3, 10, 20, 11, 21, ..., 17, 27, 30, 31, 33, 32 on its
  * rows (n_local of n_total); after a step, abc_wquantile_exchange names the
  * words of ws to all-reduce across ranks before the next step (offset in
  * bytes, count of int64 words, op 1 = sum, 2 = max, 3 = min, 4 = max of the

@@ -794,19 +794,13 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib) {
   // many short blocks: at N = M = 1e6 split 1 -> 32 is 181 -> 163 ms
   // (tools/bench_kde.py msplit); split % 8 == 0 pins each j-segment set to
   // one XCD's L2 (blocks go round-robin over the 8 XCDs)
-  // A block keeps >= ~3000 j-rows (about 50 64-row chunks): at N = M = 1e5
-  // split 64 gave blocks of 25 chunks whose prologue / partial writes cost
-  // 13 % (d = 1..6: 1.20 -> 1.04-1.09 ms with split 32; tools/kde_variants.py)
   constexpr int64_t target_blocks = 65536;
-  constexpr int64_t min_block_rows = 3000;
   MPlan p;
   p.nseg = kde_num_segments(npad);
   p.jseg = static_cast<int>(ceil_div(ceil_div(npad, p.nseg), 64) * 64);
   p.row_blocks = mpad_rows<D>(M) / (32 * kWaves * ib);
   int split = 1;
-  while (split < p.nseg && p.row_blocks * split < target_blocks &&
-         npad / (2 * split) >= min_block_rows)
-    split *= 2;
+  while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
   if (const char* env = getenv("ABC_KDE_MFMA_SPLIT")) {  // tuning override
     const int v = atoi(env);
     if (v >= 1 && v <= p.nseg && (p.nseg % v) == 0) split = v;
@@ -851,11 +845,9 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
       return;
     }
   }
-  // software pipelining pays at D <= 8 (VALU-bound) on long j-ranges; at
-  // larger D the MFMA chain dominates and the lower register count wins
-  // (bench_kde sweep); on short ranges (N = 1e5) its prologue costs 7 %
-  // (d = 4: 1.26 -> 1.17 ms without it; d = 8 at N = 1e6: 131 vs 132 ms)
-  if (env_int("ABC_KDE_MFMA_PIPE", D <= 8 && npad >= (int64_t{1} << 19)) != 0)
+  // software pipelining pays at D <= 8 (VALU-bound); at larger D the MFMA
+  // chain dominates and the lower register count wins (bench_kde sweep)
+  if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
                        p.spb, p.jseg, partial);

@@ -71,7 +71,15 @@ struct WQXchg {
   long long knext_x;          // MIN: smallest key above the knot
   unsigned long long wprev;   // SUM: mass of the key kprev
   unsigned long long wnext;   // SUM: mass of the key knext
-  unsigned long long pad[2];
+  // MIN: smallest single weight among the elements of key kprev / knext /
+  // the knot's key (fixed point; 2^63 - 1 when none).  With ties a key is
+  // a block of knots x_j = cs_j - w_j / 2 whose order inside the block
+  // numpy's argsort leaves open; the block is taken with its smallest
+  // weight at both ends (see wq_finalize_kernel)
+  unsigned long long wmin_prev;
+  unsigned long long wmin_next;
+  unsigned long long wmin_k;
+  unsigned long long pad;
   unsigned long long hist_w[kBins];  // SUM: fixed-point mass per digit
   unsigned long long hist_c[kBins];  // SUM: count per digit
 };
@@ -105,6 +113,7 @@ struct WQWide {
   unsigned long long cw[kWqCand];
 };
 constexpr unsigned long long kKeyFlip = 0x8000000000000000ull;
+constexpr unsigned long long kWMinNone = 0x7fffffffffffffffull;
 
 __device__ inline unsigned long long fixw(double w, double scale) {
   return static_cast<unsigned long long>(__double2ull_rn(w * scale));
@@ -121,6 +130,7 @@ __global__ void wq_reset_kernel(WQState* st) {
     st->x.knext_x = static_cast<long long>(~0ull ^ kKeyFlip);  // key max
     st->x.wprev = 0;
     st->x.wnext = 0;
+    st->x.wmin_prev = st->x.wmin_next = st->x.wmin_k = kWMinNone;
     st->prefix = 0;
     st->w_less = 0;
     st->w_eq = 0;
@@ -271,21 +281,44 @@ __global__ __launch_bounds__(256) void wq_neighbor_mass_kernel(
     WQState* st) {
   const unsigned long long kp = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
   const unsigned long long kn = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
+  const unsigned long long kk = st->none ? ~0ull : st->prefix;
   const double scale = st->scale;
   unsigned long long sp = 0, sn = 0;
+  unsigned long long mp = kWMinNone, mn = kWMinNone, mk = kWMinNone;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     const uint64_t k = f64_key(d[i]);
     const unsigned long long wi = fixw(w ? w[i] : 1.0, scale);
-    if (k == kp) sp += wi;
-    if (k == kn) sn += wi;
+    if (k == kp) {
+      sp += wi;
+      mp = wi < mp ? wi : mp;
+    }
+    if (k == kn) {
+      sn += wi;
+      mn = wi < mn ? wi : mn;
+    }
+    if (k == kk) mk = wi < mk ? wi : mk;
   }
   block_atomic_add_u64<256>(&st->x.wprev, sp);
   __syncthreads();
   block_atomic_add_u64<256>(&st->x.wnext, sn);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->x.wmin_prev, mp);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->x.wmin_next, mn);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->x.wmin_k, mk);
 }
 
-// np.interp(alpha, xp, fp) restricted to the bracketing knots
+// np.interp(alpha, xp, fp) restricted to the bracketing knots.  A key held
+// by several elements (ties) is a block of knots x_j = cs_j - w_j / 2, all
+// at the same point p: alpha between the block's first and last knot gives
+// p exactly, whatever the order inside the block.  numpy's argsort
+// (quicksort) leaves that order open, so the block's end knots are taken
+// with the block's smallest weight (wmin_*): the interval that gives p is
+// then the widest any order gives, and outside it the interpolation runs to
+// the neighbouring block's nearest knot.  Without ties every block is one
+// element and the arithmetic is the plain two-knot interpolation.
 __global__ void wq_finalize_kernel(const WQState* st, double alpha,
                                    double* __restrict__ out) {
   const double W = static_cast<double>(st->x.w_tot);
@@ -296,9 +329,15 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
     eps = key_f64(kprev);  // alpha past the last knot: largest point
   } else {
     const double pk = key_f64(st->prefix);
-    const double wk = static_cast<double>(st->w_eq) / W;
+    const unsigned long long wmk = st->x.wmin_k < st->w_eq ? st->x.wmin_k : st->w_eq;
+    const double wk = static_cast<double>(wmk) / W;
     const double csk = static_cast<double>(st->w_less + st->w_eq) / W;
+    // last knot of the block (= the only one without ties)
     const double xk = csk - 0.5 * wk;
+    // first knot of the block
+    const double xa = wmk == st->w_eq
+                          ? xk
+                          : static_cast<double>(st->w_less) / W + 0.5 * wk;
     // a sorted neighbour exists (zero-mass neighbours are knots too)
     const bool prev_ok = kprev != 0;
     const bool next_ok = knext != ~0ull;
@@ -307,23 +346,29 @@ __global__ void wq_finalize_kernel(const WQState* st, double alpha,
         eps = pk;
       } else {
         const double pn = key_f64(knext);
-        const double wn = static_cast<double>(st->x.wnext) / W;
+        const unsigned long long wmn =
+            st->x.wmin_next < st->x.wnext ? st->x.wmin_next : st->x.wnext;
+        const double wn = static_cast<double>(wmn) / W;
         const double xn = csk + wn - 0.5 * wn;
         const double slope = (pn - pk) / (xn - xk);
         eps = slope * (alpha - xk) + pk;
       }
+    } else if (alpha >= xa) {
+      eps = pk;  // inside the tied block
     } else {
       if (!prev_ok) {
         eps = pk;
       } else {
         const double pp = key_f64(kprev);
-        const double wp = static_cast<double>(st->x.wprev) / W;
+        const unsigned long long wmp =
+            st->x.wmin_prev < st->x.wprev ? st->x.wmin_prev : st->x.wprev;
+        const double wp = static_cast<double>(wmp) / W;
         const double csp = static_cast<double>(st->w_less) / W;
         const double xp = csp - 0.5 * wp;
         if (alpha == xp) {
           eps = pp;
         } else {
-          const double slope = (pk - pp) / (xk - xp);
+          const double slope = (pk - pp) / (xa - xp);
           eps = slope * (alpha - xp) + pp;
         }
       }
@@ -632,13 +677,41 @@ __global__ __launch_bounds__(1024) void wqc_finish_kernel(
   if (!kp_in) kp = st->kp_out;
   if (!kn_in) kn = st->kn_out;
   unsigned long long sp = 0, sn = 0;
+  unsigned long long mp = kWMinNone, mn = kWMinNone, mk = kWMinNone;
   for (long long i = t; i < cnt; i += 1024) {
     const unsigned long long k = key_at(i);
-    if (kp_in && k == kp) sp += mass_at(i);
-    if (kn_in && k == kn) sn += mass_at(i);
+    if (kp_in && k == kp) {
+      const unsigned long long m = mass_at(i);
+      sp += m;
+      mp = m < mp ? m : mp;
+    }
+    if (kn_in && k == kn) {
+      const unsigned long long m = mass_at(i);
+      sn += m;
+      mn = m < mn ? m : mn;
+    }
+    if (k == key) {
+      const unsigned long long m = mass_at(i);
+      mk = m < mk ? m : mk;
+    }
   }
   sp = wave_sum(sp);
   sn = wave_sum(sn);
+  // smallest single weights of the three keys (tie blocks, wq_finalize)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mp, o, 64);
+    const unsigned long long b = __shfl_xor(mn, o, 64);
+    const unsigned long long c = __shfl_xor(mk, o, 64);
+    mp = a < mp ? a : mp;
+    mn = b < mn ? b : mn;
+    mk = c < mk ? c : mk;
+  }
+  if ((t & 63) == 0) {
+    atomicMin(&st->x.wmin_prev, mp);
+    atomicMin(&st->x.wmin_next, mn);
+    atomicMin(&st->x.wmin_k, mk);
+  }
   __syncthreads();
   if ((t & 63) == 0) red[t >> 6] = sp;
   __syncthreads();
@@ -670,23 +743,35 @@ __global__ __launch_bounds__(256) void wqc_mass_kernel(
   const unsigned long long kp = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
   const unsigned long long kn = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
   const double scale = st->scale;
-  unsigned long long sp = 0, sn = 0;
+  unsigned long long sp = 0, sn = 0, mp = kWMinNone, mn = kWMinNone;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     const uint64_t k = f64_key(d[i]);
-    if ((need & 1) && k == kp) sp += fixw(w ? w[i] : 1.0, scale);
-    if ((need & 2) && k == kn) sn += fixw(w ? w[i] : 1.0, scale);
+    if ((need & 1) && k == kp) {
+      const unsigned long long m = fixw(w ? w[i] : 1.0, scale);
+      sp += m;
+      mp = m < mp ? m : mp;
+    }
+    if ((need & 2) && k == kn) {
+      const unsigned long long m = fixw(w ? w[i] : 1.0, scale);
+      sn += m;
+      mn = m < mn ? m : mn;
+    }
   }
   block_atomic_add_u64<256>(&st->x.wprev, sp);
   __syncthreads();
   block_atomic_add_u64<256>(&st->x.wnext, sn);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->x.wmin_prev, mp);
+  __syncthreads();
+  block_atomic_min_u64<256>(&st->x.wmin_next, mn);
 }
 
 // one step of the sharded select (see abc_wquantile_step_f64)
 enum WQStep {
   kWqReset = 0, kWqWmax = 1, kWqTotal = 2, kWqTarget = 3,
   kWqHist0 = 10, kWqSelect0 = 20, kWqNeighbors = 30, kWqMass = 31,
-  kWqFinish = 32
+  kWqFinish = 32, kWqMassMin = 33  // 33: exchange only (the mins of step 31)
 };
 
 int wq_step(int step, const double* d, const double* w, int64_t n,
@@ -724,6 +809,8 @@ int wq_step(int step, const double* d, const double* w, int64_t n,
   } else if (step == kWqFinish) {
     hipLaunchKernelGGL(wq_finalize_kernel, dim3(1), dim3(1), 0, st, s, alpha,
                        out4);
+  } else if (step == kWqMassMin) {
+    // no kernel: the host all-reduces the three smallest weights (MIN)
   } else {
     set_error("wquantile: unknown step %d", step);
     return kInvalidArg;
@@ -1418,6 +1505,8 @@ int abc_wquantile_exchange(int step, int64_t* offset_bytes, int64_t* count,
     *offset_bytes = offsetof(WQXchg, kprev_x); *count = 2; *op = 4;
   } else if (step == kWqMass) {
     *offset_bytes = offsetof(WQXchg, wprev); *count = 2; *op = 1;
+  } else if (step == kWqMassMin) {
+    *offset_bytes = offsetof(WQXchg, wmin_prev); *count = 3; *op = 3;
   }
   return kOk;
 }

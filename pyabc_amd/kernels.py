@@ -385,7 +385,7 @@ def column_std(data_T, n=None):
 
 
 _WQ_SEQ = [0, 1, 2, 3] + [s for p in range(8) for s in (10 + p, 20 + p)] \
-    + [30, 31, 32]
+    + [30, 31, 33, 32]
 
 
 def weighted_quantile(d, w, alpha, comm=None):

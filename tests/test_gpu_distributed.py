@@ -59,6 +59,10 @@ def _generation(comm, n, min_batch, record):
                                 record=record)
     th, dd, ww, n_eval, _ = eng.gather_population(res)
     eps1 = float(K.weighted_quantile(dd, ww, 0.5, comm=comm)[0].item())
+    # heavily tied distances (the sharded tie-block words, exchange step 33)
+    dt = torch.round(dd * 2.0) / 2.0
+    eps_ties = [float(K.weighted_quantile(dt, wq, a, comm=comm)[0].item())
+                for wq in (ww, None) for a in (0.3, 0.5, 0.7, 0.9)]
     fit1 = DeviceMVNFit(th, ww)
     # exact-inference generation: stochastic acceptance with u keyed by the
     # global evaluation id, acceptance weights, particle records
@@ -75,7 +79,7 @@ def _generation(comm, n, min_batch, record):
                 stats=res.stats_T.cpu().numpy(),
                 rec=None if res.rec_stats_T is None
                 else res.rec_stats_T.cpu().numpy(),
-                eps1=eps1, cov1=fit1.cov,
+                eps1=eps1, eps_ties=np.array(eps_ties), cov1=fit1.cov,
                 s_theta=rs.theta.cpu().numpy(), s_d=rs.d.cpu().numpy(),
                 s_w=rs.w.cpu().numpy(), s_accw=rs.accw.cpu().numpy(),
                 s_rec_theta=rs.rec_theta.cpu().numpy(),
@@ -119,7 +123,7 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     for r in (0, 1):
         got = res[r]
         for k in ("theta0", "theta", "d", "w", "logpd", "stats", "rec",
-                  "cov1", "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta",
+                  "cov1", "eps_ties", "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta",
                   "s_rec_d", "s_rec_acc"):
             np.testing.assert_array_equal(got[k], one[k], err_msg=k)
         for k in ("eps0", "eps1", "n_eval", "s_n_eval"):

@@ -537,6 +537,84 @@ def test_weighted_quantile_golden(K):
             assert abs(qu - g[f"qu_{N}"][j]) <= tolu
 
 
+def _wq_tie_blocks(d, w, alpha):
+    """np.interp over knots where each run of equal points is one block
+    whose end knots carry the block's smallest weight (the device's
+    convention for ties, wq_finalize_kernel); equal to the reference
+    whenever the block order is immaterial."""
+    order = np.argsort(d, kind="stable")
+    p, ww = d[order], w[order]
+    cs = np.cumsum(ww)
+    xs, fs = [], []
+    start = 0
+    for i in range(1, len(p) + 1):
+        if i == len(p) or p[i] != p[start]:
+            wmin = ww[start:i].min()
+            lo = (cs[start - 1] if start else 0.0) + 0.5 * wmin
+            hi = cs[i - 1] - 0.5 * wmin
+            xs += [lo, hi] if i - start > 1 else [cs[i - 1] - 0.5 * ww[start]]
+            fs += [p[start]] * (2 if i - start > 1 else 1)
+            start = i
+    return float(np.interp(alpha, xs, fs))
+
+
+@pytest.mark.parametrize("case", ["ties70", "discrete", "zeros", "spike_edges"])
+def test_weighted_quantile_ties_large(K, case):
+    """N = 1.2e6 with heavy ties (the selected 22-bit bucket overflows the
+    candidate buffer: the single-block finish reads the full arrays), few
+    distinct values, a block of zero distances and a tie spike, alpha at
+    0.1 / 0.5 / 0.9, in the middle of the tied block and at its edges.
+    A run of equal points is a block of knots at one p: alpha between its
+    first and last knot gives p exactly (weighted_statistics.py:26-43).
+    Uniform weights and block interiors do not depend on the order numpy's
+    argsort gives the ties: equal to the oracle; the block edges with
+    random weights follow the device's convention (the block's smallest
+    weight at both ends, include/abc_hip.h)."""
+    import time
+    rng = np.random.default_rng({"ties70": 1, "discrete": 2, "zeros": 3,
+                                 "spike_edges": 4}[case])
+    N = 1_200_000
+    if case == "ties70":
+        d = np.where(rng.uniform(size=N) < 0.7, 3.0, rng.exponential(size=N) * 5)
+    elif case == "discrete":
+        d = rng.integers(0, 5, size=N).astype(float)
+    elif case == "zeros":
+        d = np.where(rng.uniform(size=N) < 0.4, 0.0, rng.uniform(1, 2, size=N))
+    else:
+        d = np.where(rng.uniform(size=N) < 0.5, 1.5, rng.normal(size=N))
+    w = rng.uniform(0.5, 1.5, size=N)
+    w /= w.sum()
+    pt = {"ties70": 3.0, "discrete": 2.0, "zeros": 0.0, "spike_edges": 1.5}[case]
+    below, inb = w[d < pt].sum(), w[d == pt].sum()
+    dd, ww = dev(d), dev(w)
+    srt = np.sort(d)
+    gaps = np.diff(srt)
+    slope = np.max(gaps) / np.min(w) * 2
+    for a in [0.1, 0.5, 0.9, below + 0.5 * inb]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        q = float(host(K.weighted_quantile(dd, ww, a))[0])
+        dt = time.perf_counter() - t0
+        want = ref.weighted_quantile(d, w, a)
+        tol = 1e-12 * abs(want) + slope * N * 2.0 ** -52
+        assert abs(q - want) <= tol, (case, a, q, want)
+        print(f"{case} alpha={a:.6f}: q={q!r} want={want!r} "
+              f"({dt * 1e3:.2f} ms incl. host read)")
+    assert float(host(K.weighted_quantile(dd, ww, below + 0.5 * inb))[0]) == pt
+    # uniform weights: the block edges are order-independent
+    wu = np.full(N, 1.0 / N)
+    for a in [below, below + 0.25 / N, below + inb - 0.25 / N, 0.5]:
+        a = float(a)
+        q = float(host(K.weighted_quantile(dd, None, a))[0])
+        want = ref.weighted_quantile(d, wu, a)
+        assert abs(q - want) <= 1e-12 * abs(want) + np.max(gaps) * 1e-9, (a, q, want)
+    # random weights at the block edges: the device's convention
+    for a in [below + 1e-9, below + inb - 1e-9]:
+        q = float(host(K.weighted_quantile(dd, ww, a))[0])
+        want = _wq_tie_blocks(d, w, a)
+        assert abs(q - want) <= 1e-12 * abs(want) + np.max(gaps) * 1e-6, (a, q, want)
+
+
 def test_weighted_quantile_kat(K):
     """test/test_weighted_statistics.py:6-20 on the device path."""
     pts = dev([1, 5, 2.5])

@@ -756,6 +756,133 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
   }
 }
 
+// ---- folded, hand-interleaved LDS-DMA pass (d <= 8) -------------------------
+// The register kernel's arithmetic (hi products first, the lo chain on top
+// in the same accumulator, then tile_sum's exps and tree) with the A
+// fragments shared by the block through LDS (as kde_mfma_lds2i_kernel) and
+// the retiring tile's 32 IB sum ops spread evenly over the next chain's
+// KT IB MFMA gaps.  Rows bit-identical to kde_mfma_kernel's.
+template <int KT, int IB>
+struct FoldPlan {
+  static constexpr int NG = KT * IB;
+  static constexpr int NS = 32 * IB;
+  static constexpr int s0(int g) { return g * NS / NG; }
+};
+template <int KT, int IB, int G>
+__device__ __forceinline__ void fold_gap_ops(f32x16 (&h)[IB], float (&sacc)[IB]) {
+  using P = FoldPlan<KT, IB>;
+  split_sum_ops<IB, P::s0(G), P::s0(G + 1)>(h, sacc);
+}
+template <int KT, int IB, bool VALU, int C = 0>
+__device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, int lane,
+                                            const bf16x8 (&bq)[IB][KT],
+                                            f32x16 (&acc)[IB], f32x16 (&prev)[IB],
+                                            float (&sacc)[IB], bf16x8 (&a)[2]) {
+  if constexpr (C < KT) {
+    bf16x8 nxt = a[(C + 1) & 1];
+    if constexpr (C + 2 < KT) nxt = Ab[tile * KT + C + 2][lane];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+          a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (VALU) {
+#define ABC_GAP(TT) \
+  if (t == TT) fold_gap_ops<KT, IB, C * IB + TT>(prev, sacc);
+        ABC_GAP(0)
+        ABC_GAP(1)
+        ABC_GAP(2)
+#undef ABC_GAP
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    a[C & 1] = nxt;
+    lds_chain_f<KT, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, sacc, a);
+  }
+}
+
+template <int KH, int KL, int IB>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
+    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
+    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int CH = 2 * KT;
+  static_assert(KL <= kFoldKL, "folded accumulation only");
+  static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int s = blockIdx.x % split;
+  const int64_t rb = blockIdx.x / split;
+  const int64_t t0 = (rb * kWaves + wave) * IB;
+
+  bf16x8 bq[IB][KT];
+#pragma unroll
+  for (int t = 0; t < IB; ++t)
+#pragma unroll
+    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+
+  for (int gi = 0; gi < spb; ++gi) {
+    const int seg = s * spb + gi;
+    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
+    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    auto fill = [&](int buf, int jc) {
+      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+      for (int f = wave; f < CH; f += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            src + f * 64 + lane,
+            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+    };
+    __syncthreads();
+    if (nj > 0) fill(0, 0);
+    int buf = 0;
+    f32x16 accA[IB], accB[IB];
+    float sprev[IB], scur[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) sprev[t] = scur[t] = 0.0f;
+    for (int jc = 0; jc < nj; jc += 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      const bf16x8(*Ab)[64] = As[buf];
+      bf16x8 a[2];
+      a[0] = Ab[0][lane];
+      a[1] = Ab[1][lane];
+      if (jc == 0) {
+        lds_chain_f<KT, IB, false>(Ab, 0, lane, bq, accA, accB, sprev, a);
+      } else {
+        lds_chain_f<KT, IB, true>(Ab, 0, lane, bq, accA, accB, sprev, a);
+#pragma unroll
+        for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < IB; ++t) scur[t] = 0.0f;
+      a[0] = Ab[KT][lane];
+      a[1] = Ab[KT + 1][lane];
+      lds_chain_f<KT, IB, true>(Ab, 1, lane, bq, accB, accA, scur, a);
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
+      buf ^= 1;
+    }
+    if (nj > 0) {
+#pragma unroll
+      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL>(accB[t], accB[t]);
+#pragma unroll
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+    }
+  }
+}
+
 template <int D>
 int64_t mpad_rows(int64_t M) {
   constexpr int rows = 32 * kWaves * Mk<D>::PADIB;
@@ -840,6 +967,16 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     }
     if (lds2 != 0) {
       hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         p.spb, p.jseg, partial);
+      return;
+    }
+  }
+  if constexpr (D <= 8) {
+    // 1: the folded pass with LDS-DMA A fragments and hand-placed VALU
+    // (kde_mfma_lds2g_kernel); rows bit-identical
+    if (env_int("ABC_KDE_MFMA_LDS2", 0) == 1) {
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
                          p.spb, p.jseg, partial);
       return;

@@ -941,8 +941,9 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib) {
 // test_kde_mfma_launch_knobs_bit_identical checks that each leaves every row
 // unchanged): ABC_KDE_MFMA_SPLIT (j-segment blocks per row block),
 // ABC_KDE_MFMA_IB (i-tiles per wave), ABC_KDE_MFMA_PIPE (software
-// pipelining of the register kernel), ABC_KDE_MFMA_LDS2 at d > 8 (0: the
-// register kernel, 1: LDS-DMA A fragments).
+// pipelining of the register kernel), ABC_KDE_MFMA_LDS2 (d > 8 -- 0: the
+// register kernel, 1: LDS-DMA A fragments, 2: the same hand-interleaved;
+// d <= 8 -- 0: the register kernel, 1: the folded LDS-DMA pass).
 int env_int(const char* name, int dflt) {
   const char* env = getenv(name);
   return env ? atoi(env) : dflt;
@@ -950,7 +951,7 @@ int env_int(const char* name, int dflt) {
 
 template <int D, int IB>
 void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
-                 const bf16x8* Afr, int64_t npad, double* partial,
+                 const bf16x8* Afr, int64_t npad, double* partial, int lds2g,
                  hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
   const dim3 block(64 * kWaves);
@@ -973,9 +974,9 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     }
   }
   if constexpr (D <= 8) {
-    // 1: the folded pass with LDS-DMA A fragments and hand-placed VALU
+    // the folded pass with LDS-DMA A fragments and hand-placed VALU
     // (kde_mfma_lds2g_kernel); rows bit-identical
-    if (env_int("ABC_KDE_MFMA_LDS2", 0) == 1) {
+    if (lds2g) {
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
                          p.spb, p.jseg, partial);
@@ -1004,9 +1005,16 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   constexpr int IBF = Mk<D>::IB;
   constexpr int IBH = IBF > 1 ? IBF / 2 : 1;
   constexpr int IB2 = IBF == 3 ? 2 : IBF;  // the third choice at D <= 8
-  int ib = IBF;
-  const int v = env_int("ABC_KDE_MFMA_IB", IBF);
-  if (v == IBH || v == IB2) ib = v;
+  // D <= 8 on a large population: the LDS-DMA folded pass at IB = 2 (three
+  // waves per SIMD) is the default -- 133.4-133.7 -> 131.1-131.3 ms at
+  // N = M = 1e6, d = 8, interleaved A/B in one process (gpurun_out/lds2g2);
+  // IB = 3 there ran 136.5 ms, IB = 1 149 ms.  Small populations keep the
+  // register kernel (equal at N = 1e5, d = 4).
+  const int lds2g =
+      D <= 8 ? env_int("ABC_KDE_MFMA_LDS2", npad >= (int64_t{1} << 19) ? 1 : 0) : 0;
+  int ib = lds2g ? IB2 : IBF;
+  const int v = env_int("ABC_KDE_MFMA_IB", ib);
+  if (v == IBF || v == IBH || v == IB2) ib = v;
   const MPlan p = make_mplan<D>(M, npad, ib);
   const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
@@ -1018,11 +1026,11 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   int* fix_rows = n_fix + 4;
   ABC_HIP(hipMemsetAsync(n_fix, 0, 16, st));
   if (ib == IBF)
-    launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, st);
+    launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, lds2g, st);
   else if (ib == IB2)
-    launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, partial, st);
+    launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, partial, lds2g, st);
   else
-    launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, st);
+    launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, lds2g, st);
   ABC_LAUNCH_CHECK("kde_mfma_kernel");
   return kde_finish_mfma(partial, M, p.nseg, Ynew, P, npad, d, lw2max,
                          log_const, out, n_fix, fix_rows, st);

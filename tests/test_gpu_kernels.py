@@ -156,7 +156,8 @@ KNOBS = {
         ("ABC_KDE_MFMA_LDS2", "1")],
     8: [("ABC_KDE_MFMA_PIPE", "0"), ("ABC_KDE_MFMA_IB", "1"),
         ("ABC_KDE_MFMA_IB", "2"), ("ABC_KDE_MFMA_SPLIT", "1"),
-        ("ABC_KDE_MFMA_SPLIT", "8"), ("ABC_KDE_MFMA_LDS2", "1")],
+        ("ABC_KDE_MFMA_SPLIT", "8"), ("ABC_KDE_MFMA_LDS2", "1"),
+        ("ABC_KDE_MFMA_LDS2", "0")],
     20: [("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_LDS2", "0"),
          ("ABC_KDE_MFMA_IB", "1"), ("ABC_KDE_MFMA_SPLIT", "2"),
          ("ABC_KDE_MFMA_PIPE", "1")],

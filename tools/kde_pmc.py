@@ -28,12 +28,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def load(path, kernel="kde_mfma_kernel"):
+HEADLINE_KERNELS = ("kde_mfma_kernel", "kde_mfma_lds2g_kernel")
+
+
+def load(path, kernel=HEADLINE_KERNELS):
     per = collections.defaultdict(dict)
     if not os.path.exists(path):
         return per
+    names = (kernel,) if isinstance(kernel, str) else kernel
     for r in csv.DictReader(open(path)):
-        if kernel not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in names):
             continue
         per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
         per[r["Dispatch_Id"]]["_ns"] = (int(r["End_Timestamp"])
@@ -64,7 +68,7 @@ def main(prof_dir, tag, N=1_000_000, M=1_000_000, d=8):
     cyc = max(issue, 32 * mfma)
     out = {
         "source": f"rocprofv3 --pmc passes over bench.py ({prof_dir}), "
-                  f"kde_mfma_kernel, N={N} M={M} d={d}",
+                  f"MFMA KDE pass (kde_mfma_kernel / kde_mfma_lds2g_kernel), N={N} M={M} d={d}",
         "N": N, "M": M, "d": d, "npad": npad, "mpad": mpad,
         "tiles_per_launch": tiles,
         "counters_per_launch": avg,

@@ -63,7 +63,8 @@ def main(prof_dir, tag):
         wr.writeheader()
         for r in rows:
             wr.writerow(r)
-    kde = [r for r in rows if r["kernel"].startswith("kde_mfma_kernel")] or \
+    kde = [r for r in rows if r["kernel"].startswith(("kde_mfma_kernel",
+                                                      "kde_mfma_lds2g_kernel"))] or \
         [r for r in rows if r["kernel"].startswith("kde_main")]
     if kde:
         r = kde[0]

@@ -20,10 +20,10 @@
 #include "common.hpp"
 #include "philox.hpp"
 #include "spatial.hpp"
+#include "local_common.hpp"
 
 namespace abc {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kKnnRows = 8;     // rows per wave (one wave per block)
 constexpr int kMaxK = 192;      // buffer of 256 = k kept + 64 appended
@@ -485,50 +485,6 @@ __global__ __launch_bounds__(128) void local_cov_kernel(
   dets[n] = det;
 }
 
-// per-previous-particle constants: lc_n = log(w_n / sqrt((2 pi)^d det_n)),
-// the global offset L = max_n lc_n (ordered-key atomic max), and the
-// symmetric quadratic-form coefficients of inv_n packed row by row:
-// (A_aa, A_ab + A_ba for b > a), d(d+1)/2 per particle.
-__global__ __launch_bounds__(256) void local_const_kernel(
-    const double* __restrict__ w, const double* __restrict__ dets,
-    const double* __restrict__ invs, int64_t N, int d,
-    double* __restrict__ lc, double* __restrict__ coef,
-    unsigned long long* __restrict__ lc_max_key) {
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  uint64_t key = 0;
-  if (n < N) {
-    const double norm = sqrt(pow(2.0 * 3.141592653589793, d) * dets[n]);
-    const double v = w[n] > 0.0 ? log(w[n] / norm) : -INFINITY;
-    lc[n] = v;
-    if (v == v) key = f64_key(v);
-    const double* A = invs + n * d * d;
-    double* c = coef + n * (d * (d + 1) / 2);
-    int t = 0;
-    for (int a = 0; a < d; ++a) {
-      c[t++] = A[a * d + a];
-      for (int b = a + 1; b < d; ++b) c[t++] = A[a * d + b] + A[b * d + a];
-    }
-  }
-  block_atomic_max_u64<256>(lc_max_key, static_cast<unsigned long long>(key));
-}
-
-// q = (theta - X_n)^T inv_n (theta - X_n) from the packed symmetric form
-// (d(d+1)/2 + d FMAs instead of d^2 + d)
-template <int D>
-__device__ inline double local_qform(const double (&dl)[D],
-                                     const double* __restrict__ c) {
-  double q = 0.0;
-  int t = 0;
-#pragma unroll
-  for (int a = 0; a < D; ++a) {
-    double r = c[t++] * dl[a];
-#pragma unroll
-    for (int b = a + 1; b < D; ++b) r = fma(c[t++], dl[b], r);
-    q = fma(dl[a], r, q);
-  }
-  return q;
-}
-
 // Main pass: one thread per evaluation point, the previous population's
 // (X_n, coef_n, lc_n) streaming through the scalar path (wave-uniform n).
 // Terms are exp(lc_n - q_n/2 - L) <= 1 (q >= 0), summed in fp64 without a
@@ -560,189 +516,6 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
     acc += exp(fma(-0.5, qf, lc[n] - L));
   }
   if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
-}
-
-// fp32 pass (precision="f32", 1e-5 relative): the same sum with the
-// population centred on X[0] in fp64, the packed coefficients pre-scaled by
-// log2(e)/2 and lc by log2(e), so a term is one v_exp_f32 of (lc2_n - q'_n);
-// 16 terms are added in fp32, then into fp64.  Centred coordinates are kept
-// as an fp32 (hi, lo) pair, x - X[0] = hi + lo, and the pair difference is
-// (th_hi - X_hi) + (th_lo - X_lo): its error is ~2^-24 of the difference
-// itself, not of the distance R to X[0], so the density's accuracy does not
-// degrade with the population's extent over the local bandwidth (a single
-// fp32 rounding of x - X[0] costs ~ sqrt(q) (R / sigma) 2^-23 relative).
-// Layout: particles in PAIRS (n, n + 1) interleaved per coordinate, so one
-// 64-bit scalar load feeds a packed-fp32 operand (v_pk_*_f32) that serves
-// two particles at once: X2[(n / 2) * D + q] = (x_n, x_{n+1}), the same for
-// the lo parts, coef2[(n / 2) * NC + t] and lc2[n / 2].  The count is padded
-// to even with a particle of lc = -inf (exp2 -> 0).
-template <int D>
-__global__ __launch_bounds__(256) void local_pack32_kernel(
-    const double* __restrict__ X, const double* __restrict__ coef,
-    const double* __restrict__ lc, const unsigned long long* __restrict__ lc_max_key,
-    int64_t N, float* __restrict__ X32, float* __restrict__ X32lo,
-    float* __restrict__ coef32, float* __restrict__ lc32) {
-  constexpr int NC = D * (D + 1) / 2;
-  const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (n >= ((N + 1) & ~int64_t{1})) return;
-  const int64_t pr = n >> 1;
-  const int h = static_cast<int>(n & 1);
-  if (n >= N) {  // padding particle of an odd count
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      X32[(pr * D + q) * 2 + h] = 0.0f;
-      X32lo[(pr * D + q) * 2 + h] = 0.0f;
-    }
-#pragma unroll
-    for (int t = 0; t < NC; ++t) coef32[(pr * NC + t) * 2 + h] = 0.0f;
-    lc32[n] = -INFINITY;
-    return;
-  }
-  const double L = key_f64(*lc_max_key);
-  constexpr double kLog2e = 1.4426950408889634;
-#pragma unroll
-  for (int q = 0; q < D; ++q) {
-    const double c = X[n * D + q] - X[q];
-    const float hi = static_cast<float>(c);
-    X32[(pr * D + q) * 2 + h] = hi;
-    X32lo[(pr * D + q) * 2 + h] = static_cast<float>(c - static_cast<double>(hi));
-  }
-#pragma unroll
-  for (int t = 0; t < NC; ++t)
-    coef32[(pr * NC + t) * 2 + h] = static_cast<float>(coef[n * NC + t] * (0.5 * kLog2e));
-  lc32[n] = static_cast<float>((lc[n] - L) * kLog2e);
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void local_pts32_kernel(const double* __restrict__ pts,
-                                                          int64_t M,
-                                                          const double* __restrict__ X,
-                                                          float* __restrict__ pts32,
-                                                          float* __restrict__ pts32lo) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= M) return;
-#pragma unroll
-  for (int q = 0; q < D; ++q) {
-    const double c = pts[i * D + q] - X[q];
-    const float h = static_cast<float>(c);
-    pts32[i * D + q] = h;
-    pts32lo[i * D + q] = static_cast<float>(c - static_cast<double>(h));
-  }
-}
-
-// Two particles per packed-fp32 lane pair: the (hi, lo) differences, the
-// quadratic form's FMAs and the exponent arguments of particles n and n + 1
-// run as v_pk_add / v_pk_fma / v_pk_mul on SGPR-pair operands, about half
-// the VALU instructions of the one-particle loop; two v_exp_f32 per pair.
-// Terms of 8 pairs are added in fp32 (even and odd particles apart), then
-// into fp64.  nchunk is even, so no pair straddles two chunks.
-template <int D>
-__global__ __launch_bounds__(256) void local_pdf32_kernel(
-    const float* __restrict__ pts, const float* __restrict__ ptslo, int64_t M,
-    const f32x2* __restrict__ X2, const f32x2* __restrict__ X2lo,
-    const f32x2* __restrict__ coef2, const f32x2* __restrict__ lc2, int64_t N,
-    int split, int64_t nchunk, double* __restrict__ part) {
-  constexpr int NC = D * (D + 1) / 2;
-  const int s = blockIdx.x % split;
-  const int64_t i0 = static_cast<int64_t>(blockIdx.x / split) * 256 + threadIdx.x;
-  const int64_t i = i0 < M ? i0 : M - 1;
-  f32x2 th[D], tl[D];
-#pragma unroll
-  for (int q = 0; q < D; ++q) {
-    const float a = pts[i * D + q], b = ptslo[i * D + q];
-    th[q] = f32x2{a, a};
-    tl[q] = f32x2{b, b};
-  }
-  double acc = 0.0;
-  const int64_t n0 = static_cast<int64_t>(s) * nchunk;  // even
-  int64_t n1 = n0 + nchunk;
-  const int64_t npair = (N + 1) & ~int64_t{1};
-  if (n1 > npair) n1 = npair;
-  for (int64_t b = n0; b < n1; b += 16) {
-    const int64_t be = b + 16 < n1 ? b + 16 : n1;
-    f32x2 a2 = f32x2{0.0f, 0.0f};
-    for (int64_t n = b; n < be; n += 2) {
-      const int64_t pr = n >> 1;
-      f32x2 dl[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q)
-        dl[q] = (th[q] - X2[pr * D + q]) + (tl[q] - X2lo[pr * D + q]);
-      const f32x2* c = coef2 + pr * NC;
-      f32x2 qf = f32x2{0.0f, 0.0f};
-      int t = 0;
-#pragma unroll
-      for (int a = 0; a < D; ++a) {
-        f32x2 r = c[t++] * dl[a];
-#pragma unroll
-        for (int bb = a + 1; bb < D; ++bb)
-          r = __builtin_elementwise_fma(c[t++], dl[bb], r);
-        qf = __builtin_elementwise_fma(dl[a], r, qf);
-      }
-      const f32x2 e = lc2[pr] - qf;
-      a2 += f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-    }
-    acc += static_cast<double>(a2.x + a2.y);
-  }
-  if (i0 < M) part[static_cast<int64_t>(s) * M + i0] = acc;
-}
-
-__global__ __launch_bounds__(256) void local_pdf_final_kernel(
-    const double* __restrict__ part, int64_t M, int split,
-    const unsigned long long* __restrict__ lc_max_key,
-    const double* __restrict__ logsumw, double* __restrict__ out,
-    int* __restrict__ n_fix, int* __restrict__ fix_rows, double thresh) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= M) return;
-  double S = 0.0;
-  for (int s = 0; s < split; ++s) S += part[s * M + i];
-  if (S >= thresh) {
-    out[i] = key_f64(*lc_max_key) + log(S) - *logsumw;
-  } else {  // the fixed offset underflowed: exact two-pass evaluation
-    fix_rows[atomicAdd(n_fix, 1)] = static_cast<int>(i);
-    out[i] = -INFINITY;
-  }
-}
-
-// exact max-then-sum for rows whose fixed-offset sum underflowed
-template <int D>
-__global__ __launch_bounds__(256) void local_pdf_fixup_kernel(
-    const double* __restrict__ pts, const double* __restrict__ X,
-    const double* __restrict__ coef, const double* __restrict__ lc, int64_t N,
-    const double* __restrict__ logsumw, const int* __restrict__ n_fix,
-    const int* __restrict__ fix_rows, double* __restrict__ out) {
-  constexpr int NC = D * (D + 1) / 2;
-  __shared__ double red[4];
-  const int count = *n_fix;
-  for (int f = blockIdx.x; f < count; f += gridDim.x) {
-    const int64_t i = fix_rows[f];
-    double th[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) th[q] = pts[i * D + q];
-    double m = -INFINITY;
-    for (int64_t n = threadIdx.x; n < N; n += 256) {
-      double dl[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
-      m = fmax(m, fma(-0.5, local_qform<D>(dl, coef + n * NC), lc[n]));
-    }
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    __syncthreads();
-    double sum = 0.0;
-    if (m > -INFINITY)
-      for (int64_t n = threadIdx.x; n < N; n += 256) {
-        double dl[D];
-#pragma unroll
-        for (int q = 0; q < D; ++q) dl[q] = th[q] - X[n * D + q];
-        sum += exp(fma(-0.5, local_qform<D>(dl, coef + n * NC), lc[n]) - m);
-      }
-    sum = block_sum<double, 256>(sum, red);
-    if (threadIdx.x == 0)
-      out[i] = (m > -INFINITY ? m + log(sum) : -INFINITY) - *logsumw;
-    __syncthreads();
-  }
 }
 
 
@@ -822,71 +595,6 @@ void convert(const S* src, int64_t n, D* dst, hipStream_t st) {
     hipLaunchKernelGGL((convert_kernel<S, D>), dim3(stream_grid(n, 256, 2048)),
                        dim3(256), 0, st, src, n, dst);
 }
-inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
-
-// Workspace of the spatial index (spatial.hpp) over n points padded to
-// whole tiles: header (ext keys, counters) | keys_in[n] | keys_out[n] |
-// vals_in[n] | perm[T*64] | tbox[T][2][8] | sort temp.
-struct SpatialWs {
-  unsigned long long* ext;  // [16]: per-dim min keys, then max keys
-  int* count;
-  uint64_t* keys_in;
-  uint64_t* keys_out;
-  int32_t* vals_in;
-  int32_t* perm;
-  float* tbox;
-  void* temp;
-  size_t temp_bytes;
-  int T;
-};
-
-static size_t spatial_ws_bytes(int64_t n) {
-  const int64_t T = ceil_div(n > 0 ? n : 1, kTile);
-  return 256 + 2 * al256(static_cast<size_t>(n) * 8) + al256(static_cast<size_t>(n) * 4) +
-         al256(static_cast<size_t>(T) * kTile * 4) + al256(static_cast<size_t>(T) * 2 * 8 * 4) +
-         al256(sort_pairs_temp_bytes(n));
-}
-
-static SpatialWs spatial_ws(void* ws, int64_t n) {
-  SpatialWs v;
-  char* q = static_cast<char*>(ws);
-  v.T = static_cast<int>(ceil_div(n > 0 ? n : 1, kTile));
-  v.ext = reinterpret_cast<unsigned long long*>(q);
-  v.count = reinterpret_cast<int*>(q + 128);
-  q += 256;
-  v.keys_in = reinterpret_cast<uint64_t*>(q);
-  q += al256(static_cast<size_t>(n) * 8);
-  v.keys_out = reinterpret_cast<uint64_t*>(q);
-  q += al256(static_cast<size_t>(n) * 8);
-  v.vals_in = reinterpret_cast<int32_t*>(q);
-  q += al256(static_cast<size_t>(n) * 4);
-  v.perm = reinterpret_cast<int32_t*>(q);
-  q += al256(static_cast<size_t>(v.T) * kTile * 4);
-  v.tbox = reinterpret_cast<float*>(q);
-  q += al256(static_cast<size_t>(v.T) * 2 * 8 * 4);
-  v.temp = q;
-  v.temp_bytes = al256(sort_pairs_temp_bytes(n));
-  return v;
-}
-
-// Morton order of X (spatial.hpp): ext, keys, sort -> keys_out / perm (the
-// padding positions of the last tile map to particle 0).
-template <int D>
-static int spatial_sort_population(const double* X, int64_t N, SpatialWs& v,
-                                   hipStream_t st) {
-  ABC_HIP(hipMemsetAsync(v.ext, 0xff, 64, st));
-  ABC_HIP(hipMemsetAsync(v.ext + 8, 0, 64 + 8, st));
-  hipLaunchKernelGGL((sp_extent_kernel<D>), dim3(stream_grid(N, 256, 64)), dim3(256),
-                     0, st, X, N, v.ext);
-  hipLaunchKernelGGL((sp_key_kernel<D>), dim3(ceil_div(N, 256)), dim3(256), 0, st,
-                     X, N, X, v.ext, v.keys_in, v.vals_in);
-  ABC_HIP(sort_pairs(v.temp, v.temp_bytes, v.keys_in, v.keys_out, v.vals_in, v.perm,
-                     N, morton_bits(D) * D, st));
-  const int64_t pad = static_cast<int64_t>(v.T) * kTile - N;
-  if (pad > 0) ABC_HIP(hipMemsetAsync(v.perm + N, 0, pad * 4, st));
-  return kOk;
-}
-
 
 }  // namespace abc
 
@@ -1025,14 +733,6 @@ int abc_local_cov_f64(const double* X, const double* w, int64_t N, int d,
 // The n-range is cut into a fixed number of chunks that depends on N only,
 // so a row's log-sum-exp does not depend on M or on how rows are shared
 // between ranks (multi-GPU results equal single-GPU results bit for bit).
-static void local_plan(int64_t /*M*/, int64_t N, int& split, int64_t& nchunk) {
-  int64_t sp = 64;
-  if (sp > N) sp = N;
-  if (sp < 1) sp = 1;
-  split = static_cast<int>(sp);
-  nchunk = ceil_div(N, sp);
-}
-
 size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N) {
   int split;
   int64_t nchunk;
@@ -1041,16 +741,6 @@ size_t abc_local_logpdf_workspace_bytes(int64_t M, int64_t N) {
   // | part[split][M] | fix_rows[M]
   return 64 + static_cast<size_t>(N) * 8 * 37 +
          static_cast<size_t>(split) * M * 8 + static_cast<size_t>(M) * 4 + 512;
-}
-
-__global__ __launch_bounds__(256) void local_sumw_kernel(const double* __restrict__ w,
-                                                         int64_t N,
-                                                         double* __restrict__ out) {
-  __shared__ double red[4];
-  double s = 0.0;
-  for (int64_t i = threadIdx.x; i < N; i += 256) s += w[i];
-  s = block_sum<double, 256>(s, red);
-  if (threadIdx.x == 0) *out = log(s);
 }
 
 int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
@@ -1101,86 +791,6 @@ int abc_local_logpdf_f64(const double* pts, int64_t M, const double* X,
   }
 #undef L
   ABC_LAUNCH_CHECK("local_logpdf kernels");
-  return kOk;
-}
-
-size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N) {
-  // the fp64 layout, then X32[N][8] | X32lo[N][8] | coef32[N][36] | lc32[N]
-  // | pts32[M][8] | pts32lo[M][8]
-  // (N padded to even: particle pairs)
-  return abc_local_logpdf_workspace_bytes(M, N) +
-         static_cast<size_t>(N + 1) * 4 * 53 + static_cast<size_t>(M) * 4 * 16 + 512;
-}
-
-int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
-                         const double* w, const double* inv_covs,
-                         const double* dets, int64_t N, int d,
-                         double* out_logpdf, void* ws, size_t ws_bytes,
-                         hipStream_t st) {
-  ABC_REQUIRE(M >= 0 && N >= 1, "local_logpdf_f32: bad sizes");
-  if (M == 0) return kOk;
-  ABC_REQUIRE(d >= 1 && d <= 8, "local_logpdf_f32: unsupported d=%d (d <= 8)", d);
-  ABC_REQUIRE(pts && X && w && inv_covs && dets && out_logpdf && ws,
-              "local_logpdf_f32: null pointer");
-  ABC_REQUIRE(ws_bytes >= abc_local_logpdf_f32_workspace_bytes(M, N),
-              "local_logpdf_f32: workspace too small");
-  int split;
-  int64_t nchunk;
-  local_plan(M, N, split, nchunk);
-  nchunk += nchunk & 1;  // even: particle pairs never straddle two chunks
-  const int64_t Np = N + (N & 1);
-  char* base = static_cast<char*>(ws);
-  double* logsumw = reinterpret_cast<double*>(base);
-  unsigned long long* lc_max_key = reinterpret_cast<unsigned long long*>(base + 8);
-  int* n_fix = reinterpret_cast<int*>(base + 16);
-  double* lc = reinterpret_cast<double*>(base + 64);
-  double* coef = lc + N;
-  double* part = coef + N * 36;
-  int* fix_rows = reinterpret_cast<int*>(part + static_cast<int64_t>(split) * M);
-  float* X32 = reinterpret_cast<float*>(
-      base + ((abc_local_logpdf_workspace_bytes(M, N) + 255) / 256) * 256);
-  float* X32lo = X32 + Np * 8;
-  float* coef32 = X32lo + Np * 8;
-  float* lc32 = coef32 + Np * 36;
-  float* pts32 = lc32 + Np;
-  float* pts32lo = pts32 + M * 8;
-  ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
-  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
-  hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
-                     st, w, dets, inv_covs, N, d, lc, coef, lc_max_key);
-  const unsigned grid = static_cast<unsigned>(ceil_div(M, 256) * split);
-  // rows whose fp32 sum is below 2^-60 take the exact fp64 fixup: the terms
-  // lost to fp32 underflow (< 2^-126 each) are then < 2^-40 of the sum
-  const double thresh = 8.673617379884035e-19;
-#define L(DD)                                                                    \
-  hipLaunchKernelGGL((local_pack32_kernel<DD>), dim3(ceil_div(Np, 256)), dim3(256), \
-                     0, st, X, coef, lc, lc_max_key, N, X32, X32lo, coef32,    \
-                     lc32);                                                      \
-  hipLaunchKernelGGL((local_pts32_kernel<DD>), dim3(ceil_div(M, 256)), dim3(256),  \
-                     0, st, pts, M, X, pts32, pts32lo);                          \
-  hipLaunchKernelGGL((local_pdf32_kernel<DD>), dim3(grid), dim3(256), 0, st,       \
-                     pts32, pts32lo, M, reinterpret_cast<const f32x2*>(X32),     \
-                     reinterpret_cast<const f32x2*>(X32lo),                      \
-                     reinterpret_cast<const f32x2*>(coef32),                     \
-                     reinterpret_cast<const f32x2*>(lc32), N, split, nchunk,     \
-                     part);                                                      \
-  hipLaunchKernelGGL(local_pdf_final_kernel, dim3(ceil_div(M, 256)), dim3(256),  \
-                     0, st, part, M, split, lc_max_key, logsumw, out_logpdf,     \
-                     n_fix, fix_rows, thresh);                                   \
-  hipLaunchKernelGGL((local_pdf_fixup_kernel<DD>), dim3(64), dim3(256), 0, st,   \
-                     pts, X, coef, lc, N, logsumw, n_fix, fix_rows, out_logpdf);
-  switch (d) {
-    case 1: L(1) break;
-    case 2: L(2) break;
-    case 3: L(3) break;
-    case 4: L(4) break;
-    case 5: L(5) break;
-    case 6: L(6) break;
-    case 7: L(7) break;
-    case 8: L(8) break;
-  }
-#undef L
-  ABC_LAUNCH_CHECK("local_logpdf_f32 kernels");
   return kOk;
 }
 

@@ -31,6 +31,8 @@ __host__ __device__ inline int morton_bits(int d) {
   return b < 21 ? b : 21;
 }
 
+namespace {  // kernels: internal linkage in every including unit
+
 // Quantisation frame: per dimension the extent of (x - X[0]) over the
 // population as ordered fp64 keys, min in [q], max in [8 + q].
 template <int D>
@@ -145,4 +147,70 @@ __device__ inline float box_dist2(const float (&x)[D], const float* __restrict__
   return s;
 }
 
+inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+// Workspace of the spatial index (spatial.hpp) over n points padded to
+// whole tiles: header (ext keys, counters) | keys_in[n] | keys_out[n] |
+// vals_in[n] | perm[T*64] | tbox[T][2][8] | sort temp.
+struct SpatialWs {
+  unsigned long long* ext;  // [16]: per-dim min keys, then max keys
+  int* count;
+  uint64_t* keys_in;
+  uint64_t* keys_out;
+  int32_t* vals_in;
+  int32_t* perm;
+  float* tbox;
+  void* temp;
+  size_t temp_bytes;
+  int T;
+};
+
+inline size_t spatial_ws_bytes(int64_t n) {
+  const int64_t T = ceil_div(n > 0 ? n : 1, kTile);
+  return 256 + 2 * al256(static_cast<size_t>(n) * 8) + al256(static_cast<size_t>(n) * 4) +
+         al256(static_cast<size_t>(T) * kTile * 4) + al256(static_cast<size_t>(T) * 2 * 8 * 4) +
+         al256(sort_pairs_temp_bytes(n));
+}
+
+inline SpatialWs spatial_ws(void* ws, int64_t n) {
+  SpatialWs v;
+  char* q = static_cast<char*>(ws);
+  v.T = static_cast<int>(ceil_div(n > 0 ? n : 1, kTile));
+  v.ext = reinterpret_cast<unsigned long long*>(q);
+  v.count = reinterpret_cast<int*>(q + 128);
+  q += 256;
+  v.keys_in = reinterpret_cast<uint64_t*>(q);
+  q += al256(static_cast<size_t>(n) * 8);
+  v.keys_out = reinterpret_cast<uint64_t*>(q);
+  q += al256(static_cast<size_t>(n) * 8);
+  v.vals_in = reinterpret_cast<int32_t*>(q);
+  q += al256(static_cast<size_t>(n) * 4);
+  v.perm = reinterpret_cast<int32_t*>(q);
+  q += al256(static_cast<size_t>(v.T) * kTile * 4);
+  v.tbox = reinterpret_cast<float*>(q);
+  q += al256(static_cast<size_t>(v.T) * 2 * 8 * 4);
+  v.temp = q;
+  v.temp_bytes = al256(sort_pairs_temp_bytes(n));
+  return v;
+}
+
+// Morton order of X (spatial.hpp): ext, keys, sort -> keys_out / perm (the
+// padding positions of the last tile map to particle 0).
+template <int D>
+int spatial_sort_population(const double* X, int64_t N, SpatialWs& v,
+                                   hipStream_t st) {
+  ABC_HIP(hipMemsetAsync(v.ext, 0xff, 64, st));
+  ABC_HIP(hipMemsetAsync(v.ext + 8, 0, 64 + 8, st));
+  hipLaunchKernelGGL((sp_extent_kernel<D>), dim3(stream_grid(N, 256, 64)), dim3(256),
+                     0, st, X, N, v.ext);
+  hipLaunchKernelGGL((sp_key_kernel<D>), dim3(ceil_div(N, 256)), dim3(256), 0, st,
+                     X, N, X, v.ext, v.keys_in, v.vals_in);
+  ABC_HIP(sort_pairs(v.temp, v.temp_bytes, v.keys_in, v.keys_out, v.vals_in, v.perm,
+                     N, morton_bits(D) * D, st));
+  const int64_t pad = static_cast<int64_t>(v.T) * kTile - N;
+  if (pad > 0) ABC_HIP(hipMemsetAsync(v.perm + N, 0, pad * 4, st));
+  return kOk;
+}
+
+
+}  // namespace
 }  // namespace abc

@@ -44,7 +44,9 @@ namespace abc {
 //      binade e_t and C + T_t <= 2^53 - 2, i.e. no element leaves the
 //      binade); any other tile runs the exact walk (exact_tile_wave: integer
 //      increments, wave scan, real fp64 add at the first tie / binade exit,
-//      re-grid, continue) -- ~1 slow tile per binade crossing
+//      re-grid, continue) -- ~1 slow tile per binade crossing; the first
+//      kHeadSeq elements (binade exits at ~1, 2, 4, ... elements) by one
+//      lane in numpy's own order (head_seq_wave)
 //   5. cdf_write       (tiles in parallel)  rebuilds every fast tile's
 //      elements from its exact start value C_t and the in-tile integer
 //      prefix, and divides by the last value (numpy's cdf /= cdf[-1])
@@ -188,6 +190,29 @@ __device__ void exact_tile_wave(const double* __restrict__ w, int64_t base,
   }
 }
 
+// The head of the array by ONE lane, numpy's loop c = fl(c + w_k) (c_0 =
+// w_0) over the tile staged in LDS: the first tile's chain doubles every
+// few elements (a binade exit at ~1, 2, 4, ... elements), where the wave walk
+// above pays a full pass per exit (~5 us each on the MI355X) and the lane
+// ~25 ns per element.  Raw values written to cdf; c out (wave-uniform).
+constexpr int kHeadSeq = 256;
+__device__ void head_seq_wave(const double* __restrict__ w, int head_n,
+                              double& c, double* __restrict__ cdf, double* buf) {
+  const int lane = threadIdx.x & 63;
+  for (int k = lane; k < head_n; k += 64) buf[k] = w[k];
+  __syncthreads();
+  if (lane == 0) {
+    double cc = buf[0];  // numpy: cdf[0] = w[0] (-0.0 stays -0.0)
+    for (int k = 1; k < head_n; ++k) {
+      cc = cc + buf[k];
+      buf[k] = cc;
+    }
+  }
+  __syncthreads();
+  c = buf[head_n - 1];
+  for (int k = lane; k < head_n; k += 64) cdf[k] = buf[k];
+}
+
 __global__ __launch_bounds__(kCdfThreads) void cdf_tile_sum_kernel(
     const double* __restrict__ w, int64_t n, double* __restrict__ tsum) {
   __shared__ double red[kCdfThreads / 64];
@@ -296,6 +321,7 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
     const int* __restrict__ e_t, const long long* __restrict__ T_t,
     long long* __restrict__ c_start, double* __restrict__ cdf,
     double* __restrict__ last) {
+  __shared__ double buf[kHeadSeq];
   const int lane = threadIdx.x;
   double c = 0.0;  // chain value (wave-uniform)
   for (int64_t t0 = 0; t0 < nt; t0 += kChainChunk) {
@@ -365,7 +391,13 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
         const int64_t t = t0 + i;
         const int64_t base = t * kCdfTile;
         const int tile_n = static_cast<int>(n - base < kCdfTile ? n - base : kCdfTile);
-        exact_tile_wave(w, base, tile_n, c, cdf);
+        if (t == 0) {  // tile 0 is always slow: its dense binade exits first
+          const int h = tile_n < kHeadSeq ? tile_n : kHeadSeq;
+          head_seq_wave(w, h, c, cdf, buf);
+          if (tile_n > h) exact_tile_wave(w, h, tile_n - h, c, cdf);
+        } else {
+          exact_tile_wave(w, base, tile_n, c, cdf);
+        }
         if (lane == 0) c_start[t] = -1;
         j = i + 1;
       }

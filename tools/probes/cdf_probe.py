@@ -13,8 +13,13 @@ from pyabc_amd import kernels as K  # noqa: E402
 torch.cuda.set_device(0)
 rng = np.random.default_rng(0)
 for n in [100_000, 1_000_000]:
-    for kind in ["uniform", "equal"]:
-        w = rng.uniform(0.5, 1.5, n) if kind == "uniform" else np.ones(n)
+    for kind in ["uniform", "equal", "lognormal1", "lognormal3"]:
+        if kind == "uniform":
+            w = rng.uniform(0.5, 1.5, n)
+        elif kind == "equal":
+            w = np.ones(n)
+        else:  # importance-weight-like spread
+            w = rng.lognormal(0.0, float(kind[-1]), n)
         w = torch.as_tensor(w / w.sum(), device="cuda")
         K.resample_cdf(w)
         torch.cuda.synchronize()

@@ -114,27 +114,28 @@ def pdf_norm_max_found(prev_pdf_norm, get_weighted_distances, **kwargs):
 
 
 class ScaledPDFNorm:
-    """pdf_norm_max_found, offset by log(factor) * next temperature once the
-    acceptance rate has fallen below ``min_acceptance_rate``
-    (pdf_norm.py:41-110; the reference ignores ``factor`` and uses 10)."""
+    """pdf_norm_max_found, lowered by log(factor) x (the next temperature)
+    from the first generation whose acceptance rate fell below
+    ``min_acceptance_rate`` on (pdf_norm.py:41-110).  As in the reference,
+    the factor is always 10 whatever is passed; the next temperature is
+    alpha x the previous one (1 before any)."""
 
     def __init__(self, factor=10, alpha=0.5, min_acceptance_rate=0.1):
         self.factor = 10
         self.alpha = alpha
         self.min_acceptance_rate = min_acceptance_rate
-        self._hit = False
+        self._hit = False  # sticky once the rate has dropped
 
     def __call__(self, prev_pdf_norm, get_weighted_distances, prev_temp,
                  acceptance_rate, **kwargs):
-        pdf_norm = pdf_norm_max_found(
-            prev_pdf_norm=prev_pdf_norm,
-            get_weighted_distances=get_weighted_distances)
-        offset = np.log(self.factor)
-        if acceptance_rate >= self.min_acceptance_rate and not self._hit:
-            return pdf_norm
-        self._hit = True
-        next_temp = 1 if prev_temp is None else self.alpha * prev_temp
-        return pdf_norm - offset * next_temp
+        base = pdf_norm_max_found(prev_pdf_norm=prev_pdf_norm,
+                                  get_weighted_distances=get_weighted_distances)
+        self._hit = self._hit or not (
+            acceptance_rate >= self.min_acceptance_rate)
+        if not self._hit:
+            return base
+        t_next = 1 if prev_temp is None else self.alpha * prev_temp
+        return base - np.log(self.factor) * t_next
 
 
 class StochasticAcceptor(Acceptor):
@@ -180,24 +181,24 @@ class StochasticAcceptor(Acceptor):
         return dict(pdf_norm=self.pdf_norms[t], kernel_scale=self.kernel_scale)
 
     def __call__(self, distance_function, eps, x, x_0, t, par):
+        """One proposal: the kernel value pd, acceptance probability
+        (pd / c)^(1/T) (linear scale) or exp((pd - c) / T) (log scale), one
+        U[0, 1) draw from numpy's global state, and the importance weight
+        p / min(1, p) (1 without importance weighting, 0 when p = 0)."""
         from .distance import SCALE_LIN
-        kernel = distance_function
-        temp = eps(t)
-        pd = kernel(x, x_0, t, par)
-        pdf_norm = self.pdf_norms[t]
-        if kernel.ret_scale == SCALE_LIN:
-            acc_prob = (pd / pdf_norm) ** (1 / temp)
+        inv_temp = 1 / eps(t)
+        pd = distance_function(x, x_0, t, par)
+        c = self.pdf_norms[t]
+        if distance_function.ret_scale == SCALE_LIN:
+            p = (pd / c) ** inv_temp
         else:
-            acc_prob = np.exp((pd - pdf_norm) * (1 / temp))
-        threshold = np.random.uniform(low=0, high=1)
-        accept = bool(acc_prob >= threshold)
-        if acc_prob == 0.0:
+            p = np.exp((pd - c) * inv_temp)
+        u = np.random.uniform(low=0, high=1)
+        if p == 0.0:
             weight = 0.0
-        elif self.apply_importance_weighting:
-            weight = acc_prob / min(1, acc_prob)
         else:
-            weight = 1.0
-        return AcceptorResult(pd, accept, weight)
+            weight = p / min(1, p) if self.apply_importance_weighting else 1.0
+        return AcceptorResult(pd, bool(p >= u), weight)
 
 
 def save_dict_to_json(dct, file_):

@@ -7,8 +7,6 @@ and density on the device: :meth:`Distribution.uniform_box` exposes a
 product of ``RV('uniform', loc, scale)`` marginals as (names, lo, scale)
 for the device kernels (prior support, random_variables.py:425-452).
 """
-from functools import reduce
-
 import numpy as np
 
 from .parameters import Parameter, ParameterStructure
@@ -90,74 +88,87 @@ class RV(RVBase):
         return f"<RV(name={self.name}, args={self.args} kwargs={self.kwargs})>"
 
 
+def _forward(method):
+    """A decorator method that hands the call to the wrapped component."""
+    def call(self, *args, **kwargs):
+        return getattr(self.component, method)(*args, **kwargs)
+    call.__name__ = method
+    return call
+
+
 class RVDecorator(RVBase):
+    """Wraps another RV; every method not overridden is the component's
+    (random_variables.py:185-229)."""
+
     def __init__(self, component):
         self.component = component
 
-    def rvs(self, *args, **kwargs):
-        return self.component.rvs(*args, **kwargs)
-
-    def pmf(self, x, *args, **kwargs):
-        return self.component.pmf(x, *args, **kwargs)
-
-    def pdf(self, x, *args, **kwargs):
-        return self.component.pdf(x, *args, **kwargs)
-
-    def cdf(self, x, *args, **kwargs):
-        return self.component.cdf(x, *args, **kwargs)
+    rvs = _forward("rvs")
+    pmf = _forward("pmf")
+    pdf = _forward("pdf")
+    cdf = _forward("cdf")
 
     def copy(self):
-        return self.__class__(self.component.copy())
+        return type(self)(self.component.copy())
 
     def decorator_repr(self):
         return "Decorator"
 
     def uniform_bounds(self):
-        return None
+        return None  # a decorated RV is never the plain uniform box
 
     def __repr__(self):
-        return f"[{self.decorator_repr()}]" + repr(self.component)
+        return "[" + self.decorator_repr() + "]" + repr(self.component)
 
 
 class LowerBoundDecorator(RVDecorator):
-    """Condition X > lower_bound by rejection (random_variables.py:232-305)."""
+    """The component conditioned on X > lower_bound
+    (random_variables.py:232-305): draws by rejection (None after
+    MAX_TRIES), densities renormalised by the mass above the bound."""
     MAX_TRIES = 10000
 
     def __init__(self, component, lower_bound):
-        if component.cdf(lower_bound) == 1:
+        below = component.cdf(lower_bound)
+        if below == 1:
             raise Exception(
                 "LowerBoundDecorator: Conditioning on a set of measure zero.")
         self.lower_bound = lower_bound
         super().__init__(component)
 
+    def _mass_below(self):
+        return self.component.cdf(self.lower_bound)
+
     def copy(self):
-        return self.__class__(self.component.copy(), self.lower_bound)
+        return type(self)(self.component.copy(), self.lower_bound)
 
     def decorator_repr(self):
-        return "Lower: X > {:2f}".format(self.lower_bound)
+        return f"Lower: X > {self.lower_bound:2f}"
 
     def rvs(self, *args, **kwargs):
-        for _ in range(self.MAX_TRIES):
-            s = self.component.rvs()
-            if not s <= self.lower_bound:
-                return s
+        tries = 0
+        while tries < self.MAX_TRIES:
+            draw = self.component.rvs()
+            if draw > self.lower_bound or draw != draw:  # NaN is not <= lb
+                return draw
+            tries += 1
         return None
 
-    def pdf(self, x, *args, **kwargs):
+    def _renormalised(self, density, x):
         if x <= self.lower_bound:
             return 0.
-        return self.component.pdf(x) / (1 - self.component.cdf(self.lower_bound))
+        return density(x) / (1 - self._mass_below())
+
+    def pdf(self, x, *args, **kwargs):
+        return self._renormalised(self.component.pdf, x)
 
     def pmf(self, x, *args, **kwargs):
-        if x <= self.lower_bound:
-            return 0.
-        return self.component.pmf(x) / (1 - self.component.cdf(self.lower_bound))
+        return self._renormalised(self.component.pmf, x)
 
     def cdf(self, x, *args, **kwargs):
         if x <= self.lower_bound:
             return 0.
-        lm = self.component.cdf(self.lower_bound)
-        return (self.component.cdf(x) - lm) / (1 - lm)
+        below = self._mass_below()
+        return (self.component.cdf(x) - below) / (1 - below)
 
 
 class Distribution(ParameterStructure):
@@ -184,19 +195,22 @@ class Distribution(ParameterStructure):
         return Parameter(**{k: v.rvs() for k, v in self.items()})
 
     def pdf(self, x):
-        if sorted(x.keys()) != sorted(self.keys()):
+        """Product of the marginal densities (pmf for discrete marginals)."""
+        expected, got = sorted(self.keys()), sorted(x.keys())
+        if got != expected:
             raise Exception("Random variable parameter mismatch. Expected: "
-                            + str(sorted(self.keys())) + " got "
-                            + str(sorted(x.keys())))
-        if len(self) == 0:
+                            + str(expected) + " got " + str(got))
+        if not self:
             return 1
-        res = []
-        for key, val in x.items():
+        value = None
+        for key, v in x.items():
+            rv = self[key]
             try:
-                res.append(self[key].pdf(val))
-            except AttributeError:
-                res.append(self[key].pmf(val))
-        return reduce(lambda s, t: s * t, res)
+                f = rv.pdf(v)
+            except AttributeError:  # discrete scipy marginals have no pdf
+                f = rv.pmf(v)
+            value = f if value is None else value * f
+        return value
 
     def uniform_box(self):
         """(sorted names, lo[d], scale[d]) if every marginal is uniform."""
@@ -213,34 +227,39 @@ class Distribution(ParameterStructure):
 
 
 class ModelPerturbationKernel:
-    """Model jump kernel (random_variables.py:455-538)."""
+    """Model jump kernel (random_variables.py:455-538): stay in model m with
+    probability p_stay, else move to one of the other models uniformly."""
 
     def __init__(self, nr_of_models, probability_to_stay=None):
         self.nr_of_models = nr_of_models
         if nr_of_models == 1:
-            self.probability_to_stay = 1
+            p = 1
         elif probability_to_stay is None:
-            self.probability_to_stay = 1 / nr_of_models
+            p = 1 / nr_of_models
         else:
-            self.probability_to_stay = min(max(probability_to_stay, 0), 1)
+            p = float(np.clip(probability_to_stay, 0, 1))
+        self.probability_to_stay = p
+
+    def _probabilities(self, m):
+        k = self.nr_of_models
+        probs = [(1 - self.probability_to_stay) / (k - 1)] * k
+        probs[m] = self.probability_to_stay
+        return probs
 
     def _get_discrete_rv(self, m):
-        p_stay = self.probability_to_stay
-        p_move = (1 - p_stay) / (self.nr_of_models - 1)
-        probs = [p_stay if n == m else p_move for n in range(self.nr_of_models)]
+        probs = self._probabilities(m)
         return RV("rv_discrete", values=(range(len(probs)), probs))
 
     def rvs(self, m):
-        if not 0 <= m <= self.nr_of_models - 1:
+        if m < 0 or m >= self.nr_of_models:
             raise Exception("m has to be between 0 and nr_of_models - 1")
         if self.nr_of_models == 1:
             return 0
         return self._get_discrete_rv(m).rvs()
 
     def pmf(self, n, m):
-        if not (0 <= n <= self.nr_of_models
-                and 0 <= m <= self.nr_of_models - 1):
+        if not (0 <= m < self.nr_of_models and 0 <= n <= self.nr_of_models):
             raise Exception("n and m have to be between 0 and nr_of_models - 1")
         if self.nr_of_models == 1:
-            return 1 if n == m else 0
+            return int(n == m)
         return self._get_discrete_rv(m).pmf(n)

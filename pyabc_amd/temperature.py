@@ -157,6 +157,14 @@ class Temperature(TemperatureBase):
         self._update(t, get_weighted_distances, get_all_records,
                      acceptance_rate, acceptor_config)
 
+    def _initial(self, **kwargs):
+        init = self.initial_temperature
+        if callable(init):
+            return init(**kwargs)
+        if isinstance(init, numbers.Number):
+            return init
+        raise ValueError("Initial temperature must be a float or a callable")
+
     def _update(self, t, get_weighted_distances, get_all_records,
                 acceptance_rate, acceptor_config):
         kwargs = dict(t=t, get_weighted_distances=get_weighted_distances,
@@ -164,30 +172,23 @@ class Temperature(TemperatureBase):
                       max_nr_populations=self.max_nr_populations,
                       pdf_norm=acceptor_config["pdf_norm"],
                       kernel_scale=acceptor_config["kernel_scale"],
-                      prev_temperature=self.temperatures.get(t - 1, None),
+                      prev_temperature=self.temperatures.get(t - 1),
                       acceptance_rate=acceptance_rate)
-        if t >= self.max_nr_populations - 1 \
-                and self.enforce_exact_final_temperature:
-            temps = [1.0]
-        elif not self.temperatures:
-            if callable(self.initial_temperature):
-                temps = [self.initial_temperature(**kwargs)]
-            elif isinstance(self.initial_temperature, numbers.Number):
-                temps = [self.initial_temperature]
-            else:
-                raise ValueError(
-                    "Initial temperature must be a float or a callable")
+        last = t >= self.max_nr_populations - 1
+        if last and self.enforce_exact_final_temperature:
+            proposals = [1.0]
+        elif self.temperatures:
+            proposals = [scheme(**kwargs) for scheme in self.schemes]
         else:
-            temps = [scheme(**kwargs) for scheme in self.schemes]
-        fallback = self.temperatures[t - 1] \
-            if t - 1 in self.temperatures else np.inf
-        temperature = self.aggregate_fun(temps)
-        temperature = max(min(temperature, fallback), 1.0)
-        if not np.isfinite(temperature):
+            proposals = [self._initial(**kwargs)]
+        # never above the previous temperature, never below 1
+        ceiling = self.temperatures.get(t - 1, np.inf)
+        value = max(min(self.aggregate_fun(proposals), ceiling), 1.0)
+        if not np.isfinite(value):
             raise ValueError("Temperature must be finite.")
-        self.temperatures[t] = temperature
-        logger.debug(f"Proposed temperatures for {t}: {temps}.")
-        self.temperature_proposals[t] = temps
+        self.temperatures[t] = value
+        self.temperature_proposals[t] = proposals
+        logger.debug(f"Proposed temperatures for {t}: {proposals}.")
         if self.log_file:
             save_dict_to_json(self.temperature_proposals, self.log_file)
 
@@ -286,13 +287,15 @@ class ExpDecayFixedRatioScheme(TemperatureScheme):
                  prev_temperature, acceptance_rate):
         if prev_temperature is None:
             return np.inf
-        alpha = self.alphas.get(t - 1, self.alpha)
-        if acceptance_rate > self.max_rate and t > 1:
-            alpha = max(alpha / 2, alpha - (1 - alpha) * 2)
+        a = self.alphas.get(t - 1, self.alpha)
+        if t > 1 and acceptance_rate > self.max_rate:
+            # accepting easily: cool faster (halve alpha, or more)
+            a = max(a / 2, a - 2 * (1 - a))
         if acceptance_rate < self.min_rate:
-            alpha = alpha + (1 - alpha) / 2
-        self.alphas[t] = alpha
-        return self.alphas[t] * prev_temperature
+            # barely accepting: move alpha half-way towards 1
+            a = a + (1 - a) / 2
+        self.alphas[t] = a
+        return a * prev_temperature
 
 
 class PolynomialDecayFixedIterScheme(TemperatureScheme):
@@ -332,15 +335,14 @@ class DalyScheme(TemperatureScheme):
                  prev_temperature, acceptance_rate):
         if prev_temperature is None:
             return np.inf
-        eps_base = np.sqrt(prev_temperature)
+        root = np.sqrt(prev_temperature)
+        step = self.k[t - 1] if self.k else root
         if not self.k:
-            self.k[t - 1] = eps_base
-        k_base = self.k[t - 1]
+            self.k[t - 1] = root
         if acceptance_rate < self.min_rate:
-            k_base = self.alpha * k_base
-        self.k[t] = min(k_base, self.alpha * eps_base)
-        eps = eps_base - self.k[t]
-        return eps ** 2
+            step = self.alpha * step
+        self.k[t] = min(step, self.alpha * root)
+        return (root - self.k[t]) ** 2
 
 
 class FrielPettittScheme(TemperatureScheme):
@@ -355,9 +357,9 @@ class FrielPettittScheme(TemperatureScheme):
         if max_nr_populations == np.inf:
             raise ValueError("Can only perform FrielPettittScheme step with a "
                              "finite max_nr_populations.")
-        beta_base = 1. / prev_temperature
-        t_to_go = max_nr_populations - t
-        beta = beta_base + ((1. - beta_base) * 1 / t_to_go) ** 2
+        beta = 1. / prev_temperature
+        remaining = max_nr_populations - t
+        beta = beta + ((1. - beta) / remaining) ** 2
         return 1. / beta
 
 

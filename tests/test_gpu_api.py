@@ -558,6 +558,13 @@ def test_singlecore_parity_same_draws(pa):
                                    g["rec_stats"], rtol=0, atol=1e-5)
         np.testing.assert_array_equal(res.rec_acc.cpu().numpy() > 0,
                                       g["rec_acc"])
+        # the accept bits agree by construction, not by luck: every recorded
+        # distance lies more than 100x the distance tolerance above away from
+        # eps, so no fp32-noise difference within it can flip a decision
+        # (the fixture places eps in a gap of the distances)
+        rd = res.rec_d.cpu().numpy()
+        margin = np.min(np.abs(rd - float(g["eps"]))) / float(g["eps"])
+        assert margin > 100 * 1e-5, margin
     for me, ok, nr in zip(g["cut_max_eval"], g["cut_ok"],
                           g["cut_nr_evaluations"]):
         eng = GenerationEngine(model, g["lo"], g["sc"], seed=int(g["seed"]),

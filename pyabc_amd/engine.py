@@ -204,19 +204,34 @@ def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps,
     return n
 
 
-def decide(acceptance, stats, nv, seed, stream, eval_off):
+def _read_counts(acount, gcount, apos, nv, need):
+    """[accepted, guard band, apos[need - 1]] in one host read; the last
+    is the position of the round's need-th acceptance (valid only when
+    accepted >= need) -- the selection's closing position without a read of
+    its own."""
+    parts = [acount.view(1), gcount.view(1)]
+    if need is not None and nv:
+        parts.append(apos[min(need, nv) - 1:min(need, nv)])
+    vals = torch.cat(parts).cpu().tolist()
+    last = vals[2] if len(vals) > 2 and vals[0] >= need else None
+    return int(vals[0]), int(vals[1]), last
+
+
+def decide(acceptance, stats, nv, seed, stream, eval_off, need=None):
     """One round's acceptance with ONE host read: distances / flags, the
-    order-preserving positions of the accepted columns, and the accepted
-    and guard-band counts as host ints -> (d, acc, guard, accw, apos,
-    n_acc, n_guard)."""
+    order-preserving positions of the accepted columns, the accepted and
+    guard-band counts as host ints and, given ``need``, the position of
+    the need-th acceptance if the round reached it -> (d, acc, guard, accw,
+    apos, n_acc, n_guard, apos_need)."""
     if hasattr(acceptance, "decide"):
-        return acceptance.decide(stats, nv, seed, stream, eval_off)
+        return acceptance.decide(stats, nv, seed, stream, eval_off,
+                                 need=need)
     d, acc, guard, accw = acceptance(stats, nv, seed, stream, eval_off)
     apos, acount = K.compact(acc)
     g = guard[:nv].sum(dtype=torch.int64).view(1) if guard is not None \
         else torch.zeros(1, dtype=torch.int64, device=acount.device)
-    n_acc, n_guard = torch.cat([acount.view(1), g]).cpu().tolist()
-    return d, acc, guard, accw, apos, int(n_acc), int(n_guard)
+    n_acc, n_guard, last = _read_counts(acount, g, apos, nv, need)
+    return d, acc, guard, accw, apos, n_acc, n_guard, last
 
 
 class PNormAcceptance:
@@ -242,7 +257,8 @@ class PNormAcceptance:
             stats, nv, d, acc, guard, x0h, fwh, self.p, self.eps)
         return d, acc, guard, None
 
-    def decide(self, stats, nv, seed, stream, eval_off, fused=None):
+    def decide(self, stats, nv, seed, stream, eval_off, fused=None,
+               need=None):
         """:func:`decide` for the p-norm: the accepted and the guard-band
         columns are compacted together and their counts read in one host
         sync; the (rare) band is then re-decided and the accepted columns
@@ -258,8 +274,7 @@ class PNormAcceptance:
             d, acc, guard, simulate = fused
         gpos, gcount = K.compact(guard[:nv])
         apos, acount = K.compact(acc)
-        n_acc, n_guard = torch.cat([acount.view(1), gcount.view(1)]).cpu(
-        ).tolist()
+        n_acc, n_guard, last = _read_counts(acount, gcount, apos, nv, need)
         if n_guard:
             if stats is None:
                 stats = simulate()
@@ -268,7 +283,8 @@ class PNormAcceptance:
                 band=(gpos, int(n_guard)))
             apos, acount = K.compact(acc)
             n_acc = acount.item()
-        return d, acc, guard, None, apos, int(n_acc), int(n_guard)
+            last = None  # the band's flags moved the positions
+        return d, acc, guard, None, apos, int(n_acc), int(n_guard), last
 
 
 class StochasticAcceptance:
@@ -450,6 +466,10 @@ class GenerationEngine:
             else:
                 stats = None
             accw = acc = None
+            alast = None
+            # one rank: this round's take is `need` if it closes the
+            # generation, so decide's read also brings the closing position
+            need1 = need if R == 1 else None
             if acceptance is None:
                 # calibration sample: everything accepted, distances later
                 # (smc.py:486-514: accepted_distances = [inf])
@@ -462,15 +482,16 @@ class GenerationEngine:
                 fd = self.model.simulate_distance(
                     theta, self.seed, sim_sid, my_eval, a.x0, a.fw, a.p, a.eps)
                 th_, me_ = theta, my_eval
-                d, acc, guard, accw, apos, acount, gcount = a.decide(
+                d, acc, guard, accw, apos, acount, gcount, alast = a.decide(
                     None, nv, self.seed, self._stream(t, stream_base + 4),
                     my_eval, fused=fd + (lambda: self.model.simulate(
-                        th_, self.seed, sim_sid, me_),))            # sync 2
+                        th_, self.seed, sim_sid, me_),), need=need1)  # sync 2
                 nas = comm.all_gather_ints(acount)
             elif nv:
-                d, acc, guard, accw, apos, acount, gcount = decide(
+                d, acc, guard, accw, apos, acount, gcount, alast = decide(
                     acceptance, stats, nv, self.seed,
-                    self._stream(t, stream_base + 4), my_eval)      # sync 2
+                    self._stream(t, stream_base + 4), my_eval,
+                    need=need1)                                     # sync 2
                 nas = comm.all_gather_ints(acount)
             else:
                 d = guard = apos = None
@@ -479,7 +500,8 @@ class GenerationEngine:
                 gcount = 0
             rounds.append(dict(theta=theta, stats=stats, d=d, apos=apos,
                                guard=guard, accw=accw, acc=acc, nvs=nvs,
-                               nas=nas, acc0=n_acc, gcount=gcount))
+                               nas=nas, acc0=n_acc, gcount=gcount,
+                               need=need1, alast=alast))
             raw_off += R * B
             eval_off += sum(nvs)
             n_acc += sum(nas)
@@ -507,7 +529,10 @@ class GenerationEngine:
         for rd, take, cl in zip(rounds, takes, closing):
             k = take[r]
             if cl[r] == 1:          # this rank holds the n-th acceptance
-                last = int(rd["apos"][k - 1].item()) + 1
+                if rd["alast"] is not None and k == rd["need"]:
+                    last = int(rd["alast"]) + 1     # read with the counts
+                else:
+                    last = int(rd["apos"][k - 1].item()) + 1
             elif cl[r] == 0:        # before it: every evaluation counts
                 last = rd["nvs"][r]
             else:                   # after it

@@ -440,11 +440,19 @@ def test_pnorm_decide_one_read(K):
     a = PNormAcceptance(x0, fw, 2, eps)
     d1, acc1, g1, _ = a(stats, B, 0, 0, 0)
     pos1, c1 = K.compact(acc1)
-    d2, acc2, g2, _, pos2, n2, ng2 = a.decide(stats, B, 0, 0, 0)
+    need = 5000
+    d2, acc2, g2, _, pos2, n2, ng2, last = a.decide(stats, B, 0, 0, 0,
+                                                    need=need)
     np.testing.assert_array_equal(host(d1), host(d2))
     np.testing.assert_array_equal(host(acc1), host(acc2))
     assert n2 == int(host(c1)[0]) and ng2 == int(host(g2).sum())
     np.testing.assert_array_equal(host(pos1)[:n2], host(pos2)[:n2])
+    # the closing position read with the counts: the need-th acceptance
+    # (None when the band moved positions or the round fell short)
+    if ng2 == 0:
+        assert last == int(host(pos1)[need - 1])
+    *_, short = a.decide(stats, B, 0, 0, 0, need=n2 + 1)
+    assert short is None
 
 
 @pytest.mark.parametrize("p", [2, 3])

@@ -48,6 +48,22 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr double kLwFloor = -160.0;  // 2^-160 is 0 in fp32: no term changes
 constexpr int kWaves = 4;            // waves per block
 
+// Block -> (j-segment set s, row block rb).  split > 0: row-block major
+// (the split blocks of one row block adjacent); split < 0: segment major
+// (|split| sets, the row blocks of one set adjacent) -- the blocks resident
+// together on an XCD then stream the same A segments, so its L2 serves
+// them.  A row's arithmetic is the same either way.
+__device__ inline void block_coords(int split, int& s, int64_t& rb) {
+  if (split > 0) {
+    s = static_cast<int>(blockIdx.x % split);
+    rb = blockIdx.x / split;
+  } else {
+    const int64_t nrb = gridDim.x / (-split);
+    s = static_cast<int>(blockIdx.x / nrb);
+    rb = blockIdx.x % nrb;
+  }
+}
+
 template <int D>
 struct Mk {
   static constexpr int KH = (D + 6 + 15) / 16;      // y1.y1, aH x3, bH x3
@@ -362,8 +378,10 @@ __device__ __forceinline__ void kde_mfma_body(
   constexpr int KT = KH + KL;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
+  int s;
+  int64_t rb;
+  block_coords(split, s, rb);
+  split = split < 0 ? -split : split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
 
   bf16x8 bq[IB][KT];
@@ -473,8 +491,10 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
   const int lane = threadIdx.x & 63;
   // wave-uniform: the LDS-DMA fill loop and its M0 address stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
+  int s;
+  int64_t rb;
+  block_coords(split, s, rb);
+  split = split < 0 ? -split : split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
 
   bf16x8 bq[IB][KT];
@@ -683,8 +703,10 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
   const int lane = threadIdx.x & 63;
   // wave-uniform: the LDS-DMA fill loop and its M0 address stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
+  int s;
+  int64_t rb;
+  block_coords(split, s, rb);
+  split = split < 0 ? -split : split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
 
   bf16x8 bq[IB][KT];
@@ -812,8 +834,10 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int s = blockIdx.x % split;
-  const int64_t rb = blockIdx.x / split;
+  int s;
+  int64_t rb;
+  block_coords(split, s, rb);
+  split = split < 0 ? -split : split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
 
   bf16x8 bq[IB][KT];
@@ -914,10 +938,11 @@ int kt_for(int d) {
 struct MPlan {
   int split, nseg, spb, jseg;
   int64_t row_blocks;
+  bool smajor;  // segment-major block order (block_coords)
 };
 
 template <int D>
-MPlan make_mplan(int64_t M, int64_t npad, int ib) {
+MPlan make_mplan(int64_t M, int64_t npad, int ib, bool smajor) {
   // many short blocks: at N = M = 1e6 split 1 -> 32 is 181 -> 163 ms
   // (tools/bench_kde.py msplit); split % 8 == 0 pins each j-segment set to
   // one XCD's L2 (blocks go round-robin over the 8 XCDs)
@@ -926,8 +951,16 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib) {
   p.nseg = kde_num_segments(npad);
   p.jseg = static_cast<int>(ceil_div(ceil_div(npad, p.nseg), 64) * 64);
   p.row_blocks = mpad_rows<D>(M) / (32 * kWaves * ib);
+  // segment major: one segment per block, so the blocks an XCD runs
+  // together share one segment of A in its L2 (fetch per launch at N = M =
+  // 1e6, d = 8: 80 GB row-block major, 25.8 GB segment major with 4
+  // segments per block, 14.5 GB with 1; time 131.1 -> 130.3 ms)
+  p.smajor = smajor;
   int split = 1;
-  while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
+  if (smajor)
+    split = p.nseg;
+  else
+    while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
   if (const char* env = getenv("ABC_KDE_MFMA_SPLIT")) {  // tuning override
     const int v = atoi(env);
     if (v >= 1 && v <= p.nseg && (p.nseg % v) == 0) split = v;
@@ -943,7 +976,8 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib) {
 // ABC_KDE_MFMA_IB (i-tiles per wave), ABC_KDE_MFMA_PIPE (software
 // pipelining of the register kernel), ABC_KDE_MFMA_LDS2 (d > 8 -- 0: the
 // register kernel, 1: LDS-DMA A fragments, 2: the same hand-interleaved;
-// d <= 8 -- 0: the register kernel, 1: the folded LDS-DMA pass).
+// d <= 8 -- 0: the register kernel, 1: the folded LDS-DMA pass),
+// ABC_KDE_MFMA_SMAJOR (1: segment-major block order, one segment per block).
 int env_int(const char* name, int dflt) {
   const char* env = getenv(name);
   return env ? atoi(env) : dflt;
@@ -955,6 +989,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
                  hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
   const dim3 block(64 * kWaves);
+  const int split = p.smajor ? -p.split : p.split;
   if constexpr (D > 8) {
     // 2: hand-interleaved split pass; 1: LDS-DMA A fragments, compiler
     // schedule (d = 20: 21.5 -> 20.4 ms at N = M = 262144 against the
@@ -962,13 +997,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
     if (lds2 == 2) {
       hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
     }
     if (lds2 != 0) {
       hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
     }
@@ -978,7 +1013,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // (kde_mfma_lds2g_kernel); rows bit-identical
     if (lds2g) {
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
-                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
     }
@@ -987,11 +1022,11 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   // chain dominates and the lower register count wins (bench_kde sweep)
   if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
-                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
   else
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
-                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, p.split,
+                       dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
 }
 
@@ -1015,7 +1050,11 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   int ib = lds2g ? IB2 : IBF;
   const int v = env_int("ABC_KDE_MFMA_IB", ib);
   if (v == IBF || v == IBH || v == IB2) ib = v;
-  const MPlan p = make_mplan<D>(M, npad, ib);
+  // segment-major block order on large populations (the A fragments no
+  // longer fit the L2s; ABC_KDE_MFMA_SMAJOR overrides, rows bit-identical)
+  const bool smajor =
+      env_int("ABC_KDE_MFMA_SMAJOR", npad >= (int64_t{1} << 18) ? 1 : 0) != 0;
+  const MPlan p = make_mplan<D>(M, npad, ib, smajor);
   const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;
   ABC_REQUIRE(ws_bytes >= need, "kde_mfma: workspace too small (%zu < %zu)",

@@ -17,7 +17,7 @@ from pyabc_amd import kernels as K  # noqa: E402
 from oracle import ref_cpu as ref  # noqa: E402
 
 KEYS = ("ABC_KDE_MFMA_IB", "ABC_KDE_MFMA_PIPE", "ABC_KDE_MFMA_SPLIT",
-        "ABC_KDE_MFMA_LDS2", "ABC_KDE_MFMA_FOLD")
+        "ABC_KDE_MFMA_LDS2", "ABC_KDE_MFMA_FOLD", "ABC_KDE_MFMA_SMAJOR")
 
 SWEEP = [
     ("default", {}),

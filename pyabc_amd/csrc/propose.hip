@@ -73,20 +73,62 @@ __device__ inline long long wave_incl_scan(long long v) {
   return v;
 }
 
-__device__ inline int wave_min_int(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+// Cross-lane steps of the single-wave walks on DPP (row shifts within the
+// 16-lane rows, then the row-15 / lane-31 broadcasts): a VALU operand
+// modifier per step instead of a ds_bpermute round trip through LDS -- the
+// walks are latency-bound, one wave on the chip.
+template <int CTRL, int ROWS = 0xf>
+__device__ inline double dpp_f64_zero(double v) {  // out-of-row lanes read 0
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS,
+                                             0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS,
+                                             0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
+// inclusive prefix sum over the 64 lanes (adds of +0.0 elsewhere: the
+// values summed here are non-negative integers held in fp64)
+__device__ inline double wave_incl_scan_f64(double v) {
+  v += dpp_f64_zero<0x111>(v);       // row_shr:1
+  v += dpp_f64_zero<0x112>(v);       // row_shr:2
+  v += dpp_f64_zero<0x114>(v);       // row_shr:4
+  v += dpp_f64_zero<0x118>(v);       // row_shr:8
+  v += dpp_f64_zero<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f64_zero<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
-__device__ inline double wave_incl_scan_f64(double v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-  return v;
+__device__ inline double wave_shr1_f64(double v) {  // lane l gets l - 1; 0 at 0
+  return dpp_f64_zero<0x138>(v);                    // wave_shr:1
+}
+
+__device__ inline long long readlane_i64(long long v, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane(static_cast<int>(v), l);
+  const unsigned hi = __builtin_amdgcn_readlane(static_cast<int>(v >> 32), l);
+  return static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+
+__device__ inline double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL, int ROWS = 0xf>
+__device__ inline int dpp_min_step(int v) {  // disabled lanes keep INT_MAX
+  return min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, CTRL, ROWS, 0xf,
+                                            false));
+}
+
+// minimum over the 64 lanes, wave-uniform (an SGPR)
+__device__ inline int wave_min_int(int v) {
+  v = dpp_min_step<0x111>(v);
+  v = dpp_min_step<0x112>(v);
+  v = dpp_min_step<0x114>(v);
+  v = dpp_min_step<0x118>(v);
+  v = dpp_min_step<0x142, 0xa>(v);
+  v = dpp_min_step<0x143, 0xc>(v);
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
 // The exact chain over w[base, base + tile_n) by ONE wave (no barriers):
@@ -144,8 +186,7 @@ __device__ void exact_tile_wave(const double* __restrict__ w, int64_t base,
     const double incl = wave_incl_scan_f64(tsum);
     // exclusive prefix = the previous lane's inclusive one (NOT incl - tsum:
     // a lane past the break may hold a sum above 2^53, inexact in fp64)
-    double excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = 0.0;
+    const double excl = wave_shr1_f64(incl);
     // binade exit: C + prefix must stay below 2^53 (one unit margin)
     const double Cx = C + excl;
 #pragma unroll
@@ -180,10 +221,10 @@ __device__ void exact_tile_wave(const double* __restrict__ w, int64_t base,
         cb = (base + b == 0) ? wb : prev + wb;
         cdf[base + b] = cb;
       }
-      c = __shfl(cb, owner, 64);
+      c = readlane_f64(cb, owner);
       s = b + 1;
     } else {
-      const double total = __shfl(incl, 63, 64);
+      const double total = readlane_f64(incl, 63);
       if (exact_mode) c = ldexp(C + total, e - 52);
       s = tile_n;
     }
@@ -353,8 +394,8 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
           e_i = re[q];
           P_i = rP[q];
         }
-      e_i = __shfl(e_i, owner, 64);
-      P_i = __shfl(P_i, owner, 64);
+      e_i = __builtin_amdgcn_readlane(e_i, owner);
+      P_i = readlane_i64(P_i, owner);
       int j = i;
       if (e_i != kCdfSlow) {
         const double lo = ldexp(1.0, e_i);
@@ -382,7 +423,7 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
 #pragma unroll
             for (int q = 0; q < kChainPer; ++q)
               if (q == qj) Pj = rP[q] + rT[q];
-            Pj = __shfl(Pj, oj, 64);
+            Pj = readlane_i64(Pj, oj);
             c = ldexp(static_cast<double>(Ci + (Pj - P_i)), e_i - 52);
           }
         }

@@ -354,50 +354,81 @@ __global__ __launch_bounds__(64) void knn_kernel(
 }
 
 // ---------------------------------------------------------------------------
-template <int D>
+// LU with partial pivoting (the reference's np.linalg.det / inv on the
+// host is LAPACK's getrf order); EXACT = (d == D): every loop bound is a
+// compile-time constant, so the d x d arrays stay in registers (the
+// runtime-d form keeps them in scratch).
+template <int D, bool EXACT>
 __device__ inline double lu_det_inv(double (&a)[D][D], double (&inv)[D][D],
-                                    int d, bool want_inv) {
+                                    int d_arg, bool want_inv) {
+  const int d = EXACT ? D : d_arg;
   int piv[D];
   double det = 1.0;
+#pragma unroll
   for (int i = 0; i < d; ++i) piv[i] = i;
+#pragma unroll
   for (int c = 0; c < d; ++c) {
     int p = c;
     double best = fabs(a[c][c]);
+#pragma unroll
     for (int r = c + 1; r < d; ++r)
       if (fabs(a[r][c]) > best) {
         best = fabs(a[r][c]);
         p = r;
       }
     if (p != c) {
-      for (int q = 0; q < d; ++q) {
-        const double t = a[c][q];
-        a[c][q] = a[p][q];
-        a[p][q] = t;
+      if constexpr (EXACT) {  // the same swap with static indices
+#pragma unroll
+        for (int r = c + 1; r < D; ++r)
+          if (r == p) {
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+              const double t = a[c][q];
+              a[c][q] = a[r][q];
+              a[r][q] = t;
+            }
+            const int t = piv[c];
+            piv[c] = piv[r];
+            piv[r] = t;
+          }
+      } else {
+        for (int q = 0; q < d; ++q) {
+          const double t = a[c][q];
+          a[c][q] = a[p][q];
+          a[p][q] = t;
+        }
+        const int t = piv[c];
+        piv[c] = piv[p];
+        piv[p] = t;
       }
-      const int t = piv[c];
-      piv[c] = piv[p];
-      piv[p] = t;
       det = -det;
     }
     const double diag = a[c][c];
     det *= diag;
     if (diag == 0.0) continue;
+#pragma unroll
     for (int r = c + 1; r < d; ++r) {
       const double f = a[r][c] / diag;
       a[r][c] = f;
+#pragma unroll
       for (int q = c + 1; q < d; ++q) a[r][q] = fma(-f, a[c][q], a[r][q]);
     }
   }
   if (want_inv) {
+#pragma unroll
     for (int col = 0; col < d; ++col) {
       double y[D];
+#pragma unroll
       for (int i = 0; i < d; ++i) {
         double s = piv[i] == col ? 1.0 : 0.0;
+#pragma unroll
         for (int q = 0; q < i; ++q) s = fma(-a[i][q], y[q], s);
         y[i] = s;
       }
+#pragma unroll
       for (int i = d - 1; i >= 0; --i) {
         double s = y[i];
+#pragma unroll
         for (int q = i + 1; q < d; ++q) s = fma(-a[i][q], inv[q][col], s);
         inv[i][col] = s / a[i][i];
       }
@@ -406,12 +437,13 @@ __device__ inline double lu_det_inv(double (&a)[D][D], double (&inv)[D][D],
   return det;
 }
 
-template <int D>
+template <int D, bool EXACT>
 __global__ __launch_bounds__(128) void local_cov_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
-    int d, const int32_t* __restrict__ nbr, int k, double scaling,
+    int d_arg, const int32_t* __restrict__ nbr, int k, double scaling,
     int64_t rlo, int64_t rhi, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets) {
+  const int d = EXACT ? D : d_arg;
   // particles [rlo, rhi); nbr and the outputs are indexed from rlo
   const int64_t n = rlo + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (n >= rhi) return;
@@ -420,64 +452,90 @@ __global__ __launch_bounds__(128) void local_cov_kernel(
   invs -= rlo * d * d;
   dets -= rlo;
   double xn[D];
+#pragma unroll
   for (int q = 0; q < d; ++q) xn[q] = X[n * d + q];
   // local weights lw = w[nbr] / sum
   double sw = 0.0;
   for (int t = 0; t < k; ++t) sw += w[nbr[n * k + t]];
   double v1 = 0.0, v2 = 0.0, mu[D];
+#pragma unroll
   for (int q = 0; q < d; ++q) mu[q] = 0.0;
   for (int t = 0; t < k; ++t) {
     const int64_t j = nbr[n * k + t];
     const double lw = w[j] / sw;
     v1 += lw;
     v2 += lw * lw;
+#pragma unroll
     for (int q = 0; q < d; ++q) mu[q] = fma(lw, X[j * d + q] - xn[q], mu[q]);
   }
+#pragma unroll
   for (int q = 0; q < d; ++q) mu[q] /= v1;
   double C[D][D];
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = 0; b < d; ++b) C[a][b] = 0.0;
   for (int t = 0; t < k; ++t) {
     const int64_t j = nbr[n * k + t];
     const double lw = w[j] / sw;
     double dl[D];
+#pragma unroll
     for (int q = 0; q < d; ++q) dl[q] = (X[j * d + q] - xn[q]) - mu[q];
+#pragma unroll
     for (int a = 0; a < d; ++a)
+#pragma unroll
       for (int b = a; b < d; ++b) C[a][b] = fma(lw * dl[a], dl[b], C[a][b]);
   }
   double fact = v1 - v2 / v1;
   if (fact <= 0.0) fact = 0.0;
   double csum = 0.0;
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = a; b < d; ++b) {
       C[a][b] = C[a][b] * (1.0 / fact);
       C[b][a] = C[a][b];
     }
   if (k == 1) {  // smart_cov of ONE delta row: diag(|delta_0|) (util.py:8-11)
     const int64_t j = nbr[n * k];
+#pragma unroll
     for (int a = 0; a < d; ++a)
+#pragma unroll
       for (int b = 0; b < d; ++b)
         C[a][b] = a == b ? fabs(X[j * d + a] - xn[a]) : 0.0;
   }
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = 0; b < d; ++b) csum += C[a][b];
-  if (fabs(csum) == 0.0)
+  if (fabs(csum) == 0.0) {
+#pragma unroll
     for (int q = 0; q < d; ++q) C[q][q] = fabs(X[q]);
+  }
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = 0; b < d; ++b) C[a][b] *= scaling;
   double work[D][D], inv[D][D];
   double det;
   for (int it = 0; it < 100000; ++it) {
+#pragma unroll
     for (int a = 0; a < d; ++a)
+#pragma unroll
       for (int b = 0; b < d; ++b) work[a][b] = C[a][b];
-    det = lu_det_inv<D>(work, inv, d, false);
+    det = lu_det_inv<D, EXACT>(work, inv, d, false);
     if (!(det <= 0.0)) break;  // reference: while det <= 0 (NaN exits)
+#pragma unroll
     for (int q = 0; q < d; ++q) C[q][q] += 1e-3;
   }
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = 0; b < d; ++b) work[a][b] = C[a][b];
-  lu_det_inv<D>(work, inv, d, true);
+  lu_det_inv<D, EXACT>(work, inv, d, true);
+#pragma unroll
   for (int a = 0; a < d; ++a)
+#pragma unroll
     for (int b = 0; b < d; ++b) {
       covs[n * d * d + a * d + b] = C[a][b];
       invs[n * d * d + a * d + b] = inv[a][b];
@@ -705,18 +763,27 @@ int abc_local_cov_rows_f64(const double* X, const double* w, int64_t N, int d,
   if (nrows == 0) return kOk;
   const unsigned g = static_cast<unsigned>(ceil_div(nrows, 128));
   const int64_t rlo = row0, rhi = row0 + nrows;
-#define L(DD)                                                                   \
-  hipLaunchKernelGGL((local_cov_kernel<DD>), dim3(g), dim3(128), 0, st, X, w, N, \
-                     d, nbr, k, scaling, rlo, rhi, covs, inv_covs, dets);
-  if (d <= 4) {
-    L(4)
-  } else if (d <= 8) {
-    L(8)
-  } else if (d <= 16) {
-    L(16)
-  } else {
-    set_error("local_cov: unsupported d=%d (d <= 16)", d);
-    return kUnsupported;
+#define L(DD, EX)                                                                \
+  hipLaunchKernelGGL((local_cov_kernel<DD, EX>), dim3(g), dim3(128), 0, st, X, w, \
+                     N, d, nbr, k, scaling, rlo, rhi, covs, inv_covs, dets);
+  // d <= 6: one instantiation per d (register-resident d x d arrays; at
+  // d = 7, 8 those need 262 / 360 VGPRs and the compile time explodes)
+  switch (d) {
+    case 1: L(1, true) break;
+    case 2: L(2, true) break;
+    case 3: L(3, true) break;
+    case 4: L(4, true) break;
+    case 5: L(5, true) break;
+    case 6: L(6, true) break;
+    default:
+      if (d <= 8) {
+        L(8, false)
+      } else if (d <= 16) {
+        L(16, false)
+      } else {
+        set_error("local_cov: unsupported d=%d (d <= 16)", d);
+        return kUnsupported;
+      }
   }
 #undef L
   ABC_LAUNCH_CHECK("local_cov_kernel");

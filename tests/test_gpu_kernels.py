@@ -656,6 +656,28 @@ def test_local_transition(K, name):
     np.testing.assert_allclose(np.exp(host(lp)), g["pdf"], rtol=1e-11)
 
 
+@pytest.mark.parametrize("d", [1, 4, 5, 7, 9])
+def test_local_cov_all_dims_vs_oracle(K, d):
+    """local_cov_kernel's per-d register form (d <= 6) and its runtime-d
+    form (d = 7..16) against the oracle's smart_cov / det / inv restatement
+    (local_transition.py:77-101) on dimensions the goldens do not cover."""
+    rng = np.random.default_rng(40 + d)
+    N, k = 700, 25
+    X = rng.normal(size=(N, d)) * rng.uniform(0.5, 2.0, d)
+    w = rng.uniform(0.5, 1.5, N)
+    w /= w.sum()
+    # neighbour rows by numpy (the device kNN stops at d = 8); both sides
+    # sum over the same rows in the same order
+    d2 = ((X[:, None, :] - X[None, :, :]) ** 2).sum(-1)
+    nb = np.argsort(d2, axis=1, kind="stable")[:, :k].astype(np.int32)
+    nbr = torch.as_tensor(nb, device="cuda")
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    rc, ri, rd = ref.local_covs(X, w, nb)
+    np.testing.assert_allclose(host(covs), rc, rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(host(dets), rd, rtol=1e-11)
+    np.testing.assert_allclose(host(invs), ri, rtol=1e-9, atol=1e-12)
+
+
 # ------------------------------------------------------ simulators
 def test_sim_linear_gaussian(K):
     rng = np.random.default_rng(1)

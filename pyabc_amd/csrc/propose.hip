@@ -231,27 +231,45 @@ __device__ void exact_tile_wave(const double* __restrict__ w, int64_t base,
   }
 }
 
-// The head of the array by ONE lane, numpy's loop c = fl(c + w_k) (c_0 =
-// w_0) over the tile staged in LDS: the first tile's chain doubles every
-// few elements (a binade exit at ~1, 2, 4, ... elements), where the wave walk
-// above pays a full pass per exit (~5 us each on the MI355X) and the lane
-// ~25 ns per element.  Raw values written to cdf; c out (wave-uniform).
+// The head of the array in numpy's own order, c = fl(c + w_k) (c_0 = w_0):
+// the first tile's chain doubles every few elements (a binade exit at ~1,
+// 2, 4, ... elements), where the wave walk above pays a full pass per exit
+// (~2.7 us each on the MI355X).  Each lane holds 4 consecutive weights; the
+// add chain takes them lane by lane through readlane (an SGPR operand), so
+// the only dependency per element is the fp64 add itself, and lane l
+// catches its own partial sums as they pass.  Raw values written to cdf;
+// c out (wave-uniform).
 constexpr int kHeadSeq = 256;
+constexpr int kHeadPer = kHeadSeq / 64;
 __device__ void head_seq_wave(const double* __restrict__ w, int head_n,
-                              double& c, double* __restrict__ cdf, double* buf) {
+                              double& c, double* __restrict__ cdf) {
   const int lane = threadIdx.x & 63;
-  for (int k = lane; k < head_n; k += 64) buf[k] = w[k];
-  __syncthreads();
-  if (lane == 0) {
-    double cc = buf[0];  // numpy: cdf[0] = w[0] (-0.0 stays -0.0)
-    for (int k = 1; k < head_n; ++k) {
-      cc = cc + buf[k];
-      buf[k] = cc;
+  double v[kHeadPer], out[kHeadPer];
+#pragma unroll
+  for (int q = 0; q < kHeadPer; ++q) {
+    const int k = lane * kHeadPer + q;
+    v[q] = k < head_n ? w[k] : 0.0;
+    out[q] = 0.0;
+  }
+  double cc = 0.0;
+#pragma unroll
+  for (int l = 0; l < 64; ++l) {
+#pragma unroll
+    for (int q = 0; q < kHeadPer; ++q) {
+      const int k = l * kHeadPer + q;
+      if (k < head_n) {  // wave-uniform
+        const double s = readlane_f64(v[q], l);
+        cc = k == 0 ? s : cc + s;  // numpy: cdf[0] = w[0] (-0.0 stays)
+        out[q] = lane == l ? cc : out[q];
+      }
     }
   }
-  __syncthreads();
-  c = buf[head_n - 1];
-  for (int k = lane; k < head_n; k += 64) cdf[k] = buf[k];
+  c = cc;
+#pragma unroll
+  for (int q = 0; q < kHeadPer; ++q) {
+    const int k = lane * kHeadPer + q;
+    if (k < head_n) cdf[k] = out[q];
+  }
 }
 
 __global__ __launch_bounds__(kCdfThreads) void cdf_tile_sum_kernel(
@@ -362,7 +380,6 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
     const int* __restrict__ e_t, const long long* __restrict__ T_t,
     long long* __restrict__ c_start, double* __restrict__ cdf,
     double* __restrict__ last) {
-  __shared__ double buf[kHeadSeq];
   const int lane = threadIdx.x;
   double c = 0.0;  // chain value (wave-uniform)
   for (int64_t t0 = 0; t0 < nt; t0 += kChainChunk) {
@@ -434,7 +451,7 @@ __global__ __launch_bounds__(64) void cdf_chain_kernel(
         const int tile_n = static_cast<int>(n - base < kCdfTile ? n - base : kCdfTile);
         if (t == 0) {  // tile 0 is always slow: its dense binade exits first
           const int h = tile_n < kHeadSeq ? tile_n : kHeadSeq;
-          head_seq_wave(w, h, c, cdf, buf);
+          head_seq_wave(w, h, c, cdf);
           if (tile_n > h) exact_tile_wave(w, h, tile_n - h, c, cdf);
         } else {
           exact_tile_wave(w, base, tile_n, c, cdf);

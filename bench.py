@@ -185,6 +185,64 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     }
 
 
+# xGMI model for the rank-slice prediction: ASSUMED
+# constants, not measured here (no multi-GPU box): one link per GPU pair,
+# 153 GB/s nominal per link (the task's figure) at an assumed 50 % RCCL
+# efficiency, and a fixed latency per collective call.
+XGMI_LINK_GBS = 153.0 * 0.5
+RCCL_LATENCY_US = 25.0
+
+
+def rank_slice_report(args, comm, N, d, S, ms_step, stages, kde_ms,
+                      kde_pairs, coll, state):
+    """One line per R: rank 0's measured share of a generation, its stage
+    breakdown, the collectives it would issue (calls, bytes) and the
+    predicted whole-job time with the xGMI model added."""
+    R = comm.world
+    steps = len(stages)
+    keys = sorted({k for tm in stages for k in tm})
+    avg = {k: sum(tm.get(k, 0.0) for tm in stages) / steps for k in keys}
+    per_step = {k: [v[0] / steps, v[1] / steps, v[2] / steps]
+                for k, v in coll.items()}
+    # latency per call; all-gathers: the largest piece over one link (each
+    # peer sends its own piece on its own link, in parallel)
+    xgmi_ms = 0.0
+    for kind, (calls, sent, recv) in per_step.items():
+        if kind == "barrier" and R == 1:
+            continue
+        xgmi_ms += calls * RCCL_LATENCY_US * 1e-3 if R > 1 else 0.0
+        if kind == "all_gather_rows" and R > 1:
+            xgmi_ms += recv / (R - 1) / (XGMI_LINK_GBS * 1e9) * 1e3
+    kde_avg = sum(kde_ms) / max(len(kde_ms), 1)
+    scaling = ("sample_generation", "engine_kde")
+    fixed = {k: v for k, v in avg.items()
+             if k in ("cdf", "normalise", "quantile", "fit_pack")}
+    pred_ms = ms_step + xgmi_ms
+    return {
+        "kind": "rank-slice (predicted, unmeasured on multi-GPU hardware)",
+        "R": R, "N": N, "d": d, "S": S, "steps": steps,
+        "rank0_ms_per_step": ms_step,
+        "stage_ms": avg,
+        "kde_launch_ms": kde_avg,
+        "kde_rows_per_launch": (sum(kde_pairs) / max(len(kde_pairs), 1)) / N,
+        "repeated_full_population_ms": sum(fixed.values()),
+        "largest_non_scaling_term": max(fixed, key=fixed.get) if fixed
+        else None,
+        "collectives_per_step": {k: {"calls": v[0], "bytes_sent": v[1],
+                                     "bytes_received": v[2]}
+                                 for k, v in per_step.items()},
+        "xgmi_model_ms": xgmi_ms,
+        "xgmi_model": f"{RCCL_LATENCY_US} us per collective call + the "
+                      f"largest all-gather piece / {XGMI_LINK_GBS} GB/s "
+                      f"(one link per GPU pair; assumed constants)",
+        "predicted_ms_per_step": pred_ms,
+        "predicted_value": N / (pred_ms * 1e-3),
+        "unit": "accepted particles/s",
+        "eps_last": state["eps"],
+        "scaling_terms": list(scaling),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,16 +254,27 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rank-slice", type=int, default=0, metavar="R",
+                    help="one GPU runs rank 0's share of an R-GPU job "
+                         "(pyabc_amd.distributed.RankSliceComm): B/R "
+                         "proposals per round, M/R KDE rows, every "
+                         "full-population stage; prints the stage times, "
+                         "the collectives' byte counts and the xGMI-model "
+                         "prediction instead of the contract line")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="multi-rank rehearsal on a one-GPU box: every rank "
                          "on cuda:0, gloo collectives staged through host")
     args = ap.parse_args()
 
-    if args.rehearse_gloo:
+    if args.rank_slice:
+        from pyabc_amd.distributed import RankSliceComm
+        comm = RankSliceComm(args.rank_slice)
+        torch.cuda.set_device(0)
+    elif args.rehearse_gloo:
         comm = Comm.from_env("gloo", device=0)
     else:
         comm = Comm.from_env("nccl")
-    if comm.world == 1:
+    if comm.world == 1 and not args.rank_slice:
         torch.cuda.set_device(0)
     R = comm.world
     N, d, S = args.particles, args.dim, args.n_stats
@@ -235,17 +304,38 @@ def main():
     state = {"fit": fit, "eps": eps, "n_eval": 0, "t": 1, "sched": {},
              "k": None}
 
+    stages = []     # --rank-slice: synchronised stage times per step
+
+    def mark(tm, key, t0):
+        if args.rank_slice:
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            tm[key] = tm.get(key, 0.0) + (t1 - t0) * 1e3
+            return t1
+        return t0
+
     def step():
         t = state["t"]
         if state["k"] is not None:
             if state["k"] in pick:
                 state["sched"][state["k"]] = (state["fit"], state["eps"])
             state["k"] += 1
+        tm, t0 = {}, time.perf_counter()
+        if args.rank_slice:
+            state["fit"].cdf          # the resampling CDF + its bucket table
+            t0 = mark(tm, "cdf", t0)
         res = eng.sample_generation(t, N, state["fit"], x0, fw, state["eps"])
+        t0 = mark(tm, "sample_generation", t0)
         th, dd, ww, n_eval, _ = eng.gather_population(res)
+        t0 = mark(tm, "normalise", t0)
         state["eps"] = float(K.weighted_quantile(dd, ww, 0.5,
                                                  comm=comm)[0].item())
+        t0 = mark(tm, "quantile", t0)
         state["fit"] = DeviceMVNFit(th, ww)
+        t0 = mark(tm, "fit_pack", t0)
+        if args.rank_slice:
+            tm.update({f"engine_{k}": v * 1e3 for k, v in eng.timers.items()})
+            stages.append(tm)
         state["n_eval"] = n_eval
         state["t"] = t + 1
         return res
@@ -253,7 +343,9 @@ def main():
     for _ in range(args.warmup):
         step()
     state["k"] = 0
+    stages.clear()
     eng.kde_events = []
+    log0 = len(comm.log) if args.rank_slice else 0
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -261,6 +353,7 @@ def main():
     for _ in range(args.steps):
         step()
         phases.append(dict(eng.timers))
+    coll = comm.summary(log0) if args.rank_slice else None
     torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -289,6 +382,11 @@ def main():
         f"n_eval={state['n_eval']} phases={phases[-1]}")
 
     if comm.rank != 0:
+        return
+    if args.rank_slice:
+        print(json.dumps(rank_slice_report(
+            args, comm, N, d, S, ms_step, stages, kde_ms, kde_pairs,
+            coll, state)), flush=True)
         return
     out = {
         "metric": "accepted particles/s per generation + KDE weight pairs/s, "

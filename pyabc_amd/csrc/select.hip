@@ -66,6 +66,8 @@ __global__ __launch_bounds__(256) void final_sum_kernel(const double* __restrict
 // the population is sharded over ranks; see abc_wquantile_exchange):
 struct WQXchg {
   long long wmax_bits;        // MAX: largest weight (positive double bits)
+  long long wmin_all_bits;    // MIN: smallest weight (equal to the largest:
+                              // uniform weights, numpy's cumsum restated)
   unsigned long long w_tot;   // SUM: total fixed-point mass
   long long kprev_x;          // MAX: largest key below the knot (key ^ 2^63)
   long long knext_x;          // MIN: smallest key above the knot
@@ -79,7 +81,6 @@ struct WQXchg {
   unsigned long long wmin_prev;
   unsigned long long wmin_next;
   unsigned long long wmin_k;
-  unsigned long long pad;
   unsigned long long hist_w[kBins];  // SUM: fixed-point mass per digit
   unsigned long long hist_c[kBins];  // SUM: count per digit
 };
@@ -125,6 +126,7 @@ __global__ void wq_reset_kernel(WQState* st) {
   st->x.hist_c[t] = 0;
   if (t == 0) {
     st->x.wmax_bits = 0;
+    st->x.wmin_all_bits = 0x7ff0000000000000ll;  // +inf
     st->x.w_tot = 0;
     st->x.kprev_x = static_cast<long long>(0ull ^ kKeyFlip);   // key 0
     st->x.knext_x = static_cast<long long>(~0ull ^ kKeyFlip);  // key max
@@ -143,19 +145,25 @@ __global__ void wq_reset_kernel(WQState* st) {
   }
 }
 
-// largest weight (weights are >= 0: their bits order as signed integers)
+// largest and smallest weight (weights are >= 0: their bits order as
+// signed integers)
 __global__ __launch_bounds__(256) void wq_wmax_kernel(const double* __restrict__ w,
                                                       int64_t n, WQState* st) {
-  long long m = 0;
+  long long m = 0, mn = 0x7ff0000000000000ll;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
     const long long b = __double_as_longlong(w ? w[i] : 1.0);
     m = b > m ? b : m;
+    mn = b < mn ? b : mn;
   }
   // weights >= 0: their bits order the same as signed or unsigned integers
   block_atomic_max_u64<256>(
       reinterpret_cast<unsigned long long*>(&st->x.wmax_bits),
       static_cast<unsigned long long>(m));
+  __syncthreads();
+  block_atomic_min_u64<256>(
+      reinterpret_cast<unsigned long long*>(&st->x.wmin_all_bits),
+      static_cast<unsigned long long>(mn));
 }
 
 // scale from the (reduced) largest weight and the total count, then the
@@ -310,23 +318,105 @@ __global__ __launch_bounds__(256) void wq_neighbor_mass_kernel(
   block_atomic_min_u64<256>(&st->x.wmin_k, mk);
 }
 
+// numpy's cumsum of n equal weights w (np.cumsum(np.full(n, w))[k]: the
+// sequential chain c_0 = w, c_j = fl(c_{j-1} + w)) in closed form.  Inside
+// one binade of c every double is a multiple of the binade's ulp, so each
+// add rounds w to the same multiple -- except the first add after c entered
+// the binade when w sits exactly halfway between two multiples and c is an
+// odd multiple (ties to even: from then on c is even and the increment
+// constant).  So: exact adds until two consecutive increments agree, then
+// as many adds of that increment as stay two ulps below the binade's top in
+// one multiplication, repeated: a few rounds per binade.  (Checked against
+// np.cumsum on 4.7e5 (w, k), tie-prone weights included.)
+__device__ inline double equal_weight_cumsum(double w, long long k) {
+#pragma clang fp contract(off)
+  double c = w;
+  long long j = 0;
+  while (j < k) {
+    c = c + w;
+    if (++j == k) break;
+    const double inc = (c + w) - c;
+    const double c2 = c + w;
+    // from an odd multiple (c just entered the binade) a halfway w rounds
+    // to the other neighbour once: take that add singly
+    if ((c2 + w) - c2 != inc) continue;
+    int e = 0;
+    frexp(c, &e);  // c in [2^(e-1), 2^e)
+    const double top = ldexp(1.0, e);
+    const double room = (top - ldexp(1.0, e - 52) - c) / inc;
+    long long s = room >= 1.0 ? static_cast<long long>(floor(room)) : 0;
+    if (s > k - j) s = k - j;
+    c = c + static_cast<double>(s) * inc;  // exact: a multiple of the ulp below top
+    j += s;
+  }
+  return c;
+}
+
 // np.interp(alpha, xp, fp) restricted to the bracketing knots.  A key held
 // by several elements (ties) is a block of knots x_j = cs_j - w_j / 2, all
 // at the same point p: alpha between the block's first and last knot gives
-// p exactly, whatever the order inside the block.  numpy's argsort
-// (quicksort) leaves that order open, so the block's end knots are taken
-// with the block's smallest weight (wmin_*): the interval that gives p is
-// then the widest any order gives, and outside it the interpolation runs to
-// the neighbouring block's nearest knot.  Without ties every block is one
-// element and the arithmetic is the plain two-knot interpolation.
+// p exactly, whatever the order inside the block.
+//
+// * Equal weights (uniform: every weight the same double, or none given --
+//   1/n each, as the reference's np.ones(n) / n): the knots are numpy's own,
+//   x_j = fl(cs_j - w/2) with cs_j its sequential cumsum restated by
+//   equal_weight_cumsum at the block's element indices, and the arithmetic
+//   is numpy's (binary_search_with_guess's bracket, slope * (x - x_j) +
+//   p_j, no contraction): the result equals the reference bit for bit, with
+//   or without ties.
+// * Other weights: the knots from the exact fixed-point masses (numpy's
+//   rounded cumsum differs from them by at most ~N ulp, the SURVEY 8(a7)
+//   bound).  numpy's argsort (quicksort) leaves the order inside a tie
+//   block open, so the block's end knots are taken with the block's
+//   smallest weight (wmin_*): the interval that gives p is then the widest
+//   any order gives, and outside it the interpolation runs to the
+//   neighbouring block's nearest knot.  Without ties every block is one
+//   element and the arithmetic is the plain two-knot interpolation.
 __global__ void wq_finalize_kernel(const WQState* st, double alpha,
                                    double* __restrict__ out) {
+#pragma clang fp contract(off)  // numpy's interp: slope * dx, then + p
   const double W = static_cast<double>(st->x.w_tot);
   const unsigned long long kprev = static_cast<unsigned long long>(st->x.kprev_x) ^ kKeyFlip;
   const unsigned long long knext = static_cast<unsigned long long>(st->x.knext_x) ^ kKeyFlip;
+  const double wmax = __longlong_as_double(st->x.wmax_bits);
+  const bool uniform = st->x.wmin_all_bits == st->x.wmax_bits && wmax > 0.0;
   double eps;
   if (st->none) {
     eps = key_f64(kprev);  // alpha past the last knot: largest point
+  } else if (uniform) {
+    const unsigned long long fw = fixw(wmax, st->scale);
+    const long long count = static_cast<long long>(st->x.w_tot / fw);
+    // all-ones weights are the no-weights call (1/n each); normalised equal
+    // weights are 1.0 only for n = 1, where 1/n = 1
+    const double wv = wmax == 1.0 ? 1.0 / static_cast<double>(count) : wmax;
+    const double h = 0.5 * wv;
+    const long long klo = static_cast<long long>(st->w_less / fw);
+    const long long khi = static_cast<long long>((st->w_less + st->w_eq) / fw) - 1;
+    const double pk = key_f64(st->prefix);
+    const double xk = equal_weight_cumsum(wv, khi) - h;
+    if (alpha >= xk) {
+      if (khi == count - 1 || alpha == xk) {
+        eps = pk;
+      } else {
+        const double xn = equal_weight_cumsum(wv, khi + 1) - h;
+        const double slope = (key_f64(knext) - pk) / (xn - xk);
+        eps = slope * (alpha - xk) + pk;
+      }
+    } else if (alpha >= (klo == khi ? xk : equal_weight_cumsum(wv, klo) - h)) {
+      eps = pk;  // inside the tied block (slope 0 in numpy)
+    } else if (klo == 0) {
+      eps = pk;  // before the first knot: fp[0]
+    } else {
+      const double xa = equal_weight_cumsum(wv, klo) - h;
+      const double xp = equal_weight_cumsum(wv, klo - 1) - h;
+      const double pp = key_f64(kprev);
+      if (alpha == xp) {
+        eps = pp;
+      } else {
+        const double slope = (pk - pp) / (xa - xp);
+        eps = slope * (alpha - xp) + pp;
+      }
+    }
   } else {
     const double pk = key_f64(st->prefix);
     const unsigned long long wmk = st->x.wmin_k < st->w_eq ? st->x.wmin_k : st->w_eq;
@@ -1494,7 +1584,8 @@ int abc_wquantile_exchange(int step, int64_t* offset_bytes, int64_t* count,
   *count = 0;
   *op = 0;  // 0 none, 1 sum, 2 max, 3 min (int64 words)
   if (step == kWqWmax) {
-    *offset_bytes = offsetof(WQXchg, wmax_bits); *count = 1; *op = 2;
+    // wmax_bits (MAX) then wmin_all_bits (MIN)
+    *offset_bytes = offsetof(WQXchg, wmax_bits); *count = 2; *op = 4;
   } else if (step == kWqTotal) {
     *offset_bytes = offsetof(WQXchg, w_tot); *count = 1; *op = 1;
   } else if (step >= kWqHist0 && step < kWqHist0 + 8) {

@@ -10,6 +10,7 @@ accepted rows (theta, distance; all-gather), the evaluation count
 computed redundantly and deterministically on every rank from identical
 inputs, so no further exchange is needed.
 """
+import math
 import os
 
 import torch
@@ -189,3 +190,97 @@ def agree_int(v):
     if env_world() == 1:
         return int(v)
     return Comm.from_env().broadcast_int(v)
+
+
+class RankSliceComm(Comm):
+    """Rank 0 of an R-rank job, emulated in ONE process on one GPU
+    (``bench.py --rank-slice R``): the engine runs exactly rank 0's share of
+    a generation -- its B/R proposals per sampling round, its M/R rows of
+    the KDE pass against the full population, and every full-population
+    stage each rank repeats -- while the other R-1 ranks are taken to be
+    statistically identical to this one:
+
+    * count all-gathers return R copies of this rank's count, sums are R
+      times this rank's value, maxima / minima are this rank's own;
+    * a row all-gather returns this rank's rows in every other rank's slot
+      (shape and byte count of the real exchange, the contents of a
+      replicated population);
+    * the weighted-quantile histogram all-reduces (SUM) multiply by R.
+
+    Nothing crosses a link, so every collective is counted instead
+    (``log``: kind, payload bytes this rank sends, bytes it receives), for
+    the xGMI model in DESIGN.md section 5.  Measurement infrastructure: the
+    generation it produces is a valid population but not the R-rank one."""
+
+    def __init__(self, world):
+        super().__init__(0, int(world), None, force=True)
+        self.log = []
+
+    def _note(self, kind, sent, recv):
+        self.log.append((kind, int(sent), int(recv)))
+
+    @property
+    def _host_staged(self):
+        return False
+
+    def barrier(self):
+        self._note("barrier", 0, 0)
+
+    def broadcast_int(self, v, src=0):
+        self._note("broadcast", 8, 8)
+        return int(v)
+
+    def all_gather_rows(self, t, sizes=None):
+        R = self.world
+        if sizes is None:
+            sizes = self.all_gather_ints(t.shape[0])
+        assert sizes[0] == t.shape[0], "all_gather_rows: bad sizes"
+        row = math.prod(t.shape[1:]) * t.element_size()
+        pieces = []
+        for s in range(R):
+            c = sizes[s]
+            if c <= t.shape[0]:
+                pieces.append(t[:c])
+            else:   # more rows than this rank holds: repeat them
+                reps = -(-c // max(t.shape[0], 1))
+                pieces.append(t.repeat((reps,) + (1,) * (t.dim() - 1))[:c])
+        self._note("all_gather_rows", sizes[0] * row,
+                   (sum(sizes) - sizes[0]) * row)
+        return torch.cat(pieces)
+
+    def all_gather_ints(self, v):
+        x = int(v.item()) if torch.is_tensor(v) else int(v)
+        self._note("all_gather_ints", 8, 8 * (self.world - 1))
+        return [x] * self.world
+
+    def all_gather_int_lists(self, vals):
+        n = len(vals)
+        self._note("all_gather_int_lists", 8 * n, 8 * n * (self.world - 1))
+        return [list(vals) for _ in range(self.world)]
+
+    def all_reduce_ints(self, vals):
+        self._note("all_reduce_ints", 8 * len(vals), 8 * len(vals))
+        return [int(v) * self.world for v in vals]
+
+    def all_reduce_int(self, v):
+        self._note("all_reduce_int", 8, 8)
+        return int(v) * self.world
+
+    def all_reduce_words(self, x, op):
+        self._note(f"all_reduce_words_op{op}", 8 * x.numel(), 8 * x.numel())
+        if op == 1:
+            x.mul_(self.world)
+
+    def all_reduce_max_float(self, v):
+        self._note("all_reduce_max_float", 8, 8)
+        return float(v)
+
+    def summary(self, since=0):
+        """{kind: [calls, bytes sent, bytes received]} over log[since:]."""
+        out = {}
+        for kind, s, r in self.log[since:]:
+            e = out.setdefault(kind, [0, 0, 0])
+            e[0] += 1
+            e[1] += s
+            e[2] += r
+        return out

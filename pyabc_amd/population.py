@@ -80,20 +80,39 @@ class Population:
         return pd.DataFrame(rows)
 
     def get_weighted_sum_stats(self):
+        """(weights, sum_stats): one entry per accepted statistic, the
+        particle's weight times its model probability (population.py:200-216)."""
         weights, sum_stats = [], []
         for p in self._list:
-            mp = self._model_probabilities[p.m]
-            n = len(p.accepted_sum_stats)
+            w = p.weight * self._model_probabilities[p.m]
             for s in p.accepted_sum_stats:
-                weights.append(p.weight * mp / n)
+                weights.append(w)
                 sum_stats.append(s)
         return weights, sum_stats
 
     def get_accepted_sum_stats(self):
-        return sum((p.accepted_sum_stats for p in self._list), [])
+        out = []
+        for p in self._list:
+            out.extend(p.accepted_sum_stats)
+        return out
 
     def get_for_keys(self, keys):
-        return {k: [getattr(p, k) for p in self._list] for k in keys}
+        """Same-ordered lists per key, one entry per accepted distance
+        (population.py:228-262)."""
+        _check_keys(keys)
+        ret = {k: [] for k in keys}
+        for p in self._list:
+            n = len(p.accepted_distances)
+            if "weight" in ret:
+                ret["weight"].extend(
+                    [p.weight * self._model_probabilities[p.m]] * n)
+            if "parameter" in ret:
+                ret["parameter"].extend([p.parameter] * n)
+            if "distance" in ret:
+                ret["distance"].extend(p.accepted_distances)
+            if "sum_stat" in ret:
+                ret["sum_stat"].extend(p.accepted_sum_stats)
+        return ret
 
     def get_distribution(self, m=0):
         pl = [p for p in self._list if p.m == m]
@@ -102,6 +121,26 @@ class Population:
             df = df[sorted(df.columns)]
         w = np.array([p.weight for p in pl], dtype=np.float64)
         return df, w
+
+
+FOR_KEYS = ("weight", "distance", "parameter", "sum_stat")
+
+
+def _check_keys(keys):
+    for k in keys:
+        if k not in FOR_KEYS:
+            raise ValueError(f"Key {k} not in {list(FOR_KEYS)}.")
+
+
+class DistanceToGroundTruth:
+    """``lambda x, par: distance(x, x_0, t, par)`` (smc.py:978-984) that a
+    device population can also evaluate with the distance's batch kernel."""
+
+    def __init__(self, distance, x_0, t):
+        self.distance, self.x_0, self.t = distance, x_0, t
+
+    def __call__(self, x, par):
+        return self.distance(x, self.x_0, self.t, par)
 
 
 class WeightedDistances:
@@ -237,25 +276,79 @@ class ColumnarPopulation:
         return self.d
 
     def update_distances(self, distance_to_ground_truth):
-        raise NotImplementedError(
-            "ColumnarPopulation: use update_distances_device (batch kernel)")
+        """Population.update_distances (population.py:144-159): every
+        accepted statistic's distance re-evaluated by the callable
+        ``(sum_stat, parameter) -> float``.  A :class:`DistanceToGroundTruth`
+        over a distance with a batch kernel runs on the device; any other
+        callable is called once per particle on host copies."""
+        f = distance_to_ground_truth
+        if isinstance(f, DistanceToGroundTruth) and \
+                hasattr(f.distance, "batch") and self.theta.is_cuda:
+            return self.update_distances_device(f.distance, f.t, f.x_0)
+        if self.stats_T is None:
+            raise ValueError("statistics of this population were not kept")
+        d = [float(f(s, p)) for s, p in
+             zip(self._host_sum_stats(), self._host_parameters())]
+        self.d = torch.as_tensor(np.asarray(d, dtype=np.float64),
+                                 device=self.theta.device)
+        return self.d
+
+    def to_dict(self):
+        """{model: [Particle, ...]} (population.py:264-286)."""
+        return {self.m: self.get_list()} if len(self) else {}
+
+    def _host_parameters(self):
+        from .parameters import Parameter
+        th = self.theta.cpu().numpy()
+        return [Parameter(dict(zip(self.names, row))) for row in th]
+
+    def _host_sum_stats(self):
+        if self.stats_T is None:
+            return [{} for _ in range(len(self))]
+        st = self.stats_T.cpu().numpy()
+        keys = self.stat_keys if self.stat_keys is not None \
+            else list(range(st.shape[0]))
+        return [dict(zip(keys, st[:, i])) for i in range(st.shape[1])]
+
+    def get_weighted_sum_stats(self):
+        """(weights, sum_stats) as host lists (population.py:200-216): one
+        statistic per particle, weight x model probability."""
+        mp = self._model_probabilities[self.m]
+        w = (self.w.cpu().numpy() * mp).tolist() if mp != 1.0 \
+            else self.w.cpu().numpy().tolist()
+        return w, self._host_sum_stats()
+
+    def get_for_keys(self, keys):
+        """Population.get_for_keys (population.py:228-262) from the
+        columns: weight (x model probability), distance, parameter,
+        sum_stat, one entry per particle."""
+        _check_keys(keys)
+        ret = {}
+        mp = self._model_probabilities[self.m]
+        for k in keys:
+            if k == "weight":
+                w = self.w.cpu().numpy()
+                ret[k] = (w * mp if mp != 1.0 else w).tolist()
+            elif k == "distance":
+                ret[k] = self.d.cpu().numpy().tolist()
+            elif k == "parameter":
+                ret[k] = self._host_parameters()
+            else:
+                if self.stats_T is None:
+                    raise ValueError("statistics of this population were "
+                                     "not kept")
+                ret[k] = self._host_sum_stats()
+        return ret
 
     def get_distribution(self, m=0):
         return DeviceFrame(self.theta, self.names), self.w
 
     def get_list(self):
-        th = self.theta.cpu().numpy()
         w = self.w.cpu().numpy()
         d = self.d.cpu().numpy()
-        st = self.stats_T.cpu().numpy() if self.stats_T is not None else None
-        out = []
-        from .parameters import Parameter
-        for i in range(th.shape[0]):
-            ss = [dict(zip(self.stat_keys, st[:, i]))] if st is not None \
-                else [{}]
-            out.append(Particle(self.m, Parameter(dict(zip(self.names, th[i]))),
-                                float(w[i]), ss, [float(d[i])]))
-        return out
+        return [Particle(self.m, par, float(w[i]), [ss], [float(d[i])])
+                for i, (par, ss) in enumerate(zip(self._host_parameters(),
+                                                  self._host_sum_stats()))]
 
 
 _COLUMNS = ("theta", "w", "d", "stats_T")

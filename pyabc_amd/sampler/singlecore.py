@@ -1,4 +1,12 @@
-"""Sequential sampler (API of pyabc/sampler/singlecore.py:1-38)."""
+"""Sequential sampler (API of pyabc/sampler/singlecore.py:1-38).
+
+Semantics the reference defines there, restated as one evaluation loop:
+every call of ``simulate_one`` is one evaluation and is counted; with
+``check_max_eval`` no evaluation starts once ``max_eval`` of them have run;
+the loop ends at the n-th acceptance; a sample that ends short of n
+acceptances is marked ``ok = False``.  (The reference nests a per-particle
+loop inside a loop over n; both stop at the same evaluation.)
+"""
 import numpy as np
 
 from .base import Sampler
@@ -9,20 +17,18 @@ class SingleCoreSampler(Sampler):
         super().__init__()
         self.check_max_eval = check_max_eval
 
+    def _may_start(self, done, max_eval):
+        return not self.check_max_eval or done < max_eval
+
     def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
                                 all_accepted=False):
-        nr_simulations = 0
         sample = self._create_empty_sample()
-        for _ in range(n):
-            while True:
-                if self.check_max_eval and nr_simulations >= max_eval:
-                    break
-                new_sim = simulate_one()
-                sample.append(new_sim)
-                nr_simulations += 1
-                if new_sim.accepted:
-                    break
-        self.nr_evaluations_ = nr_simulations
-        if sample.n_accepted < n:
-            sample.ok = False
+        done = accepted = 0
+        while accepted < n and self._may_start(done, max_eval):
+            particle = simulate_one()
+            done += 1
+            accepted += bool(particle.accepted)
+            sample.append(particle)
+        self.nr_evaluations_ = done
+        sample.ok = sample.ok and accepted >= n
         return sample

@@ -20,7 +20,7 @@ from .distance import PNormDistance, to_distance
 from .epsilon import MedianEpsilon
 from .model import SimpleModel
 from .parameters import Parameter
-from .population import Particle, ColumnarPopulation
+from .population import Particle, ColumnarPopulation, DistanceToGroundTruth
 from .populationstrategy import ConstantPopulationSize
 from .random_variables import RV, ModelPerturbationKernel
 from .sampler import GPUBatchSampler
@@ -175,12 +175,10 @@ class ABCSMC:
                             self.acceptor.get_epsilon_config(t))
 
     def _update_distances(self, population, t):
-        if isinstance(population, ColumnarPopulation):
-            population.update_distances_device(self.distance_function, t,
-                                               self.x_0)
-        else:
-            population.update_distances(
-                lambda x, par: self.distance_function(x, self.x_0, t, par))
+        # smc.py:978-984; a device population runs the distance's batch
+        # kernel when it has one
+        population.update_distances(
+            DistanceToGroundTruth(self.distance_function, self.x_0, t))
 
     def _get_initial_population(self, t):
         """smc.py:447-470 (cached)."""

@@ -574,3 +574,20 @@ def test_singlecore_parity_same_draws(pa):
                                     float(g["eps"]), max_eval=float(me))
         assert bool(res.ok) == bool(ok) and res.n_eval == int(nr), (me, res.ok,
                                                                   res.n_eval)
+
+
+def test_columnar_population_reference_api_gpu(pa):
+    """ColumnarPopulation on device columns (weights normalised by the
+    device sum) against the list Population of the same particles: every
+    reader (get_for_keys, get_weighted_sum_stats, to_dict, get_list,
+    get_accepted_sum_stats) and update_distances -- with a Python callable
+    (host loop) and with the reference's closure over a p-norm distance
+    (DistanceToGroundTruth: the batch kernel on the device)."""
+    from tests.test_population_api import _pair, check_population_api
+    ref, col = _pair(n=300, S=5, seed=3, device="cuda", normalize=True)
+    assert col.theta.is_cuda and col.w.is_cuda
+    dist = pa.PNormDistance(p=2)
+    x_0 = {f"s{k}": 0.1 * k for k in range(5)}
+    dist.initialize(0, lambda: [], x_0)
+    check_population_api(ref, col, dist, x_0)
+    assert col.d.is_cuda

@@ -73,7 +73,8 @@ def _generation(comm, n, min_batch, record):
     rs = eng.sample_generation(2, n, fit1, None, None, None, keep_stats=False,
                                record=False, acceptance=acc,
                                record_particles=True)
-    return dict(theta0=theta.cpu().numpy(), eps0=eps, theta=th.cpu().numpy(),
+    return dict(theta0=theta.cpu().numpy(), eps0=eps, d0=dist.cpu().numpy(),
+                theta=th.cpu().numpy(),
                 d=dd.cpu().numpy(), w=ww.cpu().numpy(),
                 logpd=res.logpd.cpu().numpy(), n_eval=int(n_eval),
                 stats=res.stats_T.cpu().numpy(),
@@ -122,7 +123,7 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     one = res["single"]
     for r in (0, 1):
         got = res[r]
-        for k in ("theta0", "theta", "d", "w", "logpd", "stats", "rec",
+        for k in ("theta0", "d0", "theta", "d", "w", "logpd", "stats", "rec",
                   "cov1", "eps_ties", "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta",
                   "s_rec_d", "s_rec_acc"):
             np.testing.assert_array_equal(got[k], one[k], err_msg=k)
@@ -141,6 +142,20 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     assert np.all(one["d"] <= one["eps0"])
     assert abs(one["w"].sum() - 1.0) < 1e-12
     assert one["eps1"] <= one["eps0"]
+    # the (one- and two-rank) epsilons against the reference's formula:
+    # random weights within SURVEY 8(a7)'s local bound, equal weights bit
+    # for bit (tests/wq_bound.py)
+    from oracle import ref_cpu as ref
+    from tests.wq_bound import local_bound
+    want = ref.weighted_quantile(one["d"], one["w"], 0.5)
+    bound, exact = local_bound(one["d"], one["w"], 0.5)
+    assert abs(one["eps1"] - want) <= (0.0 if exact else
+                                       1e-12 * abs(want) + bound)
+    assert one["eps0"] == ref.weighted_quantile(
+        one["d0"], np.full(len(one["d0"]), 1.0 / len(one["d0"])), 0.5)
+    dt = np.round(one["d"] * 2.0) / 2.0
+    for i, a in enumerate((0.3, 0.5, 0.7, 0.9)):
+        assert one["eps_ties"][4 + i] == ref.weighted_quantile(dt, None, a)
 
 
 def _rccl_main(rank, port, n, out):
@@ -347,3 +362,29 @@ def test_two_ranks_local_transition_fit_sharded_bit_for_bit():
         for k in ("covs", "invs", "dets", "nbr", "theta", "logpd"):
             np.testing.assert_array_equal(res[r][k], one[k], err_msg=k)
         assert res[r]["n_eval"] == one["n_eval"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_slice():
+    """bench.py --rank-slice 4: one process runs rank 0's share of a 4-GPU
+    generation (a quarter of the KDE rows, every full-population stage) and
+    prints the stage breakdown, the collectives' calls and bytes and the
+    xGMI-model prediction."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rank-slice",
+           "4", "--steps", "2", "--warmup", "1", "--particles", "40000",
+           "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines()
+             if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = lines[0]
+    assert r["R"] == 4 and r["steps"] == 2
+    assert r["kde_rows_per_launch"] == pytest.approx(10000, rel=1e-9)
+    ag = r["collectives_per_step"]["all_gather_rows"]
+    assert ag["calls"] >= 3 and ag["bytes_received"] > ag["bytes_sent"] > 0
+    assert r["predicted_ms_per_step"] >= r["rank0_ms_per_step"] > 0
+    assert r["largest_non_scaling_term"] in r["stage_ms"]

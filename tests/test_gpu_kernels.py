@@ -530,28 +530,76 @@ def test_column_mad_and_std(K, name):
 
 # ------------------------------------------------------ (a7) quantile
 def test_weighted_quantile_golden(K):
+    """The reference's own outputs (tests/golden/quantile.npz, written by
+    weighted_quantile itself).  Random weights: within SURVEY 8(a7)'s local
+    bound at the bracketing knots, and <= 1e-9 absolute.  Uniform weights
+    (weights=None, np.ones(n) / n): bit for bit -- the device restates
+    numpy's cumsum of equal weights (select.hip equal_weight_cumsum)."""
+    from tests.wq_bound import local_bound, record
     g = load_golden("quantile")
+    rows = []
     for N in [3, 4, 1000, 100000]:
         d, w = g[f"d_{N}"], g[f"w_{N}"]
         for j, a in enumerate(g["alphas"]):
+            a = float(a)
             q = float(host(K.weighted_quantile(dev(d), dev(w), a))[0])
+            want = float(g[f"q_{N}"][j])
+            bound, exact = local_bound(d, w, a)
+            tol = 0.0 if exact else 1e-12 * abs(want) + bound
+            err = abs(q - want)
+            rows.append(dict(N=N, alpha=a, weights="random", err=err,
+                             tol=tol, rel=err / abs(want) if want else err))
+            assert err <= tol, (N, a, q, want, tol)
+            assert err <= 1e-9, (N, a, err)
             qu = float(host(K.weighted_quantile(dev(d), None, a))[0])
-            # reference cumsum rounding enters through the interpolation
-            # slope: |dq| <= 1e-12 q + slope * N * 2^-52
-            srt = np.sort(d)
-            slope = np.max(np.diff(srt)) / np.min(w) * 2 if N > 1 else 0
-            tol = 1e-12 * abs(g[f"q_{N}"][j]) + slope * N * 2.0 ** -52
-            assert abs(q - g[f"q_{N}"][j]) <= tol, (N, a, q, g[f"q_{N}"][j])
-            tolu = 1e-12 * abs(g[f"qu_{N}"][j]) + np.max(np.diff(srt)) * N * \
-                N * 2.0 ** -51 if N > 1 else 0
-            assert abs(qu - g[f"qu_{N}"][j]) <= tolu
+            wantu = float(g[f"qu_{N}"][j])
+            rows.append(dict(N=N, alpha=a, weights="uniform (None)",
+                             err=abs(qu - wantu), tol=0.0))
+            assert qu == wantu, (N, a, qu, wantu)
+            # the same equal weights passed as an array
+            wu = np.ones(N) / N
+            qa = float(host(K.weighted_quantile(dev(d), dev(wu), a))[0])
+            assert qa == wantu, (N, a, qa, wantu)
+    record("golden", rows)
+    print(f"max |dq| random weights: "
+          f"{max(r['err'] for r in rows if r['weights'] == 'random'):.3e}")
 
 
-def _wq_tie_blocks(d, w, alpha):
+@pytest.mark.parametrize("N", [1, 2, 5, 64, 999, 4096, 100003, 1_000_000])
+def test_weighted_quantile_equal_weights_bit_exact(K, N):
+    """Equal weights -- none, np.ones(n) / n, and a constant that is not
+    1/n (normalised weights of equal particles) -- with continuous and
+    heavily tied points, alpha on a grid and at knots: equal to the
+    reference's formula (np.argsort, np.cumsum, np.interp) bit for bit."""
+    rng = np.random.default_rng(N)
+    cont = rng.exponential(size=N) * 3.0
+    tied = np.round(rng.normal(size=N) * 4.0) / 4.0
+    alphas = [0.0, 1e-9, 0.1, 0.25, 0.5, 0.75, 0.9, 0.999, 1.0] + \
+        list(rng.uniform(size=8)) + [(k + 0.5) / N for k in (0, N // 3, N - 1)]
+    c = float(np.full(N, 0.37)[0] / np.sum(np.full(N, 0.37)))
+    worst = 0.0
+    for pts in (cont, tied):
+        dd = dev(pts)
+        for wname, w in (("none", None), ("ones/n", np.ones(N) / N),
+                         ("const", np.full(N, c))):
+            wd = None if w is None else dev(w)
+            for a in alphas:
+                a = float(a)
+                q = float(host(K.weighted_quantile(dd, wd, a))[0])
+                want = ref.weighted_quantile(pts, None if w is None else w, a)
+                worst = max(worst, abs(q - want))
+                assert q == want, (N, wname, a, q, want)
+    assert worst == 0.0
+
+
+def _wq_tie_blocks(d, w, alpha, first=np.min, last=np.min):
     """np.interp over knots where each run of equal points is one block
-    whose end knots carry the block's smallest weight (the device's
-    convention for ties, wq_finalize_kernel); equal to the reference
-    whenever the block order is immaterial."""
+    whose first knot carries ``first`` and whose last knot carries
+    ``last`` of the block's weights.  (np.min, np.min) is the device's
+    convention for ties; the four (min / max) combinations bracket every
+    result an order of the ties can give (the slope into a block edge grows
+    with the last weight of the block before it and falls with the first
+    weight of the block)."""
     order = np.argsort(d, kind="stable")
     p, ww = d[order], w[order]
     cs = np.cumsum(ww)
@@ -559,13 +607,76 @@ def _wq_tie_blocks(d, w, alpha):
     start = 0
     for i in range(1, len(p) + 1):
         if i == len(p) or p[i] != p[start]:
-            wmin = ww[start:i].min()
-            lo = (cs[start - 1] if start else 0.0) + 0.5 * wmin
-            hi = cs[i - 1] - 0.5 * wmin
-            xs += [lo, hi] if i - start > 1 else [cs[i - 1] - 0.5 * ww[start]]
-            fs += [p[start]] * (2 if i - start > 1 else 1)
+            if i - start > 1:
+                xs += [(cs[start - 1] if start else 0.0)
+                       + 0.5 * first(ww[start:i]),
+                       cs[i - 1] - 0.5 * last(ww[start:i])]
+                fs += [p[start]] * 2
+            else:
+                xs += [cs[i - 1] - 0.5 * ww[start]]
+                fs += [p[start]]
             start = i
     return float(np.interp(alpha, xs, fs))
+
+
+def _wq_tie_bracket(d, w, alpha):
+    v = [_wq_tie_blocks(d, w, alpha, f, g) for f in (np.min, np.max)
+         for g in (np.min, np.max)]
+    return min(v), max(v)
+
+
+def _wq_device_convention(d, w, alpha):
+    """The device's general-weight path restated (select.hip
+    wq_finalize_kernel: exact 2^62 fixed-point masses, the key whose mass
+    interval holds alpha * W, tie blocks with their smallest weight at both
+    end knots, the same double operations in the same order): the kernel's
+    result bit for bit.  Not the reference -- the convention it follows
+    where numpy's unstable argsort leaves the order of ties open."""
+    d = np.asarray(d, dtype=np.float64)
+    w = np.asarray(w, dtype=np.float64)
+    n = d.size
+    E = math.frexp(float(n) * float(w.max()))[1]
+    fw = np.rint(w * math.ldexp(1.0, 62 - E)).astype(np.uint64)
+    order = np.argsort(d, kind="stable")
+    ps, fs = d[order], fw[order]
+    starts = np.flatnonzero(np.r_[True, ps[1:] != ps[:-1]])
+    val = ps[starts]
+    bmass = [int(x) for x in np.add.reduceat(fs, starts)]
+    bmin = [int(x) for x in np.minimum.reduceat(fs, starts)]
+    W = float(sum(bmass))
+    t = alpha * W
+    rem = 2 ** 64 - 1 if t >= 18446744073709551615.0 else int(t)
+    excl = 0
+    b = None
+    for j, m in enumerate(bmass):
+        if excl <= rem < excl + m:
+            b = j
+            break
+        excl += m
+    if b is None:
+        return float(val[-1])
+    pk, w_less, w_eq = float(val[b]), excl, bmass[b]
+    wmk = min(bmin[b], w_eq)
+    wk = float(wmk) / W
+    csk = float(w_less + w_eq) / W
+    xk = csk - 0.5 * wk
+    xa = xk if wmk == w_eq else float(w_less) / W + 0.5 * wk
+    if alpha >= xk:
+        if b == len(val) - 1 or alpha == xk:
+            return pk
+        wn = float(min(bmin[b + 1], bmass[b + 1])) / W
+        xn = csk + wn - 0.5 * wn
+        slope = (float(val[b + 1]) - pk) / (xn - xk)
+        return slope * (alpha - xk) + pk
+    if alpha >= xa or b == 0:
+        return pk
+    pp = float(val[b - 1])
+    wp = float(min(bmin[b - 1], bmass[b - 1])) / W
+    xp = float(w_less) / W - 0.5 * wp
+    if alpha == xp:
+        return pp
+    slope = (pk - pp) / (xa - xp)
+    return slope * (alpha - xp) + pp
 
 
 @pytest.mark.parametrize("case", ["ties70", "discrete", "zeros", "spike_edges"])
@@ -576,11 +687,18 @@ def test_weighted_quantile_ties_large(K, case):
     0.1 / 0.5 / 0.9, in the middle of the tied block and at its edges.
     A run of equal points is a block of knots at one p: alpha between its
     first and last knot gives p exactly (weighted_statistics.py:26-43).
-    Uniform weights and block interiors do not depend on the order numpy's
-    argsort gives the ties: equal to the oracle; the block edges with
-    random weights follow the device's convention (the block's smallest
-    weight at both ends, include/abc_hip.h)."""
+    * random weights, alpha away from block edges: the local bound
+      (tests/wq_bound.py; 0, i.e. equality, inside a tie block);
+    * uniform weights: bit for bit, edges included (equal weights: numpy's
+      cumsum restated, the order of ties immaterial);
+    * random weights at the block edges: numpy's unstable argsort leaves the
+      order of ties open, so parity there is a convention (the block's
+      smallest weight at both ends, include/abc_hip.h); the result equals
+      that convention restated on the host bit for bit, and both it and the
+      reference's result lie between the min- / max-weight placements of
+      the edge knots, which bracket every order."""
     import time
+    from tests.wq_bound import local_bound, record
     rng = np.random.default_rng({"ties70": 1, "discrete": 2, "zeros": 3,
                                  "spike_edges": 4}[case])
     N = 1_200_000
@@ -597,32 +715,55 @@ def test_weighted_quantile_ties_large(K, case):
     pt = {"ties70": 3.0, "discrete": 2.0, "zeros": 0.0, "spike_edges": 1.5}[case]
     below, inb = w[d < pt].sum(), w[d == pt].sum()
     dd, ww = dev(d), dev(w)
-    srt = np.sort(d)
-    gaps = np.diff(srt)
-    slope = np.max(gaps) / np.min(w) * 2
+    rows = []
     for a in [0.1, 0.5, 0.9, below + 0.5 * inb]:
+        a = float(a)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         q = float(host(K.weighted_quantile(dd, ww, a))[0])
         dt = time.perf_counter() - t0
         want = ref.weighted_quantile(d, w, a)
-        tol = 1e-12 * abs(want) + slope * N * 2.0 ** -52
-        assert abs(q - want) <= tol, (case, a, q, want)
-        print(f"{case} alpha={a:.6f}: q={q!r} want={want!r} "
+        bound, exact = local_bound(d, w, a)
+        tol = 0.0 if exact else 1e-12 * abs(want) + bound
+        rows.append(dict(alpha=a, weights="random", err=abs(q - want),
+                         tol=tol))
+        assert abs(q - want) <= tol, (case, a, q, want, tol)
+        print(f"{case} alpha={a:.6f}: q={q!r} want={want!r} tol={tol:.2e} "
               f"({dt * 1e3:.2f} ms incl. host read)")
     assert float(host(K.weighted_quantile(dd, ww, below + 0.5 * inb))[0]) == pt
-    # uniform weights: the block edges are order-independent
+    # uniform weights: bit for bit, at and around the block edges too
     wu = np.full(N, 1.0 / N)
-    for a in [below, below + 0.25 / N, below + inb - 0.25 / N, 0.5]:
+    cu = float((d < pt).sum()) / N
+    cb = float((d == pt).sum()) / N
+    for a in [cu, cu + 0.25 / N, cu + 0.5 / N, cu + cb - 0.25 / N,
+              cu + cb - 0.5 / N, cu + cb, 0.5, 0.9]:
         a = float(a)
-        q = float(host(K.weighted_quantile(dd, None, a))[0])
         want = ref.weighted_quantile(d, wu, a)
-        assert abs(q - want) <= 1e-12 * abs(want) + np.max(gaps) * 1e-9, (a, q, want)
-    # random weights at the block edges: the device's convention
-    for a in [below + 1e-9, below + inb - 1e-9]:
+        q = float(host(K.weighted_quantile(dd, None, a))[0])
+        rows.append(dict(alpha=a, weights="uniform", err=abs(q - want),
+                         tol=0.0))
+        assert q == want, (a, q, want)
+    # random weights at the block edges: the convention (bit for bit), and
+    # the reference's own result (numpy's order of the ties) inside the
+    # bracket of the min- / max-weight placements of the edge knots
+    for a in [below + 1e-9, below + inb - 1e-9, below + 0.1 / N,
+              below + inb - 0.1 / N]:
+        a = float(a)
         q = float(host(K.weighted_quantile(dd, ww, a))[0])
-        want = _wq_tie_blocks(d, w, a)
-        assert abs(q - want) <= 1e-12 * abs(want) + np.max(gaps) * 1e-6, (a, q, want)
+        conv = _wq_device_convention(d, w, a)
+        assert q == conv, (a, q, conv)
+        lo, hi = _wq_tie_bracket(d, w, a)
+        want = ref.weighted_quantile(d, w, a)
+        slack = 1e-12 * abs(want) + local_bound(d, w, a)[0]
+        assert lo - slack <= want <= hi + slack, (a, want, lo, hi)
+        assert lo - slack <= q <= hi + slack, (a, q, lo, hi)
+        rows.append(dict(alpha=a, weights="random, tie edge (convention)",
+                         err_vs_reference=abs(q - want), bracket=[lo, hi]))
+    # the non-edge alphas: the same restatement, bit for bit
+    for a in [0.1, 0.5, 0.9]:
+        q = float(host(K.weighted_quantile(dd, ww, a))[0])
+        assert q == _wq_device_convention(d, w, a), a
+    record(f"ties_large_{case}", rows)
 
 
 def test_weighted_quantile_kat(K):

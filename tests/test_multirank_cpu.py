@@ -111,3 +111,36 @@ def test_forced_one_rank_group_runs_collectives():
     assert res["ints"] == [5]
     assert res["lists"] == [[1, 2, 3]]
     assert res["sum"] == [4, 7]
+
+
+def test_rank_slice_comm_matches_identical_ranks():
+    """bench.py --rank-slice R: RankSliceComm answers every collective as R
+    ranks holding this rank's data would (sums x R, maxima / minima as is,
+    gathers replicate this rank's rows), and counts calls and bytes."""
+    import torch
+    from pyabc_amd.distributed import RankSliceComm
+    from pyabc_amd.engine import gather_segments, selection_plan
+    c = RankSliceComm(4)
+    assert c.active and c.world == 4 and c.rank == 0
+    assert c.all_gather_ints(torch.tensor(7)) == [7] * 4
+    assert c.all_reduce_ints([3, 5]) == [12, 20]
+    assert c.all_gather_int_lists([1, 2]) == [[1, 2]] * 4
+    words = torch.tensor([5, 9], dtype=torch.int64)
+    c.all_reduce_words(words, 1)
+    assert words.tolist() == [20, 36]
+    c.all_reduce_words(words, 4)
+    assert words.tolist() == [20, 36]
+    assert c.all_reduce_max_float(1.5) == 1.5
+    rows = torch.arange(12, dtype=torch.float64).reshape(6, 2)
+    g = c.all_gather_rows(rows, [6, 6, 4, 0])
+    assert g.shape == (16, 2)
+    assert torch.equal(g[6:12], rows) and torch.equal(g[12:], rows[:4])
+    # the engine's selection and segment gather run on it unchanged
+    takes, closing = selection_plan([[5] * 4, [5] * 4], [[2] * 4, [3] * 4], 13)
+    counts = [[t[s] for t in takes] for s in range(4)]
+    got = gather_segments(c, [rows[:2], rows[2:5]], (2,), counts, "cpu")
+    assert got.shape[0] == 13
+    s = c.summary()
+    assert s["all_gather_rows"][0] == 2
+    # 6 + 5 rows sent, (16 - 6) + (13 - 5) received, 16 B per row
+    assert s["all_gather_rows"][1:] == [(6 + 5) * 16, (10 + 8) * 16]

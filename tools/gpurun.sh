@@ -1,6 +1,8 @@
 #!/bin/bash
-# Rebuild the in-tree library, then run one command on the GPU box.
-#   tools/gpurun.sh TIMEOUT 'command'
+# Rebuild the in-tree library here, then run tools/gpu_job.sh on the GPU box.
+#   tools/gpurun.sh TIMEOUT NAME STEP [STEP ...]     (steps: tools/gpu_job.sh)
 set -e
 make -C "$(dirname "$0")/../pyabc_amd/csrc" -j8 > /dev/null
-exec /usr/local/graft/bin/gpurun --timeout "$1" -- "$2"
+T=$1
+shift
+exec /usr/local/graft/bin/gpurun --timeout "$T" -- "bash tools/gpu_job.sh $*"

@@ -3,7 +3,7 @@
     python tools/kde_pmc.py gpurun_out/r02a r02 [N M d]
 
 Reads the ``pmcA`` / ``pmcB`` (and optional ``pmcC``) counter collections of
-tools/gpu_r02a.sh (bench.py under ``rocprofv3 --pmc``), averages every
+tools/gpu_job.sh profile (bench.py under ``rocprofv3 --pmc``), averages every
 counter over the ``kde_mfma_kernel`` dispatches, divides by the 32x32 tiles
 one launch computes (Mpad/32 * npad/32) and writes
 ``profiles/<tag>_kde_pmc.json``.  bench.py prices its live launch with these

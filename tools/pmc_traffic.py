@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 PMC passes (tools/gpu_profile.sh) into per-kernel HBM
+"""Summarise rocprofv3 PMC passes (tools/gpu_job.sh profile) into per-kernel HBM
 traffic and VALU counters, and write profiles/kde_traffic.json for bench.py.
 
     python tools/pmc_traffic.py gpurun_out/prof_r01 r01

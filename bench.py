@@ -79,7 +79,7 @@ def kde_pmc(d):
     return None, None
 
 
-PROBE_MIX = {8: 0, 20: 1}   # tools/probes/issue_probe.hip variants
+PROBE_MIX = {8: 0, 20: 2}   # tools/probes/issue_probe.hip variants
 
 
 def issue_probe(d, waves_per_simd=2):
@@ -165,6 +165,12 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "peak": peak_tf,
         "unit": "TFLOP/s",
         "frac": frac,
+        "frac_static_issue": t_static / avg_launch_s,
+        "ceiling_note": "frac divides by a SELF-MEASURED ceiling (this "
+                        "repo's tools/probes/issue_probe.hip run live on "
+                        "this GPU); frac_static_issue prices the same "
+                        "PMC-counted mix at MI355X_MICROARCH.md's issue "
+                        "costs at 2.4 GHz",
         "traffic": traffic,
         "traffic_source": traffic_src,
         "peak_basis": basis,

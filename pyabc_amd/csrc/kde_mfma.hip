@@ -43,6 +43,7 @@ namespace abc {
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr double kLwFloor = -160.0;  // 2^-160 is 0 in fp32: no term changes
@@ -66,8 +67,12 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
 
 template <int D>
 struct Mk {
-  static constexpr int KH = (D + 6 + 15) / 16;      // y1.y1, aH x3, bH x3
-  static constexpr int KL = (7 * D + 4 + 15) / 16;  // 7 cross terms, aL, bL
+  // d > 8: every piece f16 (kF16 scheme below): y1.y1, aH x2, bH x2 | five
+  // cross terms per dimension, aL, bL.  d <= 8: bf16 y1.y1, aH x3, bH x3 |
+  // seven cross terms, aL, bL (the folded accumulation needs one scale).
+  static constexpr bool F16 = D > 8;
+  static constexpr int KH = F16 ? (D + 4 + 15) / 16 : (D + 6 + 15) / 16;
+  static constexpr int KL = F16 ? (5 * D + 4 + 15) / 16 : (7 * D + 4 + 15) / 16;
   static constexpr int KT = KH + KL;
   static constexpr int IB = D <= 8 ? 3 : (D <= 24 ? 2 : 1);  // i-tiles/wave
   // row padding unit in i-tiles per wave: every IB the launch may pick
@@ -88,6 +93,53 @@ __device__ inline float bf16_f(unsigned short b) {
 }
 constexpr unsigned short kBf16One = 0x3F80;
 constexpr unsigned short kBf16NegInf = 0xFF80;
+
+// ---- f16 pieces (d > 8) -------------------------------------------------------
+// The bf16 scheme spends 7 cross products per dimension because bf16 keeps 8
+// bits; with f16's 11 bits the same exactness takes five, on a grid eight
+// times finer:
+//   y1 = g rint(y/g) with the grid from the population's largest NORM,
+//        |y_j| < 2^E -> g = 2^(E-10): |y1/g| <= 1027 (population), <= 2043
+//        (new rows, |y_i| <= 2040 g; others take the exact fixup) -- f16
+//        integers;
+//   r = y - y1 (|r| <= g/2) -> r2 = f16(r 2^10), r3 = f16((r - r2) 2^10):
+//        22 bits below g/2; lo = y1.r2, y1.r3, r2.y1, r3.y1, r2.r2 per
+//        dimension + aL + bL (r2.r3, r3.r2 <= D g^2 2^-12 are dropped:
+//        numpy emulation tools/probes/kde_f16lo_emul.py, max row error 6.6e-7
+//        -- 8.2e-7 at d = 12, 20, 24 against 1.2e-6 -- 1.7e-6 for the bf16
+//        scheme);
+//   hi = sum 2 y1_i y1_j + aH + bH: multiples of G = g^2, |sum|/G <= 2^23.4
+//        (Cauchy-Schwarz: 2 * 2043 * 1027, |a|/G <= 160/G + 1027^2 with
+//        g >= 2^-7, |b|/G <= 2043^2), so exact in any order;
+//   every lo piece carries 2^10 (r2.r2 2^5 per side) so the pieces that
+//   matter are NORMAL f16 numbers whatever the MFMA does with f16
+//   denormals; e = fma(lo_acc, 2^-10, hi), one rounding as before.  aH, bH
+//   pieces (up to ~2^(2E+2)) are scaled by 2^-K against a partner 2^K,
+//   K = max(0, 2E - 13), to stay below the f16 maximum.  A population whose
+//   largest norm reaches 2^14 (E > 13) is packed with e = -inf everywhere:
+//   every row then takes the exact fixup.
+constexpr int kF16GridBits = 10;   // g = 2^(E - 10)
+constexpr double kF16MinGrid = 0.0078125;  // 2^-7: 160 / G <= 2^21.3
+constexpr int kF16MaxE = 13;
+constexpr float kF16LoScale = 1024.0f;     // lo pieces x 2^10
+constexpr float kF16LoUnscale = 0.0009765625f;
+constexpr unsigned short kF16One = 0x3C00;
+constexpr unsigned short kF16NegInf = 0xFC00;
+
+__device__ inline unsigned short f16_bits(float x) {  // RNE
+  return __builtin_bit_cast(unsigned short, static_cast<_Float16>(x));
+}
+__device__ inline float f16_f(unsigned short b) {
+  return static_cast<float>(__builtin_bit_cast(_Float16, b));
+}
+// grid exponent E (|y| < 2^E) -> the aH / bH scale K
+__device__ inline int f16_shift(double g) {
+  int E = 0;
+  frexp(g, &E);                        // g = 2^(E - 1 - 10) * 2^1 ...
+  E = E - 1 + kF16GridBits;            // g = 2^(E - 10)
+  const int K = 2 * E - 13;
+  return K > 0 ? K : 0;
+}
 
 // y -> (y1, y2, y3) bf16 bits, scaled by `side` (1 for the population, 2 for
 // new rows: exact); returns |y1 + y2 + y3|^2 (the represented point)
@@ -133,6 +185,110 @@ __device__ inline void split_value(double v, double G, unsigned short* h,
   const unsigned short l0 = bf16_rne(static_cast<float>(lo));
   l[0] = l0;
   l[1] = bf16_rne(static_cast<float>(lo - static_cast<double>(bf16_f(l0))));
+}
+
+// f16 pieces of one row (scaled as above), `side` 1 (population) or 2
+// (new rows, exact); returns |y1 + r2 + r3|^2 (the represented point)
+template <int D>
+__device__ inline double split_row_f16(const double* y, double g, float side,
+                                       unsigned short* y1, unsigned short* r2,
+                                       unsigned short* r3, unsigned short* r2h) {
+  double n2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double v1 = rint(y[k] / g) * g;
+    const double r = y[k] - v1;                       // exact
+    const unsigned short b2 = f16_bits(static_cast<float>(r * kF16LoScale));
+    const double v2 = static_cast<double>(f16_f(b2)) * kF16LoUnscale;
+    const unsigned short b3 = f16_bits(static_cast<float>((r - v2) * kF16LoScale));
+    const double v3 = static_cast<double>(f16_f(b3)) * kF16LoUnscale;
+    y1[k] = f16_bits(side * static_cast<float>(v1));
+    r2[k] = f16_bits(side * f16_f(b2));
+    r3[k] = f16_bits(side * f16_f(b3));
+    r2h[k] = f16_bits(side * static_cast<float>(v2 * 32.0));  // exact
+    const double yt = v1 + v2 + v3;
+    n2 = fma(yt, yt, n2);
+  }
+  return n2;
+}
+
+// v -> two f16 pieces holding rint(v/G) G exactly (|rint(v/G)| < 2^22:
+// 11 + 11 bits), each x 2^-K, plus two f16 pieces of the remainder x 2^10
+__device__ inline void split_value_f16(double v, double G, int K,
+                                       unsigned short* h, unsigned short* l) {
+  double q = rint(v / G);
+  q = fmin(fmax(q, -4194303.0), 4194303.0);
+  const double q0 = trunc(q / 2048.0) * 2048.0;     // top 11 bits
+  const double q1 = q - q0;                         // |q1| < 2^11
+  const double sc = ldexp(G, -K);
+  h[0] = f16_bits(static_cast<float>(q0 * sc));     // exact (11 bits)
+  h[1] = f16_bits(static_cast<float>(q1 * sc));
+  const double lo = (v - q * G) * kF16LoScale;      // exact, |lo| <= 512 G
+  const unsigned short l0 = f16_bits(static_cast<float>(lo));
+  l[0] = l0;
+  l[1] = f16_bits(static_cast<float>(lo - static_cast<double>(f16_f(l0))));
+}
+
+// Slot k of the f16 operands (d > 8):
+//  hi  k < D: y1 | 2y1     k = D, D+1: aH 2^-K | 2^K   k = D+2, D+3: 2^K | bH 2^-K
+//  lo  k' = 5m + q (m < D): q: 0 r2|2y1  1 r3|2y1  2 y1|2r2  3 y1|2r3
+//                                4 r2 2^-5|2r2 2^-5 (x 2^10 included above)
+//      k' = 5D, 5D+1: aL | 1   k' = 5D+2, 5D+3: 1 | bL
+template <int D, bool kA>
+__device__ inline unsigned short slot_f16(int k, const unsigned short* y1,
+                                          const unsigned short* r2,
+                                          const unsigned short* r3,
+                                          const unsigned short* r2h,
+                                          const unsigned short* h,
+                                          const unsigned short* l,
+                                          unsigned short kpow) {
+  constexpr int KH = Mk<D>::KH;
+  if (k < 16 * KH) {
+    if (k < D) return y1[k];
+    if (k < D + 2) return kA ? h[k - D] : kpow;
+    if (k < D + 4) return kA ? kpow : h[k - D - 2];
+    return 0;
+  }
+  const int kk = k - 16 * KH;
+  if (kk < 5 * D) {
+    const int m = kk / 5, q = kk % 5;
+    switch (q) {
+      case 0: return kA ? r2[m] : y1[m];
+      case 1: return kA ? r3[m] : y1[m];
+      case 2: return kA ? y1[m] : r2[m];
+      case 3: return kA ? y1[m] : r3[m];
+      default: return r2h[m];
+    }
+  }
+  if (kk < 5 * D + 2) return kA ? l[kk - 5 * D] : kF16One;
+  if (kk < 5 * D + 4) return kA ? kF16One : l[kk - 5 * D - 2];
+  return 0;
+}
+
+template <int D, bool kA>
+__device__ inline void store_frags_f16(bf16x8* __restrict__ F, int64_t p,
+                                       const unsigned short* y1,
+                                       const unsigned short* r2,
+                                       const unsigned short* r3,
+                                       const unsigned short* r2h,
+                                       const unsigned short* h,
+                                       const unsigned short* l,
+                                       unsigned short kpow) {
+  constexpr int KT = Mk<D>::KT;
+  const int64_t tile = p >> 5;
+  const int r = static_cast<int>(p & 31);
+#pragma unroll
+  for (int c = 0; c < KT; ++c) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = static_cast<short>(
+            slot_f16<D, kA>(16 * c + 8 * hh + e, y1, r2, r3, r2h, h, l, kpow));
+      F[(tile * KT + c) * 64 + 32 * hh + r] = v;
+    }
+  }
 }
 
 // Slot k of the population (A) and new-row (B) operands.
@@ -227,8 +383,15 @@ __global__ __launch_bounds__(256) void ymax_kernel(
        i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     double y[D];
     whiten_row<D>(X, i, d, mu, Us, y);
+    if constexpr (Mk<D>::F16) {  // largest norm
+      double n2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) m = fmax(m, fabs(y[k]));
+      for (int k = 0; k < D; ++k) n2 = fma(y[k], y[k], n2);
+      m = fmax(m, sqrt(n2));
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) m = fmax(m, fabs(y[k]));
+    }
   }
   block_atomic_max_u64<256>(key, static_cast<unsigned long long>(f64_key(m)));
 }
@@ -239,6 +402,15 @@ __device__ inline double grid_from_key(const unsigned long long* key) {
   if (m > 0.0) frexp(m, &E);  // m < 2^E
   return fmax(ldexp(1.0, E - 7), 0.015625);  // 256 g = 2^(E+1) >= 2 max|y|
 }
+// f16 scheme: from the largest norm, |y| < 2^E -> g = 2^(E - 10) (floor
+// 2^-7); a negative value flags E > kF16MaxE (the all-fixup packing)
+__device__ inline double grid_from_key_f16(const unsigned long long* key) {
+  const double m = key_f64(*key);
+  int E = 0;
+  if (m > 0.0) frexp(m, &E);
+  if (E > kF16MaxE) return -1.0;
+  return fmax(ldexp(1.0, E - kF16GridBits), kF16MinGrid);
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
@@ -248,7 +420,7 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
     const unsigned long long* __restrict__ ykey, double* __restrict__ gscale,
     bf16x8* __restrict__ A) {
   const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const double g = grid_from_key(ykey);
+  const double g = Mk<D>::F16 ? grid_from_key_f16(ykey) : grid_from_key(ykey);
   if (j == 0) *gscale = g;
   if (j >= npad) return;
   double y[D];
@@ -261,10 +433,27 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) y[k] = 0.0;
   }
-  unsigned short y1[D], y2[D], y3[D], h[3], l[2];
-  const double n2 = split_row<D>(y, g, 1.0f, y1, y2, y3);
-  split_value(lw - n2, g * g, h, l);
-  store_frags<D, true>(A, j, y1, y2, y3, h, l);
+  if constexpr (Mk<D>::F16) {
+    unsigned short y1[D], r2[D], r3[D], r2h[D], h[2], l[2];
+    if (g > 0.0) {
+      const int K = f16_shift(g);
+      const double n2 = split_row_f16<D>(y, g, 1.0f, y1, r2, r3, r2h);
+      split_value_f16(lw - n2, g * g, K, h, l);
+      store_frags_f16<D, true>(A, j, y1, r2, r3, r2h, h, l,
+                               f16_bits(ldexpf(1.0f, K)));
+    } else {  // E > kF16MaxE: e = -inf for every pair (all rows to the fixup)
+#pragma unroll
+      for (int k = 0; k < D; ++k) y1[k] = r2[k] = r3[k] = r2h[k] = 0;
+      h[0] = kF16NegInf;
+      h[1] = l[0] = l[1] = 0;
+      store_frags_f16<D, true>(A, j, y1, r2, r3, r2h, h, l, kF16One);
+    }
+  } else {
+    unsigned short y1[D], y2[D], y3[D], h[3], l[2];
+    const double n2 = split_row<D>(y, g, 1.0f, y1, y2, y3);
+    split_value(lw - n2, g * g, h, l);
+    store_frags<D, true>(A, j, y1, y2, y3, h, l);
+  }
 }
 
 template <int D>
@@ -280,11 +469,32 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
   bool ok = i < M;
   if (ok) {
     whiten_row<D>(theta, i, d, mu, Us, y);
+    double n2 = 0.0;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       Ydir[i * D + k] = y[k];
       ok = ok && fabs(y[k]) <= 256.0 * g;  // NaN -> not ok
+      n2 = fma(y[k], y[k], n2);
     }
+    if constexpr (Mk<D>::F16)  // the norm bound of the f16 scheme
+      ok = i < M && g > 0.0 && sqrt(n2) <= 2040.0 * g;
+  }
+  if constexpr (Mk<D>::F16) {
+    unsigned short y1[D], r2[D], r3[D], r2h[D], h[2], l[2];
+    unsigned short kpow = kF16One;
+    if (ok) {
+      const int K = f16_shift(g);
+      kpow = f16_bits(ldexpf(1.0f, K));
+      const double n2 = split_row_f16<D>(y, g, 2.0f, y1, r2, r3, r2h);
+      split_value_f16(-n2, g * g, K, h, l);
+    } else {  // padding / out-of-grid row: e = -inf, exact fixup if i < M
+#pragma unroll
+      for (int k = 0; k < D; ++k) y1[k] = r2[k] = r3[k] = r2h[k] = 0;
+      h[0] = kF16NegInf;
+      h[1] = l[0] = l[1] = 0;
+    }
+    store_frags_f16<D, false>(B, i, y1, r2, r3, r2h, h, l, kpow);
+    return;
   }
   unsigned short y1[D], y2[D], y3[D], h[3], l[2];
   if (ok) {
@@ -297,6 +507,27 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     h[1] = h[2] = l[0] = l[1] = 0;
   }
   store_frags<D, false>(B, i, y1, y2, y3, h, l);
+}
+
+// the 32x32x16 MFMA of the piece scheme: f16 (d > 8) or bf16 (d <= 8); the
+// fragments are 16-bit patterns either way
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma_op(const bf16x8& a, const bf16x8& b,
+                                          const f32x16& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// e = hi + lo, rounded once (the f16 lo accumulator carries 2^10)
+template <bool F16>
+__device__ __forceinline__ float combine(float hi, float lo) {
+  if constexpr (F16)
+    return __builtin_fmaf(lo, kF16LoUnscale, hi);
+  else
+    return hi + lo;
 }
 
 // Folded accumulation (KL <= kFoldKL, i.e. D <= 8, the VALU-bound shapes):
@@ -315,34 +546,35 @@ constexpr int kFoldKL = 4;
 
 // one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
 // folded e in hi
-template <int KH, int KL>
+// folded: the bf16 scheme with few lo chunks (d <= 8)
+template <int KL, bool F16>
+constexpr bool kFolded = !F16 && KL <= kFoldKL;
+
+template <int KH, int KL, bool F16>
 __device__ __forceinline__ void mfma_step(const bf16x8* a, const bf16x8* b,
                                           f32x16& hi, f32x16& lo) {
   hi = f32x16{};
 #pragma unroll
-  for (int c = 0; c < KH; ++c)
-    hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], b[c], hi, 0, 0, 0);
-  if constexpr (KL <= kFoldKL) {
+  for (int c = 0; c < KH; ++c) hi = mfma_op<F16>(a[c], b[c], hi);
+  if constexpr (kFolded<KL, F16>) {
 #pragma unroll
-    for (int c = 0; c < KL; ++c)
-      hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], hi, 0,
-                                                   0, 0);
+    for (int c = 0; c < KL; ++c) hi = mfma_op<F16>(a[KH + c], b[KH + c], hi);
   } else {
     lo = f32x16{};
 #pragma unroll
-    for (int c = 0; c < KL; ++c)
-      lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[KH + c], b[KH + c], lo, 0,
-                                                   0, 0);
+    for (int c = 0; c < KL; ++c) lo = mfma_op<F16>(a[KH + c], b[KH + c], lo);
   }
 }
 
 // sum of 2^(hi+lo) over the lane's 16 values: 16 independent exps, then a
 // fixed pairwise tree (v, v+8), (v, v+4), (v, v+2), (v, v+1)
+template <bool F16>
 __device__ __forceinline__ float tile_sum_split(const f32x16& hi,
                                                 const f32x16& lo) {
   float e[16];
 #pragma unroll
-  for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(hi[v] + lo[v]);
+  for (int v = 0; v < 16; ++v)
+    e[v] = __builtin_amdgcn_exp2f(combine<F16>(hi[v], lo[v]));
 #pragma unroll
   for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
@@ -351,10 +583,10 @@ __device__ __forceinline__ float tile_sum_split(const f32x16& hi,
 }
 
 // the same after mfma_step (folded: e is in hi)
-template <int KL>
+template <int KL, bool F16>
 __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
-  if constexpr (KL > kFoldKL) {
-    return tile_sum_split(hi, lo);
+  if constexpr (!kFolded<KL, F16>) {
+    return tile_sum_split<F16>(hi, lo);
   } else {
     float e[16];
 #pragma unroll
@@ -371,7 +603,7 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB, bool PIPE>
+template <int KH, int KL, int IB, bool PIPE, bool F16>
 __device__ __forceinline__ void kde_mfma_body(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -421,17 +653,17 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
         f32x16 hi[2], lo[2];
-        mfma_step<KH, KL>(a[0], bq[0], hi[0], lo[0]);
+        mfma_step<KH, KL, F16>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           if (q + 1 < 2 * IB)
-            mfma_step<KH, KL>(a[(q + 1) / IB], bq[(q + 1) % IB],
-                              hi[(q + 1) & 1], lo[(q + 1) & 1]);
+            mfma_step<KH, KL, F16>(a[(q + 1) / IB], bq[(q + 1) % IB],
+                                   hi[(q + 1) & 1], lo[(q + 1) & 1]);
           if (q + 1 == IB) {  // last MFMA reading tile 0 is issued
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += tile_sum<KL>(hi[q & 1], lo[q & 1]);
+          sacc[q % IB] += tile_sum<KL, F16>(hi[q & 1], lo[q & 1]);
         }
       } else {
 #pragma unroll
@@ -439,8 +671,8 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
-          mfma_step<KH, KL>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += tile_sum<KL>(hi, lo);
+          mfma_step<KH, KL, F16>(a[q / IB], bq[q % IB], hi, lo);
+          sacc[q % IB] += tile_sum<KL, F16>(hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -459,12 +691,12 @@ __device__ __forceinline__ void kde_mfma_body(
   }
 }
 
-template <int KH, int KL, int IB, bool PIPE>
+template <int KH, int KL, int IB, bool PIPE, bool F16>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  kde_mfma_body<KH, KL, IB, PIPE>(Bfr, M, Afr, npad, split, spb, jseg,
-                                         partial);
+  kde_mfma_body<KH, KL, IB, PIPE, F16>(Bfr, M, Afr, npad, split, spb, jseg,
+                                       partial);
 }
 
 // MFMA-bound form for d > 8.  Per 32x32 tile a wave runs KT = KH + KL
@@ -481,7 +713,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
 // arithmetic and summation order are those of kde_mfma_body (split hi / lo
 // accumulators, tile 0 then tile 1 of each chunk): the rows are
 // bit-identical to kde_mfma_kernel's.
-template <int KH, int KL, int IB>
+template <int KH, int KL, int IB, bool F16>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -543,11 +775,9 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
 #pragma unroll
           for (int t = 0; t < IB; ++t) {
             if (c < KH)
-              hi[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t][c], hi[t],
-                                                              0, 0, 0);
+              hi[t] = mfma_op<F16>(a, bq[t][c], hi[t]);
             else
-              lo[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[t][c], lo[t],
-                                                              0, 0, 0);
+              lo[t] = mfma_op<F16>(a, bq[t][c], lo[t]);
           }
           // one fragment read ahead of its IB MFMAs, no early hoisting
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -555,7 +785,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
         }
 #pragma unroll
         for (int t = 0; t < IB; ++t)
-          sacc[t] += tile_sum_split(hi[t], lo[t]);
+          sacc[t] += tile_sum_split<F16>(hi[t], lo[t]);
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
@@ -619,12 +849,12 @@ struct SplitPlan {
   static constexpr int a0(int g) { return g * NA / GA; }
   static constexpr int s0(int g) { return (g - GA) * NS / (NG - GA); }
 };
-template <int KT, int KH, int IB, int Q, int QE>
+template <int KT, int KH, int IB, bool F16, int Q, int QE>
 __device__ __forceinline__ void split_add_ops(f32x16 (&h)[IB],
                                               const f32x16 (&l)[IB]) {
   if constexpr (Q < QE) {
-    h[Q / 16][Q % 16] += l[Q / 16][Q % 16];
-    split_add_ops<KT, KH, IB, Q + 1, QE>(h, l);
+    h[Q / 16][Q % 16] = combine<F16>(h[Q / 16][Q % 16], l[Q / 16][Q % 16]);
+    split_add_ops<KT, KH, IB, F16, Q + 1, QE>(h, l);
   }
 }
 template <int IB, int Q, int QE>
@@ -634,12 +864,12 @@ __device__ __forceinline__ void split_sum_ops(f32x16 (&h)[IB], float (&sacc)[IB]
     split_sum_ops<IB, Q + 1, QE>(h, sacc);
   }
 }
-template <int KT, int KH, int IB, int G>
+template <int KT, int KH, int IB, bool F16, int G>
 __device__ __forceinline__ void split_gap_ops(f32x16 (&h)[IB], const f32x16 (&l)[IB],
                                               float (&sacc)[IB]) {
   using P = SplitPlan<KT, KH, IB>;
   if constexpr (G < P::GA) {
-    split_add_ops<KT, KH, IB, P::a0(G), P::a0(G + 1)>(h, l);
+    split_add_ops<KT, KH, IB, F16, P::a0(G), P::a0(G + 1)>(h, l);
   } else {
     split_sum_ops<IB, P::s0(G), P::s0(G + 1)>(h, sacc);
   }
@@ -649,7 +879,7 @@ __device__ __forceinline__ void split_gap_ops(f32x16 (&h)[IB], const f32x16 (&l)
 // this tile's hi accumulators; prev: the retiring tile's; lo: the lo
 // accumulators (read as the retiring tile's lo by the first gaps, then
 // overwritten by this chain).
-template <int KT, int KH, int IB, bool VALU, int C = 0>
+template <int KT, int KH, int IB, bool F16, bool VALU, int C = 0>
 __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int lane,
                                           const bf16x8 (&bq)[IB][KT],
                                           f32x16 (&acc)[IB], f32x16 (&prev)[IB],
@@ -662,17 +892,15 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
       if (C >= KH)
-        lo[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            a[C & 1], bq[t][C], C == KH ? f32x16{} : lo[t], 0, 0, 0);
+        lo[t] = mfma_op<F16>(a[C & 1], bq[t][C], C == KH ? f32x16{} : lo[t]);
       else
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t], 0, 0, 0);
+        acc[t] = mfma_op<F16>(a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VALU) {
         // t is a compile-time constant after unrolling; each branch names
         // its gap index
 #define ABC_GAP(TT) \
-  if (t == TT) split_gap_ops<KT, KH, IB, C * IB + TT>(prev, lo, sacc);
+  if (t == TT) split_gap_ops<KT, KH, IB, F16, C * IB + TT>(prev, lo, sacc);
         ABC_GAP(0)
         ABC_GAP(1)
         ABC_GAP(2)
@@ -681,8 +909,8 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
       }
     }
     a[C & 1] = nxt;
-    lds_chain<KT, KH, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, lo, sacc,
-                                        a);
+    lds_chain<KT, KH, IB, F16, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, lo,
+                                             sacc, a);
   }
 }
 
@@ -692,7 +920,7 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
 // (The folded accumulation in the same schedule ran 16.8 ms but its error
 // reached 6.3e-6 at N = M = 1e6 against 1.5e-6 -- DESIGN.md section 4 --
 // and was dropped.)
-template <int KH, int KL, int IB>
+template <int KH, int KL, int IB, bool F16>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -746,9 +974,11 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
       a[0] = Ab[0][lane];
       a[1] = Ab[1][lane];
       if (jc == 0) {  // tile 0, nothing to retire yet
-        lds_chain<KT, KH, IB, false>(Ab, 0, lane, bq, accA, accB, lo, sprev, a);
+        lds_chain<KT, KH, IB, F16, false>(Ab, 0, lane, bq, accA, accB, lo, sprev,
+                                          a);
       } else {        // tile 0 || tile 1 of the previous chunk
-        lds_chain<KT, KH, IB, true>(Ab, 0, lane, bq, accA, accB, lo, sprev, a);
+        lds_chain<KT, KH, IB, F16, true>(Ab, 0, lane, bq, accA, accB, lo, sprev,
+                                         a);
 #pragma unroll
         for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
       }
@@ -757,7 +987,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
       a[0] = Ab[KT][lane];
       a[1] = Ab[KT + 1][lane];
       // tile 1 || tile 0 of this chunk
-      lds_chain<KT, KH, IB, true>(Ab, 1, lane, bq, accB, accA, lo, scur, a);
+      lds_chain<KT, KH, IB, F16, true>(Ab, 1, lane, bq, accB, accA, lo, scur, a);
 #pragma unroll
       for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
       buf ^= 1;
@@ -765,7 +995,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
     if (nj > 0) {  // retire the last tile
 #pragma unroll
       for (int t = 0; t < IB; ++t)
-        sprev[t] += tile_sum_split(accB[t], lo[t]);
+        sprev[t] += tile_sum_split<F16>(accB[t], lo[t]);
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
     }
@@ -894,7 +1124,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
     }
     if (nj > 0) {
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL>(accB[t], accB[t]);
+      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL, false>(accB[t], accB[t]);
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
     }
@@ -996,13 +1226,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // register kernel); 0: the register kernel.  Rows bit-identical.
     const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
     if (lds2 == 2) {
-      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::F16>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
     }
     if (lds2 != 0) {
-      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::F16>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
@@ -1021,11 +1251,11 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   // software pipelining pays at D <= 8 (VALU-bound); at larger D the MFMA
   // chain dominates and the lower register count wins (bench_kde sweep)
   if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
-    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true>),
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, Mk<D>::F16>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
   else
-    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false>),
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false, Mk<D>::F16>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
 }

@@ -922,7 +922,15 @@ struct SegState {
   int compacted;        // the remaining passes read the candidate buffer
   int fresh;            // compacted by the pass that just ended
   int next_done;        // knext found among the candidates
-  int pad;
+  int done;             // answered by the bracket select (bs_*): the radix
+                        // passes skip the column
+  // bracket select
+  long long r_lo, r_hi;           // sample ranks bracketing the target
+  unsigned long long p_lo, p_hi;  // their key prefixes (12, then 24 bits)
+  unsigned long long lo_key, hi_key;
+  unsigned long long c_below;     // column keys < lo_key
+  unsigned long long kabove;      // smallest column key > hi_key
+  unsigned long long cmin, cmax;  // smallest / largest key inside
 };
 
 // After 24 (or, failing that, 32) key bits a column's selected bucket is
@@ -951,7 +959,7 @@ __global__ __launch_bounds__(256) void seg_hist_kernel(
   constexpr int NB = 1 << BITS;
   __shared__ unsigned hc[NB];
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
-  if (st[s].compacted) return;   // block-uniform: seg_hist_cand_kernel's
+  if (st[s].compacted || st[s].done) return;   // seg_hist_cand_kernel's
   for (int b = threadIdx.x; b < NB; b += 256) hc[b] = 0;
   __syncthreads();
   const unsigned long long prefix = st[s].prefix;
@@ -1007,6 +1015,7 @@ __global__ __launch_bounds__(256) void seg_select_kernel(SegState* st, int shift
   constexpr int NB = 1 << BITS, PER = NB / 256;
   __shared__ long long sc[256];
   const int s = blockIdx.x, t = threadIdx.x;
+  if (st[s].done) return;
   unsigned* h = hist + static_cast<int64_t>(s) * NB + t * PER;
   long long v[PER];
   long long tot = 0;
@@ -1055,12 +1064,17 @@ __global__ void seg_init_kernel(SegState* st, int S, long long rank) {
   st[s].compacted = 0;
   st[s].fresh = 0;
   st[s].next_done = 0;
+  st[s].done = 0;
+  st[s].c_below = 0;
+  st[s].kabove = ~0ull;
+  st[s].cmin = ~0ull;
+  st[s].cmax = 0;
 }
 
 __global__ void seg_mark_kernel(SegState* st, int S) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
-  const int now = !st[s].compacted && st[s].cand <= kCandCap;
+  const int now = !st[s].done && !st[s].compacted && st[s].cand <= kCandCap;
   st[s].fresh = now;
   if (now) st[s].compacted = 1;
 }
@@ -1114,7 +1128,7 @@ __global__ __launch_bounds__(256) void seg_hist_cand_kernel(
     int shift, unsigned long long mask, unsigned* __restrict__ hist) {
   __shared__ unsigned hc[kBins];
   const int s = blockIdx.x;
-  if (!st[s].compacted) return;
+  if (!st[s].compacted || st[s].done) return;
   hc[threadIdx.x] = 0;
   __syncthreads();
   const unsigned long long prefix = st[s].prefix;
@@ -1133,7 +1147,7 @@ __global__ __launch_bounds__(256) void seg_next_kernel(
     const double* __restrict__ data, int64_t ld, int64_t n, int bps,
     const double* __restrict__ center, SegState* st) {
   const int s = blockIdx.x / bps, part = blockIdx.x % bps;
-  if (st[s].next_done) return;
+  if (st[s].next_done || st[s].done) return;
   const unsigned long long key = st[s].prefix;
   const double c = MODE == 1 ? center[s] : 0.0;
   const double* col = data + static_cast<int64_t>(s) * ld;
@@ -1167,7 +1181,7 @@ __global__ __launch_bounds__(256) void seg_next_cand_kernel(
     SegState* st, const unsigned long long* __restrict__ cbuf) {
   __shared__ unsigned long long red[4];
   const int s = blockIdx.x;
-  if (!st[s].compacted) return;
+  if (!st[s].compacted || st[s].done) return;
   const unsigned long long key = st[s].prefix;
   const long long cnt = static_cast<long long>(st[s].ccount);
   const unsigned long long* keys = cbuf + static_cast<int64_t>(s) * kCandCap;
@@ -1197,7 +1211,7 @@ __global__ __launch_bounds__(256) void seg_next_cand_kernel(
 __global__ void seg_median_kernel(const SegState* st, int S, int64_t n,
                                   double* __restrict__ out) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= S) return;
+  if (s >= S || st[s].done) return;
   const double a = key_f64(st[s].prefix);
   if (n & 1) {
     out[s] = a;
@@ -1207,6 +1221,337 @@ __global__ void seg_median_kernel(const SegState* st, int S, int64_t n,
   const bool same = st[s].less + st[s].eq > k + 1;
   const double b = same ? a : key_f64(st[s].knext);
   out[s] = (a + b) / 2.0;
+}
+
+// ---------------------------------------------------------------------------
+// bracket select (round 4): one read of the column per order statistic
+// ---------------------------------------------------------------------------
+// The statistics columns hold independent draws in evaluation order, so
+// their first M entries are a random sample of the column.  Two 12-bit
+// digit passes over that sample (M = n/16 ... , ~6 % of a column) find the
+// 24-bit key buckets of the sample ranks k M / n -+ 4.5 sigma; ONE read of
+// the column then counts the keys below the bracket, compacts the keys
+// inside it (~1-2 % of the column: 22k at n = 2e6) and finds the smallest
+// key above it; one block per column selects rank k (and k + 1 for even n)
+// among the candidates.  The answer is exact whatever the sample: a column
+// whose bracket misses rank k, or holds more than kCandCap keys of more
+// than one value (sorted columns, heavy ties), keeps done = 0 and takes the
+// radix passes above.
+constexpr int kBsBins = 4096;
+constexpr int kBsWaveBuf = 1024;        // compaction buffer per wave (keys)
+
+__host__ __device__ inline int64_t bs_sample_size(int64_t n) {
+  int64_t m = n / 16;
+  const int64_t q = n / 8192;
+  if (q * q > m) m = q * q;            // keeps n 4.5 / sqrt(M) under the cap
+  if (m < 65536) m = 65536;
+  return m < n ? m : n;
+}
+
+// 12-bit digit histograms of the sample's keys: pass 0 the leading digit,
+// pass 1 the second digit below each of the two selected leading digits
+template <int MODE>
+__global__ __launch_bounds__(256) void bs_hist_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t m, int sbps,
+    const double* __restrict__ center, const SegState* __restrict__ st,
+    int pass, unsigned* __restrict__ hist) {
+  __shared__ unsigned hc[2 * kBsBins];
+  const int s = blockIdx.x / sbps, part = blockIdx.x % sbps;
+  for (int b = threadIdx.x; b < 2 * kBsBins; b += 256) hc[b] = 0;
+  __syncthreads();
+  const double c = MODE == 1 ? center[s] : 0.0;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  const unsigned long long plo = st[s].p_lo, phi = st[s].p_hi;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = static_cast<int64_t>(sbps) * 256;
+  for (int64_t i0 = static_cast<int64_t>(part) * 256; i0 < m; i0 += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      v[u] = i < m ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      if (i >= m) continue;
+      const uint64_t k = seg_key<MODE>(v[u], c);
+      const unsigned top = static_cast<unsigned>(k >> 52);
+      if (pass == 0) {
+        // wave-aggregated: most keys of a column share the leading digit
+        const unsigned long long act = __ballot(true);
+        const int leader = __ffsll(static_cast<long long>(act)) - 1;
+        const unsigned lb = __shfl(top, leader, 64);
+        if (__ballot(top == lb) == act) {
+          if (lane == leader) atomicAdd(&hc[lb], static_cast<unsigned>(__popcll(act)));
+        } else {
+          atomicAdd(&hc[top], 1u);
+        }
+      } else {
+        const unsigned mid = static_cast<unsigned>(k >> 40) & (kBsBins - 1);
+        if (top == plo) atomicAdd(&hc[mid], 1u);
+        if (top == phi) atomicAdd(&hc[kBsBins + mid], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const int nb = pass == 0 ? kBsBins : 2 * kBsBins;
+  for (int b = threadIdx.x; b < nb; b += 256)
+    if (hc[b]) atomicAdd(&hist[static_cast<int64_t>(s) * 2 * kBsBins + b], hc[b]);
+}
+
+// digit of rank r in a 4096-bin histogram (256 threads, 16 bins each):
+// returns the digit and the rank inside it (block-uniform)
+__device__ inline void bs_find(const unsigned* h, long long r, long long* sc,
+                               int* dig, long long* rem) {
+  constexpr int PER = kBsBins / 256;
+  const int t = threadIdx.x;
+  long long v[PER], tot = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = h[t * PER + j];
+    tot += v[j];
+  }
+  __syncthreads();
+  sc[t] = tot;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const long long a = t >= o ? sc[t - o] : 0;
+    __syncthreads();
+    sc[t] += a;
+    __syncthreads();
+  }
+  long long run = sc[t] - tot;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if (v[j] > 0 && run <= r && r < run + v[j]) {
+      sc[0] = t * PER + j;
+      sc[1] = r - run;
+    }
+    run += v[j];
+  }
+  __syncthreads();
+  *dig = static_cast<int>(sc[0]);
+  *rem = sc[1];
+  __syncthreads();
+}
+
+// pass 0: sample ranks -> leading digits; pass 1: -> 24-bit buckets and the
+// key bracket [lo_key, hi_key]; clears the histograms
+__global__ __launch_bounds__(256) void bs_select_kernel(SegState* st, int64_t n,
+                                                        int64_t m, int pass,
+                                                        unsigned* __restrict__ hist) {
+  __shared__ long long sc[256];
+  const int s = blockIdx.x;
+  unsigned* h = hist + static_cast<int64_t>(s) * 2 * kBsBins;
+  if (pass == 0) {
+    // rank k = (n - 1) / 2 (and k + 1 for even n) at sample scale, +-4.5 sd
+    const double k = static_cast<double>((n - 1) / 2);
+    const double c = (k + 1.0) * static_cast<double>(m) / static_cast<double>(n);
+    const double w = 4.5 * 0.5 * sqrt(static_cast<double>(m)) + 2.0;
+    long long rl = static_cast<long long>(floor(c - w));
+    long long rh = static_cast<long long>(ceil(c + w));
+    if (rl < 0) rl = 0;
+    if (rh > m - 1) rh = m - 1;
+    if (m == n) rl = rh = (n - 1) / 2;       // the sample is the column
+    int dl, dh;
+    long long el, eh;
+    bs_find(h, rl, sc, &dl, &el);
+    bs_find(h, rh, sc, &dh, &eh);
+    if (threadIdx.x == 0) {
+      st[s].p_lo = static_cast<unsigned long long>(dl);
+      st[s].p_hi = static_cast<unsigned long long>(dh);
+      st[s].r_lo = el;
+      st[s].r_hi = eh;
+    }
+    for (int b = threadIdx.x; b < kBsBins; b += 256) h[b] = 0;
+  } else {
+    int dl, dh;
+    long long el, eh;
+    bs_find(h, st[s].r_lo, sc, &dl, &el);
+    bs_find(h + kBsBins, st[s].r_hi, sc, &dh, &eh);
+    if (threadIdx.x == 0) {
+      const unsigned long long pl = (st[s].p_lo << 12) | static_cast<unsigned>(dl);
+      const unsigned long long ph = (st[s].p_hi << 12) | static_cast<unsigned>(dh);
+      st[s].lo_key = pl << 40;
+      st[s].hi_key = (ph << 40) | ((1ull << 40) - 1ull);
+      st[s].ccount = 0;
+    }
+    for (int b = threadIdx.x; b < 2 * kBsBins; b += 256) h[b] = 0;
+  }
+}
+
+// ONE read of the column: keys below the bracket (count), inside it
+// (compacted: a buffer per wave in LDS, flushed with one global atomic per
+// 1024 keys), the smallest key above it
+template <int MODE>
+__global__ __launch_bounds__(256) void bs_full_kernel(
+    const double* __restrict__ data, int64_t ld, int64_t n, int bps,
+    const double* __restrict__ center, SegState* st,
+    unsigned long long* __restrict__ cbuf) {
+  __shared__ unsigned long long wbuf[4][kBsWaveBuf];
+  const int s = blockIdx.x / bps, part = blockIdx.x % bps;
+  const double c = MODE == 1 ? center[s] : 0.0;
+  const double* col = data + static_cast<int64_t>(s) * ld;
+  const unsigned long long lo = st[s].lo_key, hi = st[s].hi_key;
+  unsigned long long* out = cbuf + static_cast<int64_t>(s) * kCandCap;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long* buf = wbuf[wv];
+  unsigned fill = 0;                 // wave-uniform
+  unsigned long long below = 0, kab = ~0ull, cmn = ~0ull, cmx = 0;
+  const int64_t stride = static_cast<int64_t>(bps) * 256;
+  auto flush = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&st[s].ccount, static_cast<unsigned long long>(fill));
+    base = __shfl(base, 0, 64);
+    for (unsigned j = lane; j < fill; j += 64)
+      if (base + j < static_cast<unsigned long long>(kCandCap)) out[base + j] = buf[j];
+    fill = 0;
+  };
+  for (int64_t i0 = static_cast<int64_t>(part) * 256; i0 < n; i0 += 4 * stride) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      v[u] = i < n ? col[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride + threadIdx.x;
+      const uint64_t k = seg_key<MODE>(v[u], c);
+      const bool ok = i < n;
+      below += (ok && k < lo) ? 1u : 0u;
+      if (ok && k > hi && k < kab) kab = k;
+      const bool in = ok && k >= lo && k <= hi;
+      const unsigned long long msk = __ballot(in);
+      if (msk == 0ull) continue;
+      if (in) {
+        buf[fill + __popcll(msk & ((1ull << lane) - 1ull))] = k;
+        cmn = k < cmn ? k : cmn;
+        cmx = k > cmx ? k : cmx;
+      }
+      fill += static_cast<unsigned>(__popcll(msk));
+    }
+    if (fill > kBsWaveBuf - 4 * 64) flush();  // room for one more trip
+  }
+  if (fill) flush();
+  below = wave_sum(below);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(kab, o, 64);
+    kab = b < kab ? b : kab;
+    const unsigned long long e = __shfl_xor(cmn, o, 64);
+    cmn = e < cmn ? e : cmn;
+    const unsigned long long f = __shfl_xor(cmx, o, 64);
+    cmx = f > cmx ? f : cmx;
+  }
+  if (lane == 0) {
+    if (below) atomicAdd(&st[s].c_below, below);
+    if (kab != ~0ull) atomicMin(&st[s].kabove, kab);
+    if (cmn != ~0ull) {
+      atomicMin(&st[s].cmin, cmn);
+      atomicMax(&st[s].cmax, cmx);
+    }
+  }
+}
+
+// one block per column: rank k (and k + 1) among the bracket's candidates
+// by 8-bit digit passes below the bracket's common key prefix; the result
+// (np.median / MAD semantics as seg_median_kernel) and done = 1, or nothing
+// when the bracket does not hold rank k / holds too many keys
+__global__ __launch_bounds__(1024) void bs_cand_kernel(SegState* st, int64_t n,
+                                                       const unsigned long long* __restrict__ cbuf,
+                                                       double* __restrict__ out) {
+  __shared__ unsigned hc[256];
+  __shared__ unsigned long long sh[4];
+  __shared__ unsigned long long red[16];
+  const int s = blockIdx.x, t = threadIdx.x;
+  const long long k = (n - 1) / 2;
+  const long long below = static_cast<long long>(st[s].c_below);
+  const long long cin = static_cast<long long>(st[s].ccount);
+  const unsigned long long lo = st[s].cmin, hi = st[s].cmax;
+  const bool one_key = lo == hi;                       // ties only
+  // the bracket missed rank k, or holds too many keys: the radix passes
+  // take the column (their compaction counter starts from 0 again)
+  if (k < below || k >= below + cin || (cin > kCandCap && !one_key)) {
+    if (t == 0) st[s].ccount = 0;
+    return;
+  }
+  const unsigned long long* keys = cbuf + static_cast<int64_t>(s) * kCandCap;
+  unsigned long long a = lo, b = lo;
+  long long eq = cin;
+  long long r = k - below;
+  if (!one_key) {
+    const int common = __clzll(static_cast<long long>(lo ^ hi));  // shared bits
+    unsigned long long prefix = lo & (common ? (~0ull << (64 - common)) : 0ull);
+    int consumed = common;
+    while (consumed < 64) {
+      const int bits = 64 - consumed < 8 ? 64 - consumed : 8;
+      const int shift = 64 - consumed - bits;
+      const unsigned long long mask = consumed ? (~0ull << (64 - consumed)) : 0ull;
+      if (t < 256) hc[t] = 0;
+      __syncthreads();
+      for (long long i = t; i < cin; i += 1024) {
+        const unsigned long long kk = keys[i];
+        if (((kk ^ prefix) & mask) == 0)
+          atomicAdd(&hc[(kk >> shift) & ((1u << bits) - 1u)], 1u);
+      }
+      __syncthreads();
+      if (t == 0) {
+        long long run = 0;
+        for (int j = 0; j < (1 << bits); ++j) {
+          if (hc[j] && run <= r && r < run + hc[j]) {
+            sh[0] = static_cast<unsigned long long>(j);
+            sh[1] = static_cast<unsigned long long>(run);
+            sh[2] = hc[j];
+            break;
+          }
+          run += hc[j];
+        }
+      }
+      __syncthreads();
+      prefix |= sh[0] << shift;
+      r -= static_cast<long long>(sh[1]);
+      eq = static_cast<long long>(sh[2]);
+      consumed += bits;
+      __syncthreads();
+    }
+    a = prefix;
+    // k + 1 (even n): the same key while the tie run lasts, else the
+    // smallest candidate above a, else the smallest column key above hi
+    if ((n & 1) == 0 && r + 1 >= eq) {
+      unsigned long long kn = ~0ull;
+      for (long long i = t; i < cin; i += 1024) {
+        const unsigned long long kk = keys[i];
+        if (kk > a && kk < kn) kn = kk;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long e = __shfl_xor(kn, o, 64);
+        kn = e < kn ? e : kn;
+      }
+      if ((t & 63) == 0) red[t >> 6] = kn;
+      __syncthreads();
+      if (t == 0) {
+        for (int w = 1; w < 16; ++w) kn = red[w] < kn ? red[w] : kn;
+        red[0] = kn;
+      }
+      __syncthreads();
+      kn = red[0];
+      b = kn != ~0ull ? kn : st[s].kabove;
+    } else {
+      b = a;
+    }
+  } else if ((n & 1) == 0 && k + 1 >= below + cin) {
+    b = st[s].kabove;                                  // one key, run ends at k
+  }
+  if (t == 0) {
+    const double va = key_f64(a);
+    out[s] = (n & 1) ? va : (va + key_f64(b)) / 2.0;
+    st[s].done = 1;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1635,7 +1980,7 @@ int abc_wquantile_f64(const double* d, const double* w, int64_t n, double alpha,
 
 size_t abc_column_select_workspace_bytes(int S) {
   return static_cast<size_t>(S) * (sizeof(SegState) + kWideBins * 4 +
-                                   kCandCap * 8) + 256;
+                                   2 * kBsBins * 4 + kCandCap * 8) + 256;
 }
 
 // median (and MAD when mad_out != NULL) of every column of data_T[S][ld]
@@ -1648,9 +1993,11 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
   SegState* sst = static_cast<SegState*>(ws);
   unsigned* hist = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
                                                static_cast<size_t>(S) * sizeof(SegState));
+  unsigned* bhist = hist + static_cast<size_t>(S) * kWideBins;
   unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
-      hist + static_cast<size_t>(S) * kWideBins);
-  ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * kWideBins * 4, st));
+      bhist + static_cast<size_t>(S) * 2 * kBsBins);
+  ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * (kWideBins + 2 * kBsBins) * 4,
+                         st));
   int bps = static_cast<int>(ceil_div(2048, S));
   const int64_t maxb = ceil_div(n, 256);
   if (bps > maxb) bps = static_cast<int>(maxb);
@@ -1661,6 +2008,28 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
     double* out = round == 0 ? median_out : mad_out;
     hipLaunchKernelGGL(seg_init_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, st,
                        sst, S, k);
+    // bracket select: sample digits, one read of each column, candidates
+    const int64_t m = bs_sample_size(n);
+    int sbps = static_cast<int>(ceil_div(m, 1024));
+    if (sbps > bps) sbps = bps;
+    for (int pass = 0; pass < 2; ++pass) {
+      if (round == 0)
+        hipLaunchKernelGGL(bs_hist_kernel<0>, dim3(S * sbps), dim3(256), 0, st,
+                           data_T, ld, m, sbps, center, sst, pass, bhist);
+      else
+        hipLaunchKernelGGL(bs_hist_kernel<1>, dim3(S * sbps), dim3(256), 0, st,
+                           data_T, ld, m, sbps, center, sst, pass, bhist);
+      hipLaunchKernelGGL(bs_select_kernel, dim3(S), dim3(256), 0, st, sst, n, m, pass,
+                         bhist);
+    }
+    if (round == 0)
+      hipLaunchKernelGGL(bs_full_kernel<0>, dim3(S * bps), dim3(256), 0, st, data_T,
+                         ld, n, bps, center, sst, cbuf);
+    else
+      hipLaunchKernelGGL(bs_full_kernel<1>, dim3(S * bps), dim3(256), 0, st, data_T,
+                         ld, n, bps, center, sst, cbuf);
+    hipLaunchKernelGGL(bs_cand_kernel, dim3(S), dim3(1024), 0, st, sst, n, cbuf, out);
+    // radix passes for the columns the bracket did not settle
     int consumed = 0;  // key bits selected so far
     for (int pass = 0; pass < kSegPasses; ++pass) {
       const int bits = kSegBits[pass];

@@ -88,7 +88,10 @@ DEVICE_SCALES = {median_absolute_deviation: "mad",
 class DeviceStats:
     """Recorded summary statistics on the device, stat-major [S, n] in x_0
     key order (what the reference gathers per key from a list of dicts,
-    distance.py:266-270)."""
+    distance.py:266-270).  ``stats_T`` is row-contiguous but its row stride
+    may exceed n (a one-round generation hands out a column slice of the
+    round's buffer): read it through (pointer, ``stats_T.stride(0)``), as
+    ``kernels._stat_major`` does."""
 
     def __init__(self, stats_T, keys):
         self.stats_T = stats_T

@@ -161,6 +161,18 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     return torch.cat(out) if out else allr[:0]
 
 
+def mirrors_simulate(model):
+    """True when ``model.simulate_distance`` is defined by the same class as
+    the ``simulate`` it mirrors: a subclass that overrides ``simulate``
+    (other noise, other statistics) without its own fused method is not
+    fused, so its distances always come from its own simulate()."""
+    def owner(name):
+        return next((c for c in type(model).__mro__ if name in c.__dict__),
+                    None)
+    o = owner("simulate_distance")
+    return o is not None and o is owner("simulate")
+
+
 def pnorm_host(x, x0, fw, p):
     """One particle's distance exactly as the reference evaluates it
     (distance/distance.py:88-100): Python floats, libm ``pow`` for every
@@ -459,7 +471,7 @@ class GenerationEngine:
             fuse = (nv and not keep_stats and not record
                     and self.fuse_sim_distance
                     and isinstance(acceptance, PNormAcceptance)
-                    and hasattr(self.model, "simulate_distance"))
+                    and mirrors_simulate(self.model))
             if nv and not fuse:
                 stats = self.model.simulate(theta, self.seed, sim_sid,
                                             my_eval)
@@ -624,7 +636,11 @@ class GenerationEngine:
         return gather_segments(self.comm, pieces, row_shape, counts, self.dev)
 
     def _gather_cols(self, pieces, counts):
-        """Stat-major [S, cols] version of :meth:`_gather` (contiguous)."""
+        """Stat-major [S, cols] version of :meth:`_gather`.  Row-contiguous
+        with any row stride: a single round's piece is returned as the
+        column slice of that round's [S, B] buffer itself (no copy), so
+        consumers take (pointer, ``stride(0)``) -- the kernels do, through
+        ``kernels._stat_major`` -- and never assume ``stride(0) == cols``."""
         S = self.model.n_stats
         if not self.comm.active:
             if len(pieces) == 1:

@@ -591,3 +591,39 @@ def test_columnar_population_reference_api_gpu(pa):
     dist.initialize(0, lambda: [], x_0)
     check_population_api(ref, col, dist, x_0)
     assert col.d.is_cuda
+
+
+def test_single_round_recorded_stats_stride(pa):
+    """A generation that closes in one sampling round hands out its recorded
+    statistics as a column slice of the round's [S, B] buffer (row stride
+    B, engine._gather_cols): an AdaptivePNormDistance update over it (MAD
+    scales, distances) equals the update over a contiguous copy bit for bit."""
+    import math
+    from pyabc_amd import kernels as K
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.distance import DeviceStats
+    from pyabc_amd.engine import DeviceMVNFit, GenerationEngine
+    d, S, n = 3, 12, 3000
+    model = LinearGaussianModel.benchmark(d, S)
+    x0 = torch.as_tensor(model._x0, device="cuda")
+    fw = torch.ones(S, dtype=torch.float64, device="cuda")
+    eng = GenerationEngine(model, np.full(d, -5.0), np.full(d, 10.0),
+                           seed=3, min_batch=1 << 16)
+    r0 = eng.sample_prior(0, n)
+    d0, _, _ = K.pnorm_distance(r0.stats_T, x0, fw, 2.0, math.inf,
+                                with_accept=False)
+    w = torch.full((n,), 1.0 / n, dtype=torch.float64, device="cuda")
+    eps = float(K.weighted_quantile(d0, w, 0.5)[0].item())
+    res = eng.sample_generation(1, n, DeviceMVNFit(r0.theta, w), x0, fw, eps,
+                                keep_stats=True, record=True)
+    rec = res.rec_stats_T
+    assert rec.stride(0) > rec.shape[1], "expected one round's column slice"
+    keys = list(model.keys)
+    x0d = dict(zip(keys, model._x0))
+    out = []
+    for st in (rec, rec.contiguous()):
+        dist = pa.AdaptivePNormDistance(p=2)
+        dist.initialize(0, lambda: DeviceStats(r0.stats_T, keys), x0d)
+        dist.update(1, lambda: DeviceStats(st, keys))
+        out.append(np.array([dist.weights[1][k] for k in keys]))
+    np.testing.assert_array_equal(out[0], out[1])

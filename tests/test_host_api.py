@@ -303,3 +303,33 @@ def test_columnar_offload_finish_is_thread_safe():
         got = [r.result(timeout=10) for r in readers]
     assert got[0] == got[1] == float(th.sum())
     assert pop._pending is None
+
+
+def test_fused_path_only_for_the_mirrored_simulate():
+    """engine.mirrors_simulate: the fused simulate + distance kernel is used
+    only when simulate_distance comes from the class whose simulate it
+    mirrors -- a subclass overriding simulate() is never fused."""
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.engine import mirrors_simulate
+
+    class Noisier(LinearGaussianModel):
+        def simulate(self, theta, seed, sid, offset):  # pragma: no cover
+            return super().simulate(theta, seed, sid, offset) * 2.0
+
+    class Both(Noisier):
+        def simulate(self, theta, seed, sid, offset):  # pragma: no cover
+            return super().simulate(theta, seed, sid, offset)
+
+        def simulate_distance(self, *a):  # pragma: no cover
+            return None
+
+    class Stale(Both):   # simulate overridden again, the fused one inherited
+        def simulate(self, theta, seed, sid, offset):  # pragma: no cover
+            return super().simulate(theta, seed, sid, offset) + 1.0
+
+    m = LinearGaussianModel.benchmark(2, 3)
+    assert mirrors_simulate(m)
+    assert not mirrors_simulate(Noisier(m.A_host, m.sigma))
+    assert mirrors_simulate(Both(m.A_host, m.sigma))
+    assert not mirrors_simulate(Stale(m.A_host, m.sigma))
+    assert not mirrors_simulate(object())

@@ -9,7 +9,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
-         1: "d=20 split: 11 MFMA, 16 v_exp_f32, 40 v_add_f32"}
+         1: "d=20 split, bf16 pieces: 11 MFMA, 16 v_exp_f32, 40 v_add_f32",
+         2: "d=20 split, f16 pieces: 9 MFMA, 16 v_exp_f32, 40 v_add_f32"}
 
 
 def load():

@@ -15,6 +15,9 @@
 // Mixes (PMC-counted per tile, profiles/r0*_kde_pmc*.json):
 //   0: d <= 8, folded accumulation   -- 5 MFMA, 16 exp, 23 other VALU
 //   1: d = 20, split accumulation    -- 11 MFMA, 16 exp, 40 other VALU
+//      (the bf16 piece scheme of rounds 1-3)
+//   2: d = 20, f16 pieces (round 4)  --  9 MFMA, 16 exp, 40 other VALU
+//      (the f16 and bf16 32x32x16 MFMAs issue alike)
 //
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC issue_probe.hip \
 //         -o libabc_probe.so
@@ -106,6 +109,7 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
   switch (variant) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
     case 1: ns = time_mix<11, 16, 40>(waves_per_simd, iters, cus, out); break;
+    case 2: ns = time_mix<9, 16, 40>(waves_per_simd, iters, cus, out); break;
     default: break;
   }
   (void)hipFree(out);

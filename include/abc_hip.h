@@ -324,6 +324,15 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
                          double* out_logpdf, void* ws, size_t ws_bytes,
                          hipStream_t stream);
 size_t abc_local_logpdf_f32_workspace_bytes(int64_t M, int64_t N);
+/* the same density on the f16 matrix cores ("z form": q = |L^T (theta - X_n)|^2
+ * with inv_n = L L^T, the GEMM on exact-grid f16 pieces, local_mfma.hip;
+ * rows whose sum falls below 2^-32 are re-evaluated exactly in fp64) */
+int abc_local_logpdf_mfma(const double* pts, int64_t M, const double* X,
+                          const double* w, const double* inv_covs,
+                          const double* dets, int64_t N, int d,
+                          double* out_logpdf, void* ws, size_t ws_bytes,
+                          hipStream_t stream);
+size_t abc_local_logpdf_mfma_workspace_bytes(int64_t M, int64_t N, int d);
 /* LocalTransition.rvs_single                        local_transition.py:141-145
  * (CDF index as abc_propose_philox_f64; Cholesky factor of C[idx]) */
 int abc_propose_local_philox_f64(const double* X, int64_t N, int d,

@@ -163,6 +163,10 @@ _SIGS = {
                                      c_ptr, c_i64, c_int, c_ptr, c_ptr,
                                      c_size, c_ptr]),
     "abc_local_logpdf_f32_workspace_bytes": (c_size, [c_i64, c_i64]),
+    "abc_local_logpdf_mfma": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+                                      c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                      c_size, c_ptr]),
+    "abc_local_logpdf_mfma_workspace_bytes": (c_size, [c_i64, c_i64, c_int]),
     "abc_propose_local_philox_f64": (c_int, [c_ptr, c_i64, c_int, c_ptr,
                                              c_ptr, c_ptr, c_ptr, c_u64,
                                              c_u64, c_u64, c_i64, c_ptr,

@@ -480,16 +480,20 @@ def local_cov(X, w, nbr, scaling=1.0):
 
 
 def local_logpdf(pts, X, w, invs, dets, precision="f64"):
-    """log LocalTransition density; ``precision`` "f64" (1e-12) or "f32"
-    (pair loop in fp32, 1e-5 relative)."""
-    if precision not in ("f64", "f32"):
+    """log LocalTransition density; ``precision`` "f64" (1e-12), "f32"
+    (pair loop in fp32, 1e-5 relative) or "mfma" (z form on the f16 matrix
+    cores, 1e-5 relative)."""
+    if precision not in ("f64", "f32", "mfma"):
         raise ValueError(f"unknown LocalTransition precision {precision!r}")
     pts = _contig(pts, F64)
     M, d = pts.shape
     N = X.shape[0]
     out = torch.empty(M, dtype=F64, device=_dev())
-    wsb = getattr(nat.lib(), f"abc_local_logpdf{'_f32' if precision == 'f32' else ''}"
-                  "_workspace_bytes")(M, N)
+    if precision == "mfma":
+        wsb = nat.lib().abc_local_logpdf_mfma_workspace_bytes(M, N, d)
+    else:
+        wsb = getattr(nat.lib(), f"abc_local_logpdf{'_f32' if precision == 'f32' else ''}"
+                      "_workspace_bytes")(M, N)
     ws = WS.get(wsb, "localpdf")
     call(f"abc_local_logpdf_{precision}", ptr(pts), M, ptr(_contig(X, F64)),
          ptr(_contig(w, F64)), ptr(invs), ptr(dets), N, d, ptr(out), ptr(ws),

@@ -219,8 +219,9 @@ class LocalTransition(Transition):
     def __init__(self, k=None, k_fraction=1 / 4, scaling=1,
                  kde_precision="f32"):
         # kde_precision: the density pass's pair loop in "f32" (1e-5
-        # relative, the default, as for the MVN transition) or "f64" (1e-12)
-        if kde_precision not in ("f32", "f64"):
+        # relative, the default, as for the MVN transition), the z form on
+        # the f16 matrix cores "mfma" (1e-5) or "f64" (1e-12)
+        if kde_precision not in ("f32", "f64", "mfma"):
             raise ValueError(f"unknown kde_precision {kde_precision!r}")
         self.kde_precision = kde_precision
         if k_fraction is not None:

@@ -1028,11 +1028,14 @@ def test_column_median_mad_sampled_splitters(K, n):
     np.testing.assert_array_equal(host(mad), mad_ref)
 
 
-@pytest.mark.parametrize("d,offset", [(6, 0.0), (6, 40.0), (2, 0.0), (8, 3.0)])
-def test_local_logpdf_f32_vs_exact(K, d, offset):
+@pytest.mark.parametrize("prec", ["f32", "mfma"])
+@pytest.mark.parametrize("d,offset", [(6, 0.0), (6, 40.0), (2, 0.0), (8, 3.0),
+                                      (4, 0.0), (5, 1.0), (1, 0.0)])
+def test_local_logpdf_f32_vs_exact(K, d, offset, prec):
     """precision="f32" LocalTransition density (pair loop in fp32, centred on
-    X[0]): within 1e-5 relative of the exact fp64 density (north_star's fp32
-    bar), including far points (exact fixup) and an offset population."""
+    X[0]) and precision="mfma" (z form on the f16 matrix cores): within 1e-5
+    relative of the exact fp64 density (north_star's fp32 bar), including
+    far points (exact fixup) and an offset population."""
     rng = np.random.default_rng(d * 7 + int(offset))
     n, k = 4000, 50
     X = rng.normal(size=(n, d)) @ (np.eye(d) + 0.4 * rng.normal(size=(d, d)))
@@ -1046,13 +1049,14 @@ def test_local_logpdf_f32_vs_exact(K, d, offset):
                           np.full((3, d), 30.0 + offset)])
     exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
     got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets,
-                              precision="f32"))
+                              precision=prec))
     assert np.all(np.isfinite(got))
     np.testing.assert_allclose(np.exp(got - exact), 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("prec", ["f32", "mfma"])
 @pytest.mark.parametrize("d", [3, 6])
-def test_local_logpdf_f32_rows_independent(K, d):
+def test_local_logpdf_f32_rows_independent(K, d, prec):
     """The fp32 pass cuts the particle range into chunks that depend on N
     only: a row's bits do not depend on which rows share its call (a subset
     in another order, a single row, duplicated rows), as the row-sharded
@@ -1066,14 +1070,14 @@ def test_local_logpdf_f32_rows_independent(K, d):
     pts = np.concatenate([X[rng.integers(0, n, 3000)] +
                           0.2 * rng.normal(size=(3000, d)),
                           rng.normal(size=(100, d)) * 4])
-    full = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, "f32"))
+    full = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, prec))
     sub = rng.permutation(len(pts))[:777]
-    part = host(K.local_logpdf(dev(pts[sub]), dev(X), dev(w), invs, dets, "f32"))
+    part = host(K.local_logpdf(dev(pts[sub]), dev(X), dev(w), invs, dets, prec))
     np.testing.assert_array_equal(part, full[sub])
-    one = host(K.local_logpdf(dev(pts[sub[:1]]), dev(X), dev(w), invs, dets, "f32"))
+    one = host(K.local_logpdf(dev(pts[sub[:1]]), dev(X), dev(w), invs, dets, prec))
     np.testing.assert_array_equal(one, full[sub[:1]])
     dup = np.repeat(pts[:50], 3, axis=0)
-    got = host(K.local_logpdf(dev(dup), dev(X), dev(w), invs, dets, "f32"))
+    got = host(K.local_logpdf(dev(dup), dev(X), dev(w), invs, dets, prec))
     np.testing.assert_array_equal(got, np.repeat(full[:50], 3))
     exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
     np.testing.assert_allclose(np.exp(full - exact), 1.0, atol=1e-5)
@@ -1103,8 +1107,9 @@ def test_knn_rows_tiled_equal_full(K, d):
     np.testing.assert_array_equal(nbr[rows], order[:, :k])
 
 
+@pytest.mark.parametrize("prec", ["f32", "mfma"])
 @pytest.mark.parametrize("d,spread", [(6, 1e3), (3, 1e4), (8, 3e3)])
-def test_local_logpdf_f32_wide_population(K, d, spread):
+def test_local_logpdf_f32_wide_population(K, d, spread, prec):
     """A population whose extent is >= 1e3 local bandwidths (small k, far
     apart clusters, X[0] at one end): the fp32 pass's (hi, lo) centred
     coordinates keep it within 1e-5 of the exact fp64 density (a single
@@ -1128,7 +1133,7 @@ def test_local_logpdf_f32_wide_population(K, d, spread):
         np.median(sig)
     exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
     got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets,
-                              precision="f32"))
+                              precision=prec))
     assert np.all(np.isfinite(got))
     np.testing.assert_allclose(np.exp(got - exact), 1.0, atol=1e-5)
 

@@ -1,5 +1,6 @@
 """LocalTransition device passes at C4 (N = 2e5, d = 6, k = 50): kNN,
-local covariances, density (fp32 and fp64) -- ms per call, HIP events."""
+local covariances, density (f16 MFMA z form, fp32, fp64) -- ms per call,
+HIP events."""
 import sys
 
 import numpy as np
@@ -37,12 +38,13 @@ def main(N=200_000, d=6, k=50, scale=1.0):
     pts, _, _ = K.propose_local(X, cdf, covs, 11, 0, 0, N)
     out = {"knn_ms": timed(lambda: K.knn(X, k)),
            "local_cov_ms": timed(lambda: K.local_cov(X, w, nbr))}
-    for prec in ("f32", "f64"):
+    for prec in ("mfma", "f32", "f64"):
         out[f"pdf_{prec}_ms"] = timed(
             lambda: K.local_logpdf(pts, X, w, invs, dets, precision=prec))
-    a = K.local_logpdf(pts, X, w, invs, dets, precision="f32")
     b = K.local_logpdf(pts, X, w, invs, dets, precision="f64")
-    out["max_rel_f32_vs_f64"] = float(torch.expm1(a - b).abs().max())
+    for prec in ("f32", "mfma"):
+        a = K.local_logpdf(pts, X, w, invs, dets, precision=prec)
+        out[f"max_rel_{prec}_vs_f64"] = float(torch.expm1(a - b).abs().max())
     print({k_: (f"{v:.3e}" if k_.startswith("max_rel") else round(v, 4))
            if isinstance(v, float) else v for k_, v in out.items()}, flush=True)
 

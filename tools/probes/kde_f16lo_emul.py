@@ -70,19 +70,27 @@ def split_value(v, G):
 
 def emulate(yj, lw2, yi, scheme):
     N, D = yj.shape
-    if scheme == "f16n":
+    if scheme in ("f16n", "f16fold"):
         # norm grid: |y_j| < 2^E -> g = 2^(E - 10), |y1/g| <= 1024 (f16 ints)
         E = math.frexp(np.sqrt((yj ** 2).sum(1)).max())[1]
         g = max(math.ldexp(1.0, E - 10), 2.0 ** -10)
     else:
         g = grid(np.abs(yj).max())
     G = g * g
+    if scheme == "f16fold":
+        # unscaled f16 pieces, subnormals kept (if the MFMA keeps them)
+        y2j = f16(yj - np.rint(yj / g) * g)
+        y2i = f16(yi - np.rint(yi / g) * g)
     y1j = np.rint(yj / g) * g
     y1i = np.rint(yi / g) * g
     rj, ri = yj - y1j, yi - y1i
     if scheme == "bf16":
         y2j = bf16(rj); y3j = bf16(rj - y2j)
         y2i = bf16(ri); y3i = bf16(ri - y2i)
+        ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
+    elif scheme == "f16fold":
+        y2j = f16(rj); y3j = f16(rj - y2j)
+        y2i = f16(ri); y3i = f16(ri - y2i)
         ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
     else:
         # absolute scale 2^10 (the kernel has no g): pieces of r * 2^10
@@ -100,6 +108,9 @@ def emulate(yj, lw2, yi, scheme):
     if scheme == "bf16":
         aL1 = bf16(aL); aL2 = bf16(aL - aL1)
         bL1 = bf16(bL); bL2 = bf16(bL - bL1)
+    elif scheme == "f16fold":
+        aL1 = f16(aL); aL2 = f16(aL - aL1)
+        bL1 = f16(bL); bL2 = f16(bL - bL1)
     else:
         aL1 = f16z(aL * 1024) / 1024
         aL2 = f16z((aL - aL1) * 1024) / 1024
@@ -113,6 +124,9 @@ def emulate(yj, lw2, yi, scheme):
             terms = [y2j * 2 * y1i[i], y3j * 2 * y1i[i], y1j * 2 * y2i[i],
                      y1j * 2 * y3i[i], y2j * 2 * y2i[i], y3j * 2 * y2i[i],
                      y2j * 2 * y3i[i]]
+        elif scheme == "f16fold":
+            terms = [y2j * 2 * y1i[i], y3j * 2 * y1i[i], y1j * 2 * y2i[i],
+                     y1j * 2 * y3i[i], f16(y2j) * f16(2 * y2i[i])]
         else:
             # r2.r2 with 2^5 on each side: a side below the f16 normal
             # range is flushed (the hardware's worst case)
@@ -122,6 +136,16 @@ def emulate(yj, lw2, yi, scheme):
         prod = np.stack(terms, -1).reshape(N, -1)
         prod = np.concatenate([prod, np.stack(
             [aL1, aL2, np.full(N, bL1[i]), np.full(N, bL2[i])], -1)], 1)
+        if scheme == "f16fold":
+            # folded: hi (exact) first, then each 16-slot lo chunk rounded
+            # onto the same fp32 accumulator
+            acc = hi.astype(np.float32)
+            for c in range(0, prod.shape[1], 16):
+                acc = (acc.astype(np.float64) + prod[:, c:c + 16].sum(1)
+                       ).astype(np.float32)
+            t = np.exp2(acc).astype(np.float32)
+            out[i] = t.astype(np.float64).sum()
+            continue
         if scheme != "bf16":
             prod = prod * 1024.0                 # the scaled accumulator
         lo = chunked_fp32(prod)
@@ -154,7 +178,9 @@ def main():
     exact = np.array([np.exp2(lw2 - ((yj - r) ** 2).sum(1)).sum() for r in yi])
     res = {"N": N, "M": len(yi), "d": d, "g_bf16": grid(np.abs(yj).max()),
            "max_abs_y": float(np.abs(yj).max())}
-    for scheme in ("bf16", "f16", "f16n"):
+    schemes = sys.argv[4].split(",") if len(sys.argv) > 4 else \
+        ["bf16", "f16", "f16n"]
+    for scheme in schemes:
         got = emulate(yj, lw2, yi, scheme)
         ok = exact > 2.0 ** -32
         rel = np.abs(got[ok] / exact[ok] - 1)

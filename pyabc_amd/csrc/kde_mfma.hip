@@ -65,12 +65,19 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
   }
 }
 
+// f16 pieces, unscaled and folded, for d <= 8 (scheme 2 below)
+constexpr bool kF16Fold = false;
+
 template <int D>
 struct Mk {
   // d > 8: every piece f16 (kF16 scheme below): y1.y1, aH x2, bH x2 | five
   // cross terms per dimension, aL, bL.  d <= 8: bf16 y1.y1, aH x3, bH x3 |
   // seven cross terms, aL, bL (the folded accumulation needs one scale).
-  static constexpr bool F16 = D > 8;
+  // piece scheme: 0 bf16 (folded when KL <= kFoldKL), 1 f16 with the lo
+  // pieces x 2^10 and split accumulation (d > 8), 2 f16 unscaled, folded
+  // (d <= 8 when kF16Fold: needs the MFMA to keep f16 denormal inputs)
+  static constexpr int SCH = D > 8 ? 1 : (kF16Fold ? 2 : 0);
+  static constexpr bool F16 = SCH != 0;
   static constexpr int KH = F16 ? (D + 4 + 15) / 16 : (D + 6 + 15) / 16;
   static constexpr int KL = F16 ? (5 * D + 4 + 15) / 16 : (7 * D + 4 + 15) / 16;
   static constexpr int KT = KH + KL;
@@ -189,23 +196,26 @@ __device__ inline void split_value(double v, double G, unsigned short* h,
 
 // f16 pieces of one row (scaled as above), `side` 1 (population) or 2
 // (new rows, exact); returns |y1 + r2 + r3|^2 (the represented point)
-template <int D>
+template <int D, bool SCALED>
 __device__ inline double split_row_f16(const double* y, double g, float side,
                                        unsigned short* y1, unsigned short* r2,
                                        unsigned short* r3, unsigned short* r2h) {
+  constexpr float LS = SCALED ? kF16LoScale : 1.0f;
+  constexpr float LU = SCALED ? kF16LoUnscale : 1.0f;
   double n2 = 0.0;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     const double v1 = rint(y[k] / g) * g;
     const double r = y[k] - v1;                       // exact
-    const unsigned short b2 = f16_bits(static_cast<float>(r * kF16LoScale));
-    const double v2 = static_cast<double>(f16_f(b2)) * kF16LoUnscale;
-    const unsigned short b3 = f16_bits(static_cast<float>((r - v2) * kF16LoScale));
-    const double v3 = static_cast<double>(f16_f(b3)) * kF16LoUnscale;
+    const unsigned short b2 = f16_bits(static_cast<float>(r * LS));
+    const double v2 = static_cast<double>(f16_f(b2)) * LU;
+    const unsigned short b3 = f16_bits(static_cast<float>((r - v2) * LS));
+    const double v3 = static_cast<double>(f16_f(b3)) * LU;
     y1[k] = f16_bits(side * static_cast<float>(v1));
     r2[k] = f16_bits(side * f16_f(b2));
     r3[k] = f16_bits(side * f16_f(b3));
-    r2h[k] = f16_bits(side * static_cast<float>(v2 * 32.0));  // exact
+    // r2.r2: 2^5 per side when scaled, the plain pieces when not
+    r2h[k] = SCALED ? f16_bits(side * static_cast<float>(v2 * 32.0)) : r2[k];
     const double yt = v1 + v2 + v3;
     n2 = fma(yt, yt, n2);
   }
@@ -214,6 +224,7 @@ __device__ inline double split_row_f16(const double* y, double g, float side,
 
 // v -> two f16 pieces holding rint(v/G) G exactly (|rint(v/G)| < 2^22:
 // 11 + 11 bits), each x 2^-K, plus two f16 pieces of the remainder x 2^10
+template <bool SCALED>
 __device__ inline void split_value_f16(double v, double G, int K,
                                        unsigned short* h, unsigned short* l) {
   double q = rint(v / G);
@@ -223,7 +234,7 @@ __device__ inline void split_value_f16(double v, double G, int K,
   const double sc = ldexp(G, -K);
   h[0] = f16_bits(static_cast<float>(q0 * sc));     // exact (11 bits)
   h[1] = f16_bits(static_cast<float>(q1 * sc));
-  const double lo = (v - q * G) * kF16LoScale;      // exact, |lo| <= 512 G
+  const double lo = (v - q * G) * (SCALED ? kF16LoScale : 1.0f);  // exact
   const unsigned short l0 = f16_bits(static_cast<float>(lo));
   l[0] = l0;
   l[1] = f16_bits(static_cast<float>(lo - static_cast<double>(f16_f(l0))));
@@ -437,8 +448,9 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
     unsigned short y1[D], r2[D], r3[D], r2h[D], h[2], l[2];
     if (g > 0.0) {
       const int K = f16_shift(g);
-      const double n2 = split_row_f16<D>(y, g, 1.0f, y1, r2, r3, r2h);
-      split_value_f16(lw - n2, g * g, K, h, l);
+      constexpr bool SC = Mk<D>::SCH == 1;
+      const double n2 = split_row_f16<D, SC>(y, g, 1.0f, y1, r2, r3, r2h);
+      split_value_f16<SC>(lw - n2, g * g, K, h, l);
       store_frags_f16<D, true>(A, j, y1, r2, r3, r2h, h, l,
                                f16_bits(ldexpf(1.0f, K)));
     } else {  // E > kF16MaxE: e = -inf for every pair (all rows to the fixup)
@@ -485,8 +497,9 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     if (ok) {
       const int K = f16_shift(g);
       kpow = f16_bits(ldexpf(1.0f, K));
-      const double n2 = split_row_f16<D>(y, g, 2.0f, y1, r2, r3, r2h);
-      split_value_f16(-n2, g * g, K, h, l);
+      constexpr bool SC = Mk<D>::SCH == 1;
+      const double n2 = split_row_f16<D, SC>(y, g, 2.0f, y1, r2, r3, r2h);
+      split_value_f16<SC>(-n2, g * g, K, h, l);
     } else {  // padding / out-of-grid row: e = -inf, exact fixup if i < M
 #pragma unroll
       for (int k = 0; k < D; ++k) y1[k] = r2[k] = r3[k] = r2h[k] = 0;
@@ -547,34 +560,34 @@ constexpr int kFoldKL = 4;
 // one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
 // folded e in hi
 // folded: the bf16 scheme with few lo chunks (d <= 8)
-template <int KL, bool F16>
-constexpr bool kFolded = !F16 && KL <= kFoldKL;
+template <int KL, int SCH>
+constexpr bool kFolded = SCH == 2 || (SCH == 0 && KL <= kFoldKL);
 
-template <int KH, int KL, bool F16>
+template <int KH, int KL, int SCH>
 __device__ __forceinline__ void mfma_step(const bf16x8* a, const bf16x8* b,
                                           f32x16& hi, f32x16& lo) {
   hi = f32x16{};
 #pragma unroll
-  for (int c = 0; c < KH; ++c) hi = mfma_op<F16>(a[c], b[c], hi);
-  if constexpr (kFolded<KL, F16>) {
+  for (int c = 0; c < KH; ++c) hi = mfma_op<(SCH != 0)>(a[c], b[c], hi);
+  if constexpr (kFolded<KL, SCH>) {
 #pragma unroll
-    for (int c = 0; c < KL; ++c) hi = mfma_op<F16>(a[KH + c], b[KH + c], hi);
+    for (int c = 0; c < KL; ++c) hi = mfma_op<(SCH != 0)>(a[KH + c], b[KH + c], hi);
   } else {
     lo = f32x16{};
 #pragma unroll
-    for (int c = 0; c < KL; ++c) lo = mfma_op<F16>(a[KH + c], b[KH + c], lo);
+    for (int c = 0; c < KL; ++c) lo = mfma_op<(SCH != 0)>(a[KH + c], b[KH + c], lo);
   }
 }
 
 // sum of 2^(hi+lo) over the lane's 16 values: 16 independent exps, then a
 // fixed pairwise tree (v, v+8), (v, v+4), (v, v+2), (v, v+1)
-template <bool F16>
+template <int SCH>
 __device__ __forceinline__ float tile_sum_split(const f32x16& hi,
                                                 const f32x16& lo) {
   float e[16];
 #pragma unroll
   for (int v = 0; v < 16; ++v)
-    e[v] = __builtin_amdgcn_exp2f(combine<F16>(hi[v], lo[v]));
+    e[v] = __builtin_amdgcn_exp2f(combine<(SCH == 1)>(hi[v], lo[v]));
 #pragma unroll
   for (int w = 8; w >= 1; w >>= 1)
 #pragma unroll
@@ -583,10 +596,10 @@ __device__ __forceinline__ float tile_sum_split(const f32x16& hi,
 }
 
 // the same after mfma_step (folded: e is in hi)
-template <int KL, bool F16>
+template <int KL, int SCH>
 __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
-  if constexpr (!kFolded<KL, F16>) {
-    return tile_sum_split<F16>(hi, lo);
+  if constexpr (!kFolded<KL, SCH>) {
+    return tile_sum_split<SCH>(hi, lo);
   } else {
     float e[16];
 #pragma unroll
@@ -603,7 +616,7 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
 // per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
 // into fp64.
-template <int KH, int KL, int IB, bool PIPE, bool F16>
+template <int KH, int KL, int IB, bool PIPE, int SCH>
 __device__ __forceinline__ void kde_mfma_body(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -653,17 +666,17 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int c = 0; c < KT; ++c) a[1][c] = ap[(KT + c) * 64];
         f32x16 hi[2], lo[2];
-        mfma_step<KH, KL, F16>(a[0], bq[0], hi[0], lo[0]);
+        mfma_step<KH, KL, SCH>(a[0], bq[0], hi[0], lo[0]);
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           if (q + 1 < 2 * IB)
-            mfma_step<KH, KL, F16>(a[(q + 1) / IB], bq[(q + 1) % IB],
+            mfma_step<KH, KL, SCH>(a[(q + 1) / IB], bq[(q + 1) % IB],
                                    hi[(q + 1) & 1], lo[(q + 1) & 1]);
           if (q + 1 == IB) {  // last MFMA reading tile 0 is issued
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += tile_sum<KL, F16>(hi[q & 1], lo[q & 1]);
+          sacc[q % IB] += tile_sum<KL, SCH>(hi[q & 1], lo[q & 1]);
         }
       } else {
 #pragma unroll
@@ -671,8 +684,8 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
-          mfma_step<KH, KL, F16>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += tile_sum<KL, F16>(hi, lo);
+          mfma_step<KH, KL, SCH>(a[q / IB], bq[q % IB], hi, lo);
+          sacc[q % IB] += tile_sum<KL, SCH>(hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -691,11 +704,11 @@ __device__ __forceinline__ void kde_mfma_body(
   }
 }
 
-template <int KH, int KL, int IB, bool PIPE, bool F16>
+template <int KH, int KL, int IB, bool PIPE, int SCH>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  kde_mfma_body<KH, KL, IB, PIPE, F16>(Bfr, M, Afr, npad, split, spb, jseg,
+  kde_mfma_body<KH, KL, IB, PIPE, SCH>(Bfr, M, Afr, npad, split, spb, jseg,
                                        partial);
 }
 
@@ -713,7 +726,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
 // arithmetic and summation order are those of kde_mfma_body (split hi / lo
 // accumulators, tile 0 then tile 1 of each chunk): the rows are
 // bit-identical to kde_mfma_kernel's.
-template <int KH, int KL, int IB, bool F16>
+template <int KH, int KL, int IB, int SCH>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -775,9 +788,9 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
 #pragma unroll
           for (int t = 0; t < IB; ++t) {
             if (c < KH)
-              hi[t] = mfma_op<F16>(a, bq[t][c], hi[t]);
+              hi[t] = mfma_op<(SCH != 0)>(a, bq[t][c], hi[t]);
             else
-              lo[t] = mfma_op<F16>(a, bq[t][c], lo[t]);
+              lo[t] = mfma_op<(SCH != 0)>(a, bq[t][c], lo[t]);
           }
           // one fragment read ahead of its IB MFMAs, no early hoisting
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -785,7 +798,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
         }
 #pragma unroll
         for (int t = 0; t < IB; ++t)
-          sacc[t] += tile_sum_split<F16>(hi[t], lo[t]);
+          sacc[t] += tile_sum_split<SCH>(hi[t], lo[t]);
       }
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
@@ -849,12 +862,12 @@ struct SplitPlan {
   static constexpr int a0(int g) { return g * NA / GA; }
   static constexpr int s0(int g) { return (g - GA) * NS / (NG - GA); }
 };
-template <int KT, int KH, int IB, bool F16, int Q, int QE>
+template <int KT, int KH, int IB, int SCH, int Q, int QE>
 __device__ __forceinline__ void split_add_ops(f32x16 (&h)[IB],
                                               const f32x16 (&l)[IB]) {
   if constexpr (Q < QE) {
-    h[Q / 16][Q % 16] = combine<F16>(h[Q / 16][Q % 16], l[Q / 16][Q % 16]);
-    split_add_ops<KT, KH, IB, F16, Q + 1, QE>(h, l);
+    h[Q / 16][Q % 16] = combine<(SCH == 1)>(h[Q / 16][Q % 16], l[Q / 16][Q % 16]);
+    split_add_ops<KT, KH, IB, SCH, Q + 1, QE>(h, l);
   }
 }
 template <int IB, int Q, int QE>
@@ -864,12 +877,12 @@ __device__ __forceinline__ void split_sum_ops(f32x16 (&h)[IB], float (&sacc)[IB]
     split_sum_ops<IB, Q + 1, QE>(h, sacc);
   }
 }
-template <int KT, int KH, int IB, bool F16, int G>
+template <int KT, int KH, int IB, int SCH, int G>
 __device__ __forceinline__ void split_gap_ops(f32x16 (&h)[IB], const f32x16 (&l)[IB],
                                               float (&sacc)[IB]) {
   using P = SplitPlan<KT, KH, IB>;
   if constexpr (G < P::GA) {
-    split_add_ops<KT, KH, IB, F16, P::a0(G), P::a0(G + 1)>(h, l);
+    split_add_ops<KT, KH, IB, SCH, P::a0(G), P::a0(G + 1)>(h, l);
   } else {
     split_sum_ops<IB, P::s0(G), P::s0(G + 1)>(h, sacc);
   }
@@ -879,7 +892,7 @@ __device__ __forceinline__ void split_gap_ops(f32x16 (&h)[IB], const f32x16 (&l)
 // this tile's hi accumulators; prev: the retiring tile's; lo: the lo
 // accumulators (read as the retiring tile's lo by the first gaps, then
 // overwritten by this chain).
-template <int KT, int KH, int IB, bool F16, bool VALU, int C = 0>
+template <int KT, int KH, int IB, int SCH, bool VALU, int C = 0>
 __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int lane,
                                           const bf16x8 (&bq)[IB][KT],
                                           f32x16 (&acc)[IB], f32x16 (&prev)[IB],
@@ -892,15 +905,15 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
       if (C >= KH)
-        lo[t] = mfma_op<F16>(a[C & 1], bq[t][C], C == KH ? f32x16{} : lo[t]);
+        lo[t] = mfma_op<(SCH != 0)>(a[C & 1], bq[t][C], C == KH ? f32x16{} : lo[t]);
       else
-        acc[t] = mfma_op<F16>(a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t]);
+        acc[t] = mfma_op<(SCH != 0)>(a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VALU) {
         // t is a compile-time constant after unrolling; each branch names
         // its gap index
 #define ABC_GAP(TT) \
-  if (t == TT) split_gap_ops<KT, KH, IB, F16, C * IB + TT>(prev, lo, sacc);
+  if (t == TT) split_gap_ops<KT, KH, IB, SCH, C * IB + TT>(prev, lo, sacc);
         ABC_GAP(0)
         ABC_GAP(1)
         ABC_GAP(2)
@@ -909,7 +922,7 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
       }
     }
     a[C & 1] = nxt;
-    lds_chain<KT, KH, IB, F16, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, lo,
+    lds_chain<KT, KH, IB, SCH, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, lo,
                                              sacc, a);
   }
 }
@@ -920,7 +933,7 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
 // (The folded accumulation in the same schedule ran 16.8 ms but its error
 // reached 6.3e-6 at N = M = 1e6 against 1.5e-6 -- DESIGN.md section 4 --
 // and was dropped.)
-template <int KH, int KL, int IB, bool F16>
+template <int KH, int KL, int IB, int SCH>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
@@ -974,10 +987,10 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
       a[0] = Ab[0][lane];
       a[1] = Ab[1][lane];
       if (jc == 0) {  // tile 0, nothing to retire yet
-        lds_chain<KT, KH, IB, F16, false>(Ab, 0, lane, bq, accA, accB, lo, sprev,
+        lds_chain<KT, KH, IB, SCH, false>(Ab, 0, lane, bq, accA, accB, lo, sprev,
                                           a);
       } else {        // tile 0 || tile 1 of the previous chunk
-        lds_chain<KT, KH, IB, F16, true>(Ab, 0, lane, bq, accA, accB, lo, sprev,
+        lds_chain<KT, KH, IB, SCH, true>(Ab, 0, lane, bq, accA, accB, lo, sprev,
                                          a);
 #pragma unroll
         for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
@@ -987,7 +1000,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
       a[0] = Ab[KT][lane];
       a[1] = Ab[KT + 1][lane];
       // tile 1 || tile 0 of this chunk
-      lds_chain<KT, KH, IB, F16, true>(Ab, 1, lane, bq, accB, accA, lo, scur, a);
+      lds_chain<KT, KH, IB, SCH, true>(Ab, 1, lane, bq, accB, accA, lo, scur, a);
 #pragma unroll
       for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
       buf ^= 1;
@@ -995,7 +1008,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2i_kernel(
     if (nj > 0) {  // retire the last tile
 #pragma unroll
       for (int t = 0; t < IB; ++t)
-        sprev[t] += tile_sum_split<F16>(accB[t], lo[t]);
+        sprev[t] += tile_sum_split<SCH>(accB[t], lo[t]);
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
     }
@@ -1025,7 +1038,7 @@ __device__ __forceinline__ void fold_gap_ops(f32x16 (&h)[IB], float (&sacc)[IB])
   using P = FoldPlan<KT, IB>;
   split_sum_ops<IB, P::s0(G), P::s0(G + 1)>(h, sacc);
 }
-template <int KT, int IB, bool VALU, int C = 0>
+template <int KT, int IB, int SCH, bool VALU, int C = 0>
 __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, int lane,
                                             const bf16x8 (&bq)[IB][KT],
                                             f32x16 (&acc)[IB], f32x16 (&prev)[IB],
@@ -1035,8 +1048,7 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
     if constexpr (C + 2 < KT) nxt = Ab[tile * KT + C + 2][lane];
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-          a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t], 0, 0, 0);
+      acc[t] = mfma_op<(SCH != 0)>(a[C & 1], bq[t][C], C == 0 ? f32x16{} : acc[t]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VALU) {
 #define ABC_GAP(TT) \
@@ -1049,17 +1061,17 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
       }
     }
     a[C & 1] = nxt;
-    lds_chain_f<KT, IB, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, sacc, a);
+    lds_chain_f<KT, IB, SCH, VALU, C + 1>(Ab, tile, lane, bq, acc, prev, sacc, a);
   }
 }
 
-template <int KH, int KL, int IB>
+template <int KH, int KL, int IB, int SCH>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
   constexpr int CH = 2 * KT;
-  static_assert(KL <= kFoldKL, "folded accumulation only");
+  static_assert(kFolded<KL, SCH>, "folded accumulation only");
   static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
@@ -1107,9 +1119,9 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
       a[0] = Ab[0][lane];
       a[1] = Ab[1][lane];
       if (jc == 0) {
-        lds_chain_f<KT, IB, false>(Ab, 0, lane, bq, accA, accB, sprev, a);
+        lds_chain_f<KT, IB, SCH, false>(Ab, 0, lane, bq, accA, accB, sprev, a);
       } else {
-        lds_chain_f<KT, IB, true>(Ab, 0, lane, bq, accA, accB, sprev, a);
+        lds_chain_f<KT, IB, SCH, true>(Ab, 0, lane, bq, accA, accB, sprev, a);
 #pragma unroll
         for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
       }
@@ -1117,14 +1129,14 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
       for (int t = 0; t < IB; ++t) scur[t] = 0.0f;
       a[0] = Ab[KT][lane];
       a[1] = Ab[KT + 1][lane];
-      lds_chain_f<KT, IB, true>(Ab, 1, lane, bq, accB, accA, scur, a);
+      lds_chain_f<KT, IB, SCH, true>(Ab, 1, lane, bq, accB, accA, scur, a);
 #pragma unroll
       for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
       buf ^= 1;
     }
     if (nj > 0) {
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL, false>(accB[t], accB[t]);
+      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL, SCH>(accB[t], accB[t]);
 #pragma unroll
       for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
     }
@@ -1226,13 +1238,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // register kernel); 0: the register kernel.  Rows bit-identical.
     const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
     if (lds2 == 2) {
-      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::F16>),
+      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
     }
     if (lds2 != 0) {
-      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::F16>),
+      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
@@ -1242,7 +1254,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // the folded pass with LDS-DMA A fragments and hand-placed VALU
     // (kde_mfma_lds2g_kernel); rows bit-identical
     if (lds2g) {
-      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB>),
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;
@@ -1251,11 +1263,11 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   // software pipelining pays at D <= 8 (VALU-bound); at larger D the MFMA
   // chain dominates and the lower register count wins (bench_kde sweep)
   if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
-    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, Mk<D>::F16>),
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, Mk<D>::SCH>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
   else
-    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false, Mk<D>::F16>),
+    hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, false, Mk<D>::SCH>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
 }

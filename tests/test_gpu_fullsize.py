@@ -267,9 +267,9 @@ def test_local_transition_c4_full_size():
       numpy brute force;
     * local covariances (1e-12) and determinants (1e-11) on those rows
       against the oracle's _cov_and_inv restatement;
-    * the default fp32 density over ALL generation-2 rows against the fp64
-      pass (1e-5), and 256 sampled rows of both against the oracle's
-      _pdf_single (1e-5 / 1e-12);
+    * the fp32 and the f16-MFMA densities over ALL generation-2 rows against
+      the fp64 pass (1e-5), and 256 sampled rows of each against the
+      oracle's _pdf_single (1e-5 / 1e-12);
     * generation 2's importance weights: prior / transition_pd with the
       fp32 density, i.e. w_i * pd_i constant over the rows (1e-5)."""
     if not torch.cuda.is_available():
@@ -298,19 +298,24 @@ def test_local_transition_c4_full_size():
     # densities: all rows f32 vs f64, sampled rows vs the oracle
     dev = lambda a: torch.as_tensor(a, device="cuda")
     Xd, wd = dev(X), dev(w)
-    lp32 = K.local_logpdf(dev(th2), Xd, wd, tr._invs, tr._dets, "f32")
-    lp64 = K.local_logpdf(dev(th2), Xd, wd, tr._invs, tr._dets, "f64")
-    lp32, lp64 = lp32.cpu().numpy(), lp64.cpu().numpy()
-    err_all = np.abs(np.expm1(lp32 - lp64))
-    assert err_all.max() < RTOL, err_all.max()
+    lp = {p: K.local_logpdf(dev(th2), Xd, wd, tr._invs, tr._dets,
+                            p).cpu().numpy() for p in ("f32", "mfma", "f64")}
+    lp64 = lp["f64"]
+    errs = {}
     pick = np.sort(rng.choice(len(th2), 256, replace=False))
     pdf_ref = ref.local_pdf(th2[pick], X, w, tr.inv_covs, tr.determinants)
     np.testing.assert_allclose(np.exp(lp64[pick]), pdf_ref, rtol=1e-12)
-    np.testing.assert_allclose(np.exp(lp32[pick]), pdf_ref, rtol=RTOL)
-    # the generation's own weights: prior (uniform, constant) / pd
-    prod = np.log(w2) + lp32
+    for p in ("f32", "mfma"):
+        err_all = np.abs(np.expm1(lp[p] - lp64))
+        errs[p] = float(err_all.max())
+        assert err_all.max() < RTOL, (p, err_all.max())
+        np.testing.assert_allclose(np.exp(lp[p][pick]), pdf_ref, rtol=RTOL)
+    # the generation's own weights: prior (uniform, constant) / pd, with the
+    # density pass the run used
+    prod = np.log(w2) + lp[tr.kde_precision]
     spread = np.abs(np.expm1(prod - np.median(prod)))
     assert spread.max() < RTOL, spread.max()
     print(json.dumps(dict(tag="c4_N2e5_d6_k50", rows=len(rows),
-                          max_rel_f32_vs_f64_all=float(err_all.max()),
+                          max_rel_f32_vs_f64_all=errs["f32"],
+                          max_rel_mfma_vs_f64_all=errs["mfma"],
                           weight_product_spread=float(spread.max()))))

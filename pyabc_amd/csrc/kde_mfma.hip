@@ -65,22 +65,43 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
   }
 }
 
-// f16 pieces, unscaled and folded, for d <= 8 (scheme 2 below)
-constexpr bool kF16Fold = false;
+// Piece scheme per dimension class (compile-time; tools/kde_ab.py prices two
+// builds on one box):
+//   0 bf16 y1.y1, aH x3, bH x3 | seven cross terms per dimension, aL, bL
+//     (folded when KL <= kFoldKL) -- d <= 8;
+//   1 f16 y1.y1, aH x2, bH x2 | five cross terms, aL, bL, the lo pieces
+//     x 2^10, split accumulation (hi exact, lo apart, e = fma(lo, 2^-10, hi))
+//     -- d > 24 (and 8 < d <= 24 with -DABC_KDE_SCHEME_LARGE=1);
+//   2 the same f16 pieces unscaled, every chunk accumulated onto one fp32
+//     value (folded: no hi + lo add per pair; the KL lo chunks each round at
+//     |e|) -- 8 < d <= 24.  Needs the MFMA to keep f16 denormal inputs
+//     (tools/probes/mfma_f16_denorm.hip: outputs down to 2^-24).  Same box,
+//     N = M = 1e6, d = 20: 209.7 ms against 232.2 ms split; max row error
+//     on the kde_variants rows 4.5e-6 against 7.5e-7 (d = 12 / 16 / 24:
+//     3.8 / 4.2 / 5.4e-6; d = 32 would be 6.2e-6, so it stays split).
+// Rejected (measured): the lo slots packed into the hi chunks' spare slots
+// (8 MFMAs at d = 20 instead of 9) -- a chunk mixing the large, cancelling hi
+// products with lo products loses the lo bits inside the MFMA (row errors
+// 1.4e-5 -- 1.6e-5 at d = 16, 24; tools/probes/mfma_acc_round.hip: the
+// 32x32x16 MFMA is not one exact sum + one rounding).
+#ifndef ABC_KDE_SCHEME_SMALL
+#define ABC_KDE_SCHEME_SMALL 0
+#endif
+#ifndef ABC_KDE_SCHEME_LARGE
+#define ABC_KDE_SCHEME_LARGE 2
+#endif
 
 template <int D>
 struct Mk {
-  // d > 8: every piece f16 (kF16 scheme below): y1.y1, aH x2, bH x2 | five
-  // cross terms per dimension, aL, bL.  d <= 8: bf16 y1.y1, aH x3, bH x3 |
-  // seven cross terms, aL, bL (the folded accumulation needs one scale).
-  // piece scheme: 0 bf16 (folded when KL <= kFoldKL), 1 f16 with the lo
-  // pieces x 2^10 and split accumulation (d > 8), 2 f16 unscaled, folded
-  // (d <= 8 when kF16Fold: needs the MFMA to keep f16 denormal inputs)
-  static constexpr int SCH = D > 8 ? 1 : (kF16Fold ? 2 : 0);
+  static constexpr int SCH =
+      D <= 8 ? ABC_KDE_SCHEME_SMALL : (D <= 24 ? ABC_KDE_SCHEME_LARGE : 1);
+  static_assert(SCH >= 0 && SCH <= 2 && (SCH != 1 || D > 8),
+                "piece scheme 0..2 (1 only for d > 8)");
   static constexpr bool F16 = SCH != 0;
   static constexpr int KH = F16 ? (D + 4 + 15) / 16 : (D + 6 + 15) / 16;
   static constexpr int KL = F16 ? (5 * D + 4 + 15) / 16 : (7 * D + 4 + 15) / 16;
   static constexpr int KT = KH + KL;
+  static constexpr int LO0 = 16 * KH;  // first lo slot
   static constexpr int IB = D <= 8 ? 3 : (D <= 24 ? 2 : 1);  // i-tiles/wave
   // row padding unit in i-tiles per wave: every IB the launch may pick
   // (1, 2, 3 at D <= 8) divides it
@@ -242,7 +263,7 @@ __device__ inline void split_value_f16(double v, double G, int K,
 
 // Slot k of the f16 operands (d > 8):
 //  hi  k < D: y1 | 2y1     k = D, D+1: aH 2^-K | 2^K   k = D+2, D+3: 2^K | bH 2^-K
-//  lo  k' = 5m + q (m < D): q: 0 r2|2y1  1 r3|2y1  2 y1|2r2  3 y1|2r3
+//  lo  from slot LO0 = 16 KH, k' = 5m + q (m < D): q: 0 r2|2y1  1 r3|2y1  2 y1|2r2  3 y1|2r3
 //                                4 r2 2^-5|2r2 2^-5 (x 2^10 included above)
 //      k' = 5D, 5D+1: aL | 1   k' = 5D+2, 5D+3: 1 | bL
 template <int D, bool kA>
@@ -253,14 +274,14 @@ __device__ inline unsigned short slot_f16(int k, const unsigned short* y1,
                                           const unsigned short* h,
                                           const unsigned short* l,
                                           unsigned short kpow) {
-  constexpr int KH = Mk<D>::KH;
-  if (k < 16 * KH) {
+  constexpr int LO0 = Mk<D>::LO0;
+  if (k < LO0) {
     if (k < D) return y1[k];
     if (k < D + 2) return kA ? h[k - D] : kpow;
     if (k < D + 4) return kA ? kpow : h[k - D - 2];
     return 0;
   }
-  const int kk = k - 16 * KH;
+  const int kk = k - LO0;
   if (kk < 5 * D) {
     const int m = kk / 5, q = kk % 5;
     switch (q) {
@@ -554,7 +575,8 @@ __device__ __forceinline__ float combine(float hi, float lo) {
 // bounded by ~8e-8 log2(N / S) for a row sum S; rows with S < 2^-32 (dominant
 // exponents beyond ~32) take the exact fp64 fixup (kMfmaFixupSum), so the
 // bound is ~4e-6 at N = 1e6 (measured: tests/test_gpu_fullsize.py, DESIGN
-// section 4).  At d > 8 (MFMA-bound) the accumulation stays split.
+// section 4).  The f16 scheme 2 (8 < d <= 24) folds the same way, its
+// error measured per dimension in the scheme table above.
 constexpr int kFoldKL = 4;
 
 // one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
@@ -1232,7 +1254,16 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   const unsigned grid = static_cast<unsigned>(p.row_blocks * p.split);
   const dim3 block(64 * kWaves);
   const int split = p.smajor ? -p.split : p.split;
-  if constexpr (D > 8) {
+  if constexpr (D > 8 && Mk<D>::SCH == 2) {
+    // the folded f16 scheme: the LDS-DMA folded pass (ABC_KDE_MFMA_LDS2 1
+    // or 2), or the register kernel (0); rows bit-identical
+    if (env_int("ABC_KDE_MFMA_LDS2", 2) != 0) {
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
+                         p.spb, p.jseg, partial);
+      return;
+    }
+  } else if constexpr (D > 8) {
     // 2: hand-interleaved split pass; 1: LDS-DMA A fragments, compiler
     // schedule (d = 20: 21.5 -> 20.4 ms at N = M = 262144 against the
     // register kernel); 0: the register kernel.  Rows bit-identical.

@@ -40,8 +40,8 @@
 // sit at ~1/16).
 //
 // Layout: 32-row MFMA tiles of (particle, component) rows, DP = 8 rows per
-// particle for d = 5..8 (4 particles per tile: a lane holds 4 components of
-// each, the two lane halves are summed with v_permlane32_swap) and DP = 4
+// particle for d = 5..8 (4 particles per tile, the rows placed so that each
+// lane holds two particles whole: lz_row) and DP = 4
 // for d <= 4 (8 particles per tile, a particle whole in one lane).  The
 // particles stream through LDS (LDS-DMA, two tiles per buffer, double
 // buffered); each wave holds IB 32-point tiles of the evaluation points in
@@ -63,6 +63,7 @@ namespace {
 typedef short h16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kLzWaves = 4;
 constexpr double kLzGrid = 0.00390625;       // g = 2^-8
@@ -135,6 +136,19 @@ __device__ inline void lz_store_row(h16x8* __restrict__ F, int64_t tile, int r,
       for (int e = 0; e < 8; ++e) x[e] = static_cast<short>(v[16 * c + 8 * hh + e]);
       F[(tile * KT + c) * 64 + 32 * hh + r] = x;
     }
+}
+
+// Row of component a of tile particle p.  The accumulator holds row
+// 8 (v >> 2) + 4 h + (v & 3) in lane half h, value v.  DP = 8: particle p
+// takes groups 2 (p & 1), 2 (p & 1) + 1 of half p >> 1, so a lane holds
+// particles 2h (values 0-7) and 2h + 1 (values 8-15) whole -- no exchange
+// between the halves; DP = 4: rows 4 p .. 4 p + 3 (group p >> 1, half p & 1).
+template <int DP>
+__device__ __forceinline__ int lz_row(int p, int a) {
+  if constexpr (DP == 8)
+    return 8 * (2 * (p & 1) + (a >> 2)) + 4 * (p >> 1) + (a & 3);
+  else
+    return DP * p + a;
 }
 
 // One thread per particle: Cholesky of inv_n, the scaled columns, their
@@ -268,7 +282,7 @@ __global__ __launch_bounds__(128) void lz_pack_prev_kernel(
     }
   }
 #pragma unroll
-  for (int a = 0; a < DP; ++a) lz_store_row<KT>(A, tile, pin * DP + a, v[a]);
+  for (int a = 0; a < DP; ++a) lz_store_row<KT>(A, tile, lz_row<DP>(pin, a), v[a]);
   lcT[lslot] = lcv;
 }
 
@@ -340,28 +354,21 @@ __device__ __forceinline__ f32x16 lz_mfma(const h16x8& a, const h16x8& b,
 template <int DP>
 __device__ __forceinline__ float lz_terms(const f32x16& acc, const float2* lcp) {
   if constexpr (DP == 8) {
-    // v = 4 k + j: particle k, component 4 h + j
-    float s[4];
+    // values 8 k .. 8 k + 7: particle 2 h + k, whole (lz_row); squares in
+    // packed pairs, the two particles' chains interleaved (no dependent
+    // back-to-back packed op)
+    const f32x2 a0 = {acc[0], acc[1]}, b0 = {acc[8], acc[9]};
+    f32x2 p = a0 * a0, r = b0 * b0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float t = acc[4 * k] * acc[4 * k];
-#pragma unroll
-      for (int j = 1; j < 4; ++j) t = __builtin_fmaf(acc[4 * k + j], acc[4 * k + j], t);
-      s[k] = t;
+    for (int j = 1; j < 4; ++j) {
+      const f32x2 aj = {acc[2 * j], acc[2 * j + 1]};
+      const f32x2 bj = {acc[8 + 2 * j], acc[8 + 2 * j + 1]};
+      p = __builtin_elementwise_fma(aj, aj, p);
+      r = __builtin_elementwise_fma(bj, bj, r);
     }
-    // lanes 32-63 of the first operand <-> lanes 0-31 of the second: each
-    // half then holds own + other half of particles 2h, 2h + 1
-    const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[0]),
-                                                    __float_as_uint(s[2]), false,
-                                                    false);
-    const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[1]),
-                                                    __float_as_uint(s[3]), false,
-                                                    false);
-    const float qa = __uint_as_float(x[0]) + __uint_as_float(x[1]);
-    const float qb = __uint_as_float(y[0]) + __uint_as_float(y[1]);
-    const float ta = __builtin_amdgcn_exp2f(__builtin_fmaf(qa, lcp[0].y, lcp[0].x));
-    const float tb = __builtin_amdgcn_exp2f(__builtin_fmaf(qb, lcp[1].y, lcp[1].x));
-    return ta + tb;
+    const float t0 = __builtin_amdgcn_exp2f(__builtin_fmaf(p.x + p.y, lcp[0].y, lcp[0].x));
+    const float t1 = __builtin_amdgcn_exp2f(__builtin_fmaf(r.x + r.y, lcp[1].y, lcp[1].x));
+    return t0 + t1;
   } else {
     // v = 4 k + j: particle 2 k + h, component j
     float t[4];
@@ -424,22 +431,34 @@ __global__ __launch_bounds__(64 * kLzWaves) void lz_kernel(
     float sacc[IB];
 #pragma unroll
     for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+    // the 2 IB (particle tile, point tile) products of this buffer, software
+    // pipelined: the MFMA chain of product q is issued before the VALU terms
+    // of product q - 1, so the terms never wait on the matrix pipe
+    constexpr int NL = DP == 8 ? 2 : 4;
+    float2 lcv[2][NL];
+    h16x8 a[2][KT];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      // (lc2, cf) of this lane's particles in tile tl + u
       const float2* lcp = lcT + (tile0 + tl + u) * PT + (DP == 8 ? 2 * h : 4 * h);
-      float2 lcv[DP == 8 ? 2 : 4];
 #pragma unroll
-      for (int k = 0; k < (DP == 8 ? 2 : 4); ++k) lcv[k] = lcp[k];
-      h16x8 a[KT];
+      for (int k = 0; k < NL; ++k) lcv[u][k] = lcp[k];
 #pragma unroll
-      for (int c = 0; c < KT; ++c) a[c] = As[buf][u * KT + c][lane];
+      for (int c = 0; c < KT; ++c) a[u][c] = As[buf][u * KT + c][lane];
+    }
+    f32x16 acc[2];
 #pragma unroll
-      for (int t = 0; t < IB; ++t) {
-        f32x16 acc = f32x16{};
+    for (int q = 0; q <= 2 * IB; ++q) {
+      if (q < 2 * IB) {
+        const int u = q / IB, t = q % IB;
+        acc[q & 1] = f32x16{};
 #pragma unroll
-        for (int c = 0; c < KT; ++c) acc = lz_mfma(a[c], bq[t][c], acc);
-        sacc[t] += lz_terms<DP>(acc, lcv);
+        for (int c = 0; c < KT; ++c) acc[q & 1] = lz_mfma(a[u][c], bq[t][c], acc[q & 1]);
+      }
+      if (q > 0) {
+        const int u = (q - 1) / IB, t = (q - 1) % IB;
+        __builtin_amdgcn_sched_barrier(0);
+        sacc[t] += lz_terms<DP>(acc[(q - 1) & 1], lcv[u]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
@@ -539,7 +558,7 @@ int lz_run(const double* pts, int64_t M, const double* X, const double* w,
   h16x8* B = reinterpret_cast<h16x8*>(q);
   ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
   ABC_HIP(hipMemsetAsync(ex, 0, 128, st));
-  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(256), 0, st, w, N, logsumw);
+  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(1024), 0, st, w, N, logsumw);
   hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, st,
                      w, dets, invs, N, D, lc, coef, lc_max_key);
   hipLaunchKernelGGL(lz_dims_kernel<D>, dim3(stream_grid(N, 256, 512)), dim3(256),

@@ -1457,15 +1457,60 @@ __global__ __launch_bounds__(256) void bs_full_kernel(
   }
 }
 
-// one block per column: rank k (and k + 1) among the bracket's candidates
-// by 8-bit digit passes below the bracket's common key prefix; the result
-// (np.median / MAD semantics as seg_median_kernel) and done = 1, or nothing
-// when the bracket does not hold rank k / holds too many keys
+// bin of rank r in a 4096-bin histogram, 1024 threads (4 bins each):
+// wave-shuffle scan + 16 wave totals; returns the bin, the count below it and
+// its count (block-uniform)
+__device__ inline void bs_find1024(const unsigned* h, long long r,
+                                   unsigned long long* sh, long long* wsum,
+                                   int* dig, long long* before, long long* cnt) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  long long v[4], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = h[4 * t + j];
+    tot += v[j];
+  }
+  long long inc = tot;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  long long run = inc - tot;
+  for (int w = 0; w < wv; ++w) run += wsum[w];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (v[j] > 0 && run <= r && r < run + v[j]) {
+      sh[0] = static_cast<unsigned long long>(4 * t + j);
+      sh[1] = static_cast<unsigned long long>(run);
+      sh[2] = static_cast<unsigned long long>(v[j]);
+    }
+    run += v[j];
+  }
+  __syncthreads();
+  *dig = static_cast<int>(sh[0]);
+  *before = static_cast<long long>(sh[1]);
+  *cnt = static_cast<long long>(sh[2]);
+  __syncthreads();
+}
+
+// one block per column: rank k (and k + 1) among the bracket's candidates.
+// Digits are taken over the candidates' key RANGE, not the key bits: the
+// keys in [base, base + span] fall in 4096 bins of width 2^sh, span < 2^(sh
+// + 12), so keys spread evenly over a narrow quantile range land in many
+// bins (no atomic pile-up on one bin) and two or three passes reach a single
+// key.  The result (np.median / MAD semantics as seg_median_kernel) and
+// done = 1, or nothing when the bracket does not hold rank k / holds too many
+// keys.
 __global__ __launch_bounds__(1024) void bs_cand_kernel(SegState* st, int64_t n,
                                                        const unsigned long long* __restrict__ cbuf,
-                                                       double* __restrict__ out) {
-  __shared__ unsigned hc[256];
+                                                       double* __restrict__ out,
+                                                       unsigned* __restrict__ ndone) {
+  __shared__ unsigned hc[kBsBins];
   __shared__ unsigned long long sh[4];
+  __shared__ long long wsum[16];
   __shared__ unsigned long long red[16];
   const int s = blockIdx.x, t = threadIdx.x;
   const long long k = (n - 1) / 2;
@@ -1484,41 +1529,40 @@ __global__ __launch_bounds__(1024) void bs_cand_kernel(SegState* st, int64_t n,
   long long eq = cin;
   long long r = k - below;
   if (!one_key) {
-    const int common = __clzll(static_cast<long long>(lo ^ hi));  // shared bits
-    unsigned long long prefix = lo & (common ? (~0ull << (64 - common)) : 0ull);
-    int consumed = common;
-    while (consumed < 64) {
-      const int bits = 64 - consumed < 8 ? 64 - consumed : 8;
-      const int shift = 64 - consumed - bits;
-      const unsigned long long mask = consumed ? (~0ull << (64 - consumed)) : 0ull;
-      if (t < 256) hc[t] = 0;
+    unsigned long long base = lo, span = hi - lo;      // keys in [base, base + span]
+    while (true) {
+      const int width = 64 - __clzll(static_cast<long long>(span));  // span < 2^width
+      const int shift = width > 12 ? width - 12 : 0;
+      for (int j = t; j < kBsBins; j += 1024) hc[j] = 0;
       __syncthreads();
       for (long long i = t; i < cin; i += 1024) {
-        const unsigned long long kk = keys[i];
-        if (((kk ^ prefix) & mask) == 0)
-          atomicAdd(&hc[(kk >> shift) & ((1u << bits) - 1u)], 1u);
-      }
-      __syncthreads();
-      if (t == 0) {
-        long long run = 0;
-        for (int j = 0; j < (1 << bits); ++j) {
-          if (hc[j] && run <= r && r < run + hc[j]) {
-            sh[0] = static_cast<unsigned long long>(j);
-            sh[1] = static_cast<unsigned long long>(run);
-            sh[2] = hc[j];
-            break;
-          }
-          run += hc[j];
+        const unsigned long long d = keys[i] - base;  // wraps above for keys < base
+        const bool in = d <= span;
+        const unsigned bin = in ? static_cast<unsigned>(d >> shift) : 0u;
+        // wave-aggregated when the wave's keys share a bin (tie runs)
+        const unsigned long long act = __ballot(in);
+        if (act == 0ull) continue;
+        const int leader = __ffsll(static_cast<long long>(act)) - 1;
+        const unsigned lb = __shfl(bin, leader, 64);
+        if (__ballot(in && bin == lb) == act) {
+          if ((t & 63) == leader) atomicAdd(&hc[lb], static_cast<unsigned>(__popcll(act)));
+        } else if (in) {
+          atomicAdd(&hc[bin], 1u);
         }
       }
       __syncthreads();
-      prefix |= sh[0] << shift;
-      r -= static_cast<long long>(sh[1]);
-      eq = static_cast<long long>(sh[2]);
-      consumed += bits;
-      __syncthreads();
+      int dig;
+      long long before, cnt;
+      bs_find1024(hc, r, sh, wsum, &dig, &before, &cnt);
+      r -= before;
+      eq = cnt;
+      base += static_cast<unsigned long long>(dig) << shift;
+      if (shift == 0) break;                           // one key: a = base
+      const unsigned long long rest = span - (static_cast<unsigned long long>(dig) << shift);
+      const unsigned long long bw = (1ull << shift) - 1ull;
+      span = rest < bw ? rest : bw;
     }
-    a = prefix;
+    a = base;
     // k + 1 (even n): the same key while the tie run lasts, else the
     // smallest candidate above a, else the smallest column key above hi
     if ((n & 1) == 0 && r + 1 >= eq) {
@@ -1551,6 +1595,7 @@ __global__ __launch_bounds__(1024) void bs_cand_kernel(SegState* st, int64_t n,
     const double va = key_f64(a);
     out[s] = (n & 1) ? va : (va + key_f64(b)) / 2.0;
     st[s].done = 1;
+    atomicAdd(ndone, 1u);
   }
 }
 
@@ -1996,8 +2041,11 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
   unsigned* bhist = hist + static_cast<size_t>(S) * kWideBins;
   unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
       bhist + static_cast<size_t>(S) * 2 * kBsBins);
+  // per-round settled-column counters (in the workspace's 256-byte tail)
+  unsigned* ndone = reinterpret_cast<unsigned*>(cbuf + static_cast<size_t>(S) * kCandCap);
   ABC_HIP(hipMemsetAsync(hist, 0, static_cast<size_t>(S) * (kWideBins + 2 * kBsBins) * 4,
                          st));
+  ABC_HIP(hipMemsetAsync(ndone, 0, 8, st));
   int bps = static_cast<int>(ceil_div(2048, S));
   const int64_t maxb = ceil_div(n, 256);
   if (bps > maxb) bps = static_cast<int>(maxb);
@@ -2028,7 +2076,14 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
     else
       hipLaunchKernelGGL(bs_full_kernel<1>, dim3(S * bps), dim3(256), 0, st, data_T,
                          ld, n, bps, center, sst, cbuf);
-    hipLaunchKernelGGL(bs_cand_kernel, dim3(S), dim3(1024), 0, st, sst, n, cbuf, out);
+    hipLaunchKernelGGL(bs_cand_kernel, dim3(S), dim3(1024), 0, st, sst, n, cbuf, out,
+                       ndone + round);
+    // every column settled (the usual case): skip the radix launches -- one
+    // 4-byte read-back per round (the caller reads the scales back anyway)
+    unsigned settled = 0;
+    ABC_HIP(hipMemcpyAsync(&settled, ndone + round, 4, hipMemcpyDeviceToHost, st));
+    ABC_HIP(hipStreamSynchronize(st));
+    if (settled == static_cast<unsigned>(S)) continue;
     // radix passes for the columns the bracket did not settle
     int consumed = 0;  // key bits selected so far
     for (int pass = 0; pass < kSegPasses; ++pass) {

@@ -49,7 +49,24 @@ def main(N=200_000, d=6, k=50, scale=1.0):
            if isinstance(v, float) else v for k_, v in out.items()}, flush=True)
 
 
+def prof(N=200_000, d=6, k=50, reps=5):
+    """the z-form pass alone at C4 (for rocprofv3 kernel stats / PMC)"""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
+    w = torch.rand(N, dtype=torch.float64, device="cuda", generator=g)
+    w /= w.sum()
+    nbr, _ = K.knn(X, k)
+    covs, invs, dets = K.local_cov(X, w, nbr)
+    pts, _, _ = K.propose_local(X, K.resample_cdf(w), covs, 11, 0, 0, N)
+    for _ in range(reps):
+        K.local_logpdf(pts, X, w, invs, dets, precision="mfma")
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["prof"]:
+        prof()
+        sys.exit(0)
     main()
     main(N=200_000, d=4, k=50)
     main(N=50_000, d=8, k=50)

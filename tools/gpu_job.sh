@@ -18,6 +18,9 @@
 #   kernels               tools/bench_kernels.py (per-kernel roofline table)
 #   configs               tools/bench_configs.py (BASELINE configs end to end)
 #   py=SECS:SCRIPT ARGS   python3 -u SCRIPT ARGS under a SECS limit
+#   bin=SECS:PROGRAM ARGS  a compiled probe under a SECS limit
+#   stats=SECS:SCRIPT ARGS
+#                         rocprofv3 kernel trace + stats over python3 SCRIPT
 #   pmc=SECS:COUNTERS:SCRIPT ARGS
 #                         one rocprofv3 --pmc pass (counters comma-separated)
 #                         over python3 SCRIPT ARGS
@@ -90,6 +93,15 @@ for step in "$@"; do
       secs=${arg%%:*}
       # shellcheck disable=SC2086
       run "$secs" "${k}_py" python3 -u ${arg#*:} ;;
+    bin)
+      secs=${arg%%:*}
+      # shellcheck disable=SC2086
+      run "$secs" "${k}_bin" ${arg#*:} ;;
+    stats)
+      secs=${arg%%:*}
+      # shellcheck disable=SC2086
+      run "$secs" "${k}_stats" rocprofv3 --kernel-trace --stats -T -f csv \
+        -d "$OUT/stats_$k" -o run -- python3 -u ${arg#*:} ;;
     pmc)
       secs=${arg%%:*}
       rest=${arg#*:}

@@ -5,4 +5,6 @@ set -e
 make -C "$(dirname "$0")/../pyabc_amd/csrc" -j8 > /dev/null
 T=$1
 shift
-exec /usr/local/graft/bin/gpurun --timeout "$T" -- "bash tools/gpu_job.sh $*"
+cmd="bash tools/gpu_job.sh"
+for a in "$@"; do cmd+=" $(printf %q "$a")"; done
+exec /usr/local/graft/bin/gpurun --timeout "$T" -- "$cmd"

@@ -70,14 +70,15 @@ def split_value(v, G):
 
 def emulate(yj, lw2, yi, scheme):
     N, D = yj.shape
-    if scheme in ("f16n", "f16fold"):
+    if scheme in ("f16n", "f16fold", "f16foldS", "f16foldR", "f16loA", "f16loB",
+                  "f16foldX"):
         # norm grid: |y_j| < 2^E -> g = 2^(E - 10), |y1/g| <= 1024 (f16 ints)
         E = math.frexp(np.sqrt((yj ** 2).sum(1)).max())[1]
         g = max(math.ldexp(1.0, E - 10), 2.0 ** -10)
     else:
         g = grid(np.abs(yj).max())
     G = g * g
-    if scheme == "f16fold":
+    if scheme in ("f16fold", "f16foldR", "f16loA", "f16loB"):
         # unscaled f16 pieces, subnormals kept (if the MFMA keeps them)
         y2j = f16(yj - np.rint(yj / g) * g)
         y2i = f16(yi - np.rint(yi / g) * g)
@@ -88,7 +89,13 @@ def emulate(yj, lw2, yi, scheme):
         y2j = bf16(rj); y3j = bf16(rj - y2j)
         y2i = bf16(ri); y3i = bf16(ri - y2i)
         ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
-    elif scheme == "f16fold":
+    elif scheme == "f16foldX":
+        # r2 unscaled (normal), r3 carried x 2^10 against y1 x 2^-10 (both
+        # exact, normal or exact subnormal)
+        y2j = f16(rj); y3j = f16((rj - y2j) * 1024) / 1024
+        y2i = f16(ri); y3i = f16((ri - y2i) * 1024) / 1024
+        ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
+    elif scheme in ("f16fold", "f16foldR", "f16loA", "f16loB"):
         y2j = f16(rj); y3j = f16(rj - y2j)
         y2i = f16(ri); y3i = f16(ri - y2i)
         ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
@@ -99,7 +106,7 @@ def emulate(yj, lw2, yi, scheme):
         y2i = f16z(ri * 1024) / 1024
         y3i = f16z((ri - y2i) * 1024) / 1024
         ytj, yti = y1j + y2j + y3j, y1i + y2i + y3i
-    if scheme == "f16n":
+    if scheme in ("f16n", "f16foldS"):
         assert np.abs(y1j / g).max() <= 2048 and np.abs(y1i / g).max() <= 2048
     a = lw2 - (ytj ** 2).sum(1)
     b = -(yti ** 2).sum(1)
@@ -108,7 +115,7 @@ def emulate(yj, lw2, yi, scheme):
     if scheme == "bf16":
         aL1 = bf16(aL); aL2 = bf16(aL - aL1)
         bL1 = bf16(bL); bL2 = bf16(bL - bL1)
-    elif scheme == "f16fold":
+    elif scheme in ("f16fold", "f16foldR", "f16loA", "f16loB"):
         aL1 = f16(aL); aL2 = f16(aL - aL1)
         bL1 = f16(bL); bL2 = f16(bL - bL1)
     else:
@@ -124,7 +131,7 @@ def emulate(yj, lw2, yi, scheme):
             terms = [y2j * 2 * y1i[i], y3j * 2 * y1i[i], y1j * 2 * y2i[i],
                      y1j * 2 * y3i[i], y2j * 2 * y2i[i], y3j * 2 * y2i[i],
                      y2j * 2 * y3i[i]]
-        elif scheme == "f16fold":
+        elif scheme in ("f16fold", "f16foldR", "f16loA", "f16loB", "f16foldX"):
             terms = [y2j * 2 * y1i[i], y3j * 2 * y1i[i], y1j * 2 * y2i[i],
                      y1j * 2 * y3i[i], f16(y2j) * f16(2 * y2i[i])]
         else:
@@ -136,7 +143,62 @@ def emulate(yj, lw2, yi, scheme):
         prod = np.stack(terms, -1).reshape(N, -1)
         prod = np.concatenate([prod, np.stack(
             [aL1, aL2, np.full(N, bL1[i]), np.full(N, bL2[i])], -1)], 1)
-        if scheme == "f16fold":
+        if scheme in ("f16loA", "f16loB"):
+            # chunk-aligned, lo chunks first (pure lo, onto 0), then the hi
+            # chunks onto them: A = y1.y1[0:16] | y1.y1[16:] aH aH bH bH,
+            # B = aH aH bH bH y1.y1[0:12] | y1.y1[12:]
+            qa = np.rint(aH / G); qb = np.rint(bH[i] / G)
+            qa0 = np.trunc(qa / 2048) * 2048; qb0 = np.trunc(qb / 2048) * 2048
+            ab = np.stack([qa0 * G, (qa - qa0) * G, np.full(N, qb0 * G),
+                           np.full(N, (qb - qb0) * G)], -1)
+            yy = 2 * y1i[i] * y1j
+            if scheme == "f16loA":
+                h0 = yy[:, :16]; h1 = np.concatenate([yy[:, 16:], ab], 1)
+            else:
+                h0 = np.concatenate([ab, yy[:, :12]], 1); h1 = yy[:, 12:]
+            acc = np.zeros(N, dtype=np.float32)
+            for c in range(0, prod.shape[1], 16):
+                acc = (acc.astype(np.float64) + prod[:, c:c + 16].sum(1)
+                       ).astype(np.float32)
+            for h in (h0, h1):
+                acc = (acc.astype(np.float64) + h.sum(1)).astype(np.float32)
+            out[i] = np.exp2(acc).astype(np.float32).astype(np.float64).sum()
+            continue
+        if scheme == "f16foldR":
+            # packed slots, lo first: the 5D + 4 lo slots, then the D + 4 hi
+            # slots (y1.y1 per dimension, aH x2, bH x2), 16-slot chunks
+            # rounded onto one fp32 accumulator starting from 0
+            qa = np.rint(aH / G); qb = np.rint(bH[i] / G)
+            qa0 = np.trunc(qa / 2048) * 2048; qb0 = np.trunc(qb / 2048) * 2048
+            hiv = np.concatenate([2 * y1i[i] * y1j, np.stack(
+                [qa0 * G, (qa - qa0) * G, np.full(N, qb0 * G),
+                 np.full(N, (qb - qb0) * G)], -1)], 1)
+            allp = np.concatenate([prod, hiv], 1)
+            acc = np.zeros(N, dtype=np.float32)
+            for c in range(0, allp.shape[1], 16):
+                acc = (acc.astype(np.float64) + allp[:, c:c + 16].sum(1)
+                       ).astype(np.float32)
+            out[i] = np.exp2(acc).astype(np.float32).astype(np.float64).sum()
+            continue
+        if scheme == "f16foldS":
+            # folded in units of 2^-10: hi (exact, x 2^10) first, then each
+            # 16-slot chunk of the scaled lo products rounded onto the same
+            # fp32 accumulator; e = acc * 2^-10 (exact)
+            allp = np.concatenate([prod * 1024.0], 1)
+            acc = (hi * 1024.0).astype(np.float32)
+            # merged slots: hi fills D + 4 slots, the lo slots follow
+            nh = (D + 4) % 16
+            first = 16 - nh if nh else 0
+            cuts = [0, first] + list(range(first + 16, allp.shape[1], 16))
+            cuts = sorted(set(c for c in cuts if c < allp.shape[1])) + [allp.shape[1]]
+            for c0, c1 in zip(cuts[:-1], cuts[1:]):
+                if c1 > c0:
+                    acc = (acc.astype(np.float64) + allp[:, c0:c1].sum(1)
+                           ).astype(np.float32)
+            t = np.exp2((acc * np.float32(2.0 ** -10)).astype(np.float32)).astype(np.float32)
+            out[i] = t.astype(np.float64).sum()
+            continue
+        if scheme in ("f16fold", "f16foldX"):
             # folded: hi (exact) first, then each 16-slot lo chunk rounded
             # onto the same fp32 accumulator
             acc = hi.astype(np.float32)
@@ -169,6 +231,8 @@ def main():
     hs = (4.0 / (1e6 * (d + 2))) ** (1.0 / (d + 4))
     s = math.sqrt(0.5 * LOG2E)
     yj = rng.normal(size=(N, d)) / hs * s
+    if len(sys.argv) > 5:      # force the grid: one particle at this norm
+        yj[0] *= float(sys.argv[5]) / np.sqrt((yj[0] ** 2).sum())
     lw = rng.normal(scale=0.3, size=N)
     lw2 = (lw - lw.max()) * LOG2E
     par = rng.integers(0, N, size=M)

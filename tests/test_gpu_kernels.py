@@ -1083,6 +1083,33 @@ def test_local_logpdf_f32_rows_independent(K, d, prec):
     np.testing.assert_allclose(np.exp(full - exact), 1.0, atol=1e-5)
 
 
+@pytest.mark.parametrize("d", [3, 6, 8])
+def test_local_mfma_launch_knobs_bit_identical(K, d, monkeypatch):
+    """The z-form pass's launch knobs (local_mfma.hip lz_run: ABC_LZ_IB point
+    tiles per wave, ABC_LZ_TPB particle tiles per LDS buffer) only change the
+    launch shape: every row is bit-identical under each."""
+    rng = np.random.default_rng(130 + d)
+    n, k = 12_000, 40
+    X = rng.normal(size=(n, d))
+    w = rng.uniform(0.1, 1.0, size=n)
+    nbr, _ = K.knn(dev(X), k)
+    covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
+    pts = np.concatenate([X[rng.integers(0, n, 2000)] +
+                          0.2 * rng.normal(size=(2000, d)),
+                          rng.normal(size=(50, d)) * 4])
+    base = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, "mfma"))
+    exact = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
+    np.testing.assert_allclose(np.exp(base - exact), 1.0, atol=1e-5)
+    for env in ({"ABC_LZ_IB": "2"}, {"ABC_LZ_IB": "1"}, {"ABC_LZ_TPB": "2"},
+                {"ABC_LZ_TPB": "8"}, {"ABC_LZ_IB": "2", "ABC_LZ_TPB": "8"}):
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, "mfma"))
+        for key in env:
+            monkeypatch.delenv(key)
+        np.testing.assert_array_equal(got, base, err_msg=str(env))
+
+
 @pytest.mark.parametrize("d", [2, 6])
 def test_knn_rows_tiled_equal_full(K, d):
     """Row ranges of the tiled kNN (the rank shares of the sharded fit) give

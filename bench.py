@@ -34,7 +34,7 @@ from pyabc_amd.distributed import Comm  # noqa: E402
 from pyabc_amd.engine import GenerationEngine, DeviceMVNFit  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (MI355X_MICROARCH.md)
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+MFMA16_PEAK_TFLOPS = 2500.0  # dense f16 / bf16 MFMA (no sparsity)
 CLOCK_HZ = 2.4e9
 HBM_PEAK_GBS = 8000.0
 
@@ -79,7 +79,7 @@ def kde_pmc(d):
     return None, None
 
 
-PROBE_MIX = {8: 0, 20: 2}   # tools/probes/issue_probe.hip variants
+PROBE_MIX = {8: 3, 20: 4}   # tools/probes/issue_probe.hip variants
 
 
 def issue_probe(d, waves_per_simd=2):
@@ -126,16 +126,17 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     pairs_per_s = pairs_per_launch / avg_launch_s
     fpp = 3 * d + 4
     D = K.padded_dim(d)
-    KL = (7 * D + 4 + 15) // 16
+    # f16 piece schemes (kde_mfma.hip Mk<D>): folded up to D = 24, split above
+    KH, KL = (D + 4 + 15) // 16, (5 * D + 4 + 15) // 16
     if pmc is not None:
         pt = pmc["per_tile"]
         V, T, F = (pt["SQ_INSTS_VALU"], pt.get("SQ_INSTS_VALU_TRANS_F32", 0.0),
                    pt["SQ_INSTS_MFMA"])
         src = f"{os.path.relpath(pmc_path, ROOT)} (rocprofv3 --pmc, per-tile)"
     else:   # static count of the kernel's per-tile code
-        F = (D + 6 + 15) // 16 + KL
-        # folded accumulation (KL <= 4): no hi + lo add (kde_mfma.hip)
-        V, T = (32.0 if KL <= 4 else 48.0), 16.0
+        F = KH + KL
+        # folded accumulation (D <= 24): no hi + lo add (kde_mfma.hip)
+        V, T = (32.0 if D <= 24 else 48.0), 16.0
         src = "static per-tile instruction count (no PMC file for this d)"
     cyc = max(4 * (V - T) + 8 * T + 8 * F, 32 * F)
     t_static = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
@@ -157,9 +158,9 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     mfma_tf = 32768 * F * tiles_per_launch / avg_launch_s / 1e12
     return {
         "bound": "issue (MFMA + VALU)",
-        "kernel": "MFMA KDE pass (exact-grid bf16 pieces: "
-                  "v_mfma_f32_32x32x16_bf16 for the d-dim exponent -- at "
-                  "d <= 8 hi and lo in one accumulator -- then v_exp_f32 + "
+        "kernel": "MFMA KDE pass (exact-grid f16 pieces: "
+                  "v_mfma_f32_32x32x16_f16 for the d-dim exponent, hi and "
+                  "lo in one accumulator up to d = 24 -- then v_exp_f32 + "
                   "the row-sum add per pair on the VALU)",
         "achieved": achieved_tf,
         "peak": peak_tf,
@@ -185,9 +186,9 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "pairs_per_s": pairs_per_s,
         "valu_equiv": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
                        "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS},
-        "mfma_bf16": {"achieved": mfma_tf, "peak": BF16_MFMA_PEAK_TFLOPS,
+        "mfma_f16": {"achieved": mfma_tf, "peak": MFMA16_PEAK_TFLOPS,
                       "unit": "TFLOP/s",
-                      "frac": mfma_tf / BF16_MFMA_PEAK_TFLOPS},
+                      "frac": mfma_tf / MFMA16_PEAK_TFLOPS},
     }
 
 
@@ -406,7 +407,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32 (KDE exponent from exact-grid bf16-piece MFMA, fp64 "
+        "dtype": "f32 (KDE exponent from exact-grid f16-piece MFMA, fp64 "
                  "row sums) / f64 (all other stages)",
         "data": "synthetic",
         "config": {

@@ -68,13 +68,17 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
 // Piece scheme per dimension class (compile-time; tools/kde_ab.py prices two
 // builds on one box):
 //   0 bf16 y1.y1, aH x3, bH x3 | seven cross terms per dimension, aL, bL
-//     (folded when KL <= kFoldKL) -- d <= 8;
+//     (folded when KL <= kFoldKL) -- d <= 8 up to round 3
+//     (-DABC_KDE_SCHEME_SMALL=0);
 //   1 f16 y1.y1, aH x2, bH x2 | five cross terms, aL, bL, the lo pieces
 //     x 2^10, split accumulation (hi exact, lo apart, e = fma(lo, 2^-10, hi))
 //     -- d > 24 (and 8 < d <= 24 with -DABC_KDE_SCHEME_LARGE=1);
 //   2 the same f16 pieces unscaled, every chunk accumulated onto one fp32
 //     value (folded: no hi + lo add per pair; the KL lo chunks each round at
-//     |e|) -- 8 < d <= 24.  Needs the MFMA to keep f16 denormal inputs
+//     |e|) -- d <= 24.  At d <= 8 it replaces scheme 0 (round 4, same box,
+//     N = M = 1e6: d = 8 128.3 -> 115.3 ms, 4 MFMAs per tile instead of 5,
+//     max row error on the kde_variants rows 4.3e-6 -> 3.0e-6; d = 2 91.7 ->
+//     83.9 ms, 3.2e-6 -> 9.8e-7; d = 4 96.4 -> 95.1 ms).  Needs the MFMA to keep f16 denormal inputs
 //     (tools/probes/mfma_f16_denorm.hip: outputs down to 2^-24).  Same box,
 //     N = M = 1e6, d = 20: 209.7 ms against 232.2 ms split; max row error
 //     on the kde_variants rows 4.5e-6 against 7.5e-7 (d = 12 / 16 / 24:
@@ -85,7 +89,7 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
 // 1.4e-5 -- 1.6e-5 at d = 16, 24; tools/probes/mfma_acc_round.hip: the
 // 32x32x16 MFMA is not one exact sum + one rounding).
 #ifndef ABC_KDE_SCHEME_SMALL
-#define ABC_KDE_SCHEME_SMALL 0
+#define ABC_KDE_SCHEME_SMALL 2
 #endif
 #ifndef ABC_KDE_SCHEME_LARGE
 #define ABC_KDE_SCHEME_LARGE 2

@@ -106,7 +106,7 @@ def main():
                 "probe_ns_per_tile_per_simd": rl["probe_ns_per_tile_per_simd"],
                 "static_cycles_per_tile": rl["static_issue"]["cycles_per_tile"],
                 "valu_equiv_frac_fp32": rl["valu_equiv"]["frac"],
-                "mfma_bf16_frac": rl["mfma_bf16"]["frac"],
+                "mfma_f16_frac": rl["mfma_f16"]["frac"],
                 "N": N, "M": N, "d": d}), flush=True)
             continue
         report(f"kde_logpdf_{prec}", t, pairs, "pairs", 3 * d + 4,

@@ -18,7 +18,8 @@
 //      (the bf16 piece scheme of rounds 1-3)
 //   2: d = 20, f16 pieces, split     --  9 MFMA, 16 exp, 40 other VALU
 //      (the f16 and bf16 32x32x16 MFMAs issue alike)
-//   3: d <= 8, f16 pieces, folded (round 4 default) -- 4 MFMA, 16 exp, 23
+//   3: d <= 8, f16 pieces, folded (round 4 default) -- 4 MFMA, 16 exp, 19
+//      (PMC, profiles/r04_kde_pmc.json: 39.3 VALU incl. the 4 MFMAs)
 //   4: d = 20, f16 pieces, folded (round 4 default) -- 9 MFMA, 16 exp, 19
 //
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC issue_probe.hip \
@@ -112,7 +113,7 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
     case 1: ns = time_mix<11, 16, 40>(waves_per_simd, iters, cus, out); break;
     case 2: ns = time_mix<9, 16, 40>(waves_per_simd, iters, cus, out); break;
-    case 3: ns = time_mix<4, 16, 23>(waves_per_simd, iters, cus, out); break;
+    case 3: ns = time_mix<4, 16, 19>(waves_per_simd, iters, cus, out); break;
     case 4: ns = time_mix<9, 16, 19>(waves_per_simd, iters, cus, out); break;
     default: break;
   }

@@ -117,11 +117,10 @@ def test_kde_mfma_all_dims_vs_oracle(K, d):
     np.testing.assert_allclose(got, expect, rtol=1e-5)
 
 
-@pytest.mark.parametrize("d", [3, 12])
+@pytest.mark.parametrize("d", [1, 3, 8, 12])
 def test_kde_mfma_out_of_grid_rows(K, d):
-    """New rows beyond the population's grid range (bf16 pieces, d <= 8:
-    |y| > 256 g; f16 pieces, d > 8: |y| > 2040 g) are flagged by the
-    packer and evaluated by the exact fixup."""
+    """New rows beyond the population's grid range (f16 pieces: |y| > 2040 g)
+    are flagged by the packer and evaluated by the exact fixup."""
     rng = np.random.default_rng(5)
     X = rng.normal(size=(2000, d))
     w = np.full(2000, 1 / 2000)
@@ -135,14 +134,15 @@ def test_kde_mfma_out_of_grid_rows(K, d):
     np.testing.assert_allclose(lp, expect, rtol=2e-6, atol=1e-5)
 
 
+@pytest.mark.parametrize("d", [2, 8, 12])
 @pytest.mark.parametrize("far,wfar", [(30.0, 1e-6), (3e3, 1e-12), (3e6, 1e-15)])
-def test_kde_mfma_f16_grid_extremes(K, far, wfar):
-    """d > 8 (f16 pieces): a light particle far out makes the population's
-    largest whitened norm 2^7 ... 2^24, i.e. the aH / bH pieces scaled by
-    2^-K (K = 2E - 13) and, past 2^13, the all-fixup packing; every row
-    against the oracle."""
-    rng = np.random.default_rng(int(far))
-    N, M, d = 3000, 300, 12
+def test_kde_mfma_f16_grid_extremes(K, far, wfar, d):
+    """f16 pieces (every d since round 4): a light particle far out makes the
+    population's largest whitened norm 2^7 ... 2^24, i.e. the aH / bH pieces
+    scaled by 2^-K (K = 2E - 13) and, past 2^13, the all-fixup packing;
+    every row against the oracle."""
+    rng = np.random.default_rng(int(far) + d)
+    N, M = 3000, 300
     X = rng.normal(size=(N, d))
     X[0] = far
     w = rng.uniform(0.5, 1.5, N)

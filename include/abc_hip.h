@@ -174,10 +174,11 @@ int abc_kde_logsum_f64(const double* Ynew, const double* Yprev,
                        const double* logw, int64_t M, int64_t N, int d,
                        double log_offset, double* out_log_sum, void* ws,
                        size_t ws_bytes, hipStream_t stream);
-/* Same density on the matrix cores (v_mfma_f32_32x32x16_bf16): the
+/* Same density on the matrix cores (v_mfma_f32_32x32x16_f16): the
  * exponent lw2_j - |y_i - y_j|^2 is expanded as a_j + b_i + 2 y_i.y_j with
- * every operand split into bf16 pieces on a power-of-two grid so that the
- * large part of the sum is EXACT in the fp32 accumulator.
+ * every operand split into f16 pieces on a power-of-two grid so that the
+ * large part of the sum is EXACT in the fp32 accumulator (the
+ * piece scheme per dimension class is kde_mfma.hip's Mk<D>::SCH).
  * Afr: population fragments (abc_kde_mfma_prev_bytes), built with the
  * fp64 whitened population P [npad][D+1] by abc_kde_pack_prev_mfma (which
  * also writes lw2max and the grid g to gscale; ws >= 128 B).  Bfr: new-row

@@ -213,7 +213,7 @@ def psd_whitening(cov):
 
 class WhitenedRows:
     """New rows prepared for the MFMA KDE pass: direct fp64 whitened rows
-    (exact underflow fixup) plus the bf16 piece fragments of the B operand."""
+    (exact underflow fixup) plus the f16 piece fragments of the B operand."""
 
     def __init__(self, Y, frags, M):
         self.Y, self.frags, self.M = Y, frags, M
@@ -223,7 +223,7 @@ class WhitenedRows:
 class PackedPopulation:
     """The previous population packed for the KDE pass (built once per fit).
 
-    precision: "mfma" (default: exact-grid bf16 pieces on the matrix cores,
+    precision: "mfma" (default: exact-grid f16 pieces on the matrix cores,
     kde_mfma.hip), "f32" (direct fp32 VALU pass) or "f64" (fp64 VALU pass).
     """
 

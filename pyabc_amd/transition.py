@@ -152,7 +152,7 @@ class MultivariateNormalTransition(Transition):
 
     fit: weighted moments kernel + host d x d finish (smart_cov * bw^2 *
     scaling, multivariatenormal.py:67-85).  rvs: device resampling +
-    perturbation (Philox).  pdf: device KDE pass (exact-grid bf16 MFMA by
+    perturbation (Philox).  pdf: device KDE pass (exact-grid f16 MFMA by
     default; ``kde_precision="f32"`` for the direct fp32 kernel,
     ``kde_precision="f64"`` for the fp64 kernel).
     """

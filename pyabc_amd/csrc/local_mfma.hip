@@ -64,7 +64,10 @@ typedef short h16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kLzWaves = 4;
+#ifndef ABC_LZ_WAVES
+#define ABC_LZ_WAVES 4
+#endif
+constexpr int kLzWaves = ABC_LZ_WAVES;  // waves per block sharing the LDS stream
 constexpr double kLzGrid = 0.00390625;       // g = 2^-8
 constexpr double kLzRowNorm = 7.9;           // |u'| bound of the grid
 constexpr float kLzLo = 4096.0f;             // lo pieces x 2^12

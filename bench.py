@@ -80,13 +80,16 @@ def kde_pmc(d):
 
 
 PROBE_MIX = {8: 3, 20: 4}   # tools/probes/issue_probe.hip variants
+PROBE_WAVES = {8: 4, 20: 2}  # the KDE kernel's occupancy (waves per SIMD)
 
 
-def issue_probe(d, waves_per_simd=2):
+def issue_probe(d, waves_per_simd=None):
     """Live ceiling of the KDE kernel's per-tile instruction mix on THIS GPU
     (tools/probes/issue_probe.hip: the mix with no memory traffic, VALU in
-    the MFMA gaps, at the kernel's 2 waves per SIMD): ns per tile and SIMD,
-    or None when the probe library is not built or has no mix for d."""
+    the MFMA gaps, at the kernel's own waves per SIMD): ns per tile and
+    SIMD, or None when the probe library is not built or has no mix for d."""
+    if waves_per_simd is None:
+        waves_per_simd = PROBE_WAVES.get(d, 2)
     import ctypes
     path = os.path.join(ROOT, "tools", "probes", "libabc_probe.so")
     v = PROBE_MIX.get(d)
@@ -110,7 +113,7 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     accumulation is split, d > 8).  The ceiling is MEASURED live: the probe
     (tools/probes/issue_probe.hip) runs that per-tile mix -- PMC-counted,
     profiles/r0*_kde_pmc.json -- with no memory traffic and the VALU spread
-    over the MFMA gaps, at the kernel's occupancy (2 waves per SIMD) on
+    over the MFMA gaps, at the kernel's own occupancy (PROBE_WAVES) on
     every SIMD of this GPU, so clock and dual-wave issue are those the chip
     really sustains:
 
@@ -145,7 +148,7 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         t_ceil = tiles_per_launch * ns_probe * 1e-9 / 1024
         basis = ("live issue probe on this GPU (tools/probes/issue_probe.hip: "
                  "the kernel's per-tile mix, no memory traffic, VALU in the "
-                 "MFMA gaps, 2 waves per SIMD) x tiles / 1024 SIMDs; "
+                 f"MFMA gaps, {PROBE_WAVES.get(d, 2)} waves per SIMD) x tiles / 1024 SIMDs; "
                  f"mix counts: {src}; algorithmic {fpp} FLOP/pair")
     else:
         t_ceil = t_static

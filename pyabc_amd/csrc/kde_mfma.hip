@@ -1091,8 +1091,22 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
   }
 }
 
+// waves per SIMD the folded LDS pass is compiled for (register budget
+// 512 / waves).  The headline d = 8 form needs 129 VGPRs unconstrained, one
+// over the 4-wave budget: held to 128 (2 spilled outside the loop) it runs
+// 114.5 vs 115.5 ms at N = M = 1e6, interleaved (gpurun_out/r04x).  d = 20
+// held to 3 waves (168 VGPRs, 6 spilled): 206.8 vs 206.0 ms -- no hint.
+#ifndef ABC_KDE_LDS2G_WAVES
+#define ABC_KDE_LDS2G_WAVES 1
+#endif
+constexpr int lds2g_waves(int KT, int IB) {
+  return ABC_KDE_LDS2G_WAVES != 0 && KT * IB <= 8 ? 4 : 1;
+}
+
 template <int KH, int KL, int IB, int SCH>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2g_kernel(
+__global__ __launch_bounds__(64 * kWaves)
+__attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB))))
+void kde_mfma_lds2g_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;

@@ -236,6 +236,10 @@ int abc_pnorm_distance_f64(const double* stats_T, int64_t ld,
  *                                                    distance/scale.py:38-65
  * as gathered by AdaptivePNormDistance._update      distance/distance.py:253-297 */
 size_t abc_column_select_workspace_bytes(int S);
+/* Median (and MAD when mad_out != NULL) of every column of data_T [S][ld],
+ * np.median semantics, bit-exact.  Synchronises `stream` once per order
+ * statistic (a 4-byte read-back of the settled-column count, which skips
+ * the radix passes when the sampled bracket settled every column). */
 int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
                               int S, double* median_out, double* mad_out,
                               void* ws, size_t ws_bytes, hipStream_t stream);

@@ -102,8 +102,9 @@ def test_kde_large_random_vs_oracle(K):
 
 @pytest.mark.parametrize("d", [1, 2, 3, 5, 8, 12, 20, 32])
 def test_kde_mfma_all_dims_vs_oracle(K, d):
-    """Exact-grid bf16 MFMA pass at every padded-dimension instance,
-    including ragged N / M (tails of 32-row tiles and 64-row chunks)."""
+    """Exact-grid f16 MFMA pass at every padded-dimension instance (folded
+    up to d = 24, split above), including ragged N / M (tails of 32-row
+    tiles and 64-row chunks)."""
     rng = np.random.default_rng(100 + d)
     N, M = 3001 + 7 * d, 517
     X = rng.normal(size=(N, d)) * rng.uniform(0.5, 3, d) + 1.0
@@ -115,6 +116,30 @@ def test_kde_mfma_all_dims_vs_oracle(K, d):
     pp = _packed(K, X, w, cov, "mfma")
     got = np.exp(host(pp.logpdf(dev(theta))))
     np.testing.assert_allclose(got, expect, rtol=1e-5)
+
+
+@pytest.mark.parametrize("d", [2, 4, 6, 8, 16])
+def test_kde_mfma_anisotropic_heavy_weights(K, d):
+    """A strongly correlated population (condition number ~1e4), log-normal
+    weights over eight decades, rows near and far (1.5x outward), ragged
+    sizes: every row against the oracle at north_star's 1e-5."""
+    rng = np.random.default_rng(300 + d)
+    N, M = 6007, 611
+    A = rng.normal(size=(d, d))
+    Q, _ = np.linalg.qr(A)
+    scales = np.logspace(0, 2, d)
+    X = (rng.normal(size=(N, d)) * scales) @ Q.T + 3.0
+    w = np.exp(rng.normal(scale=3.0, size=N))
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    theta = np.concatenate([X[rng.integers(0, N, M - 100)]
+                            + 0.1 * rng.normal(size=(M - 100, d)) * scales,
+                            3.0 + 1.5 * (X[:100] - 3.0)])
+    expect = ref.kde_transition_pd(theta, X, w, cov)
+    pp = _packed(K, X, w, cov, "mfma")
+    got = np.exp(host(pp.logpdf(dev(theta))))
+    ok = expect > 0
+    np.testing.assert_allclose(got[ok], expect[ok], rtol=1e-5)
 
 
 @pytest.mark.parametrize("d", [1, 3, 8, 12])

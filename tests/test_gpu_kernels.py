@@ -969,10 +969,12 @@ def test_knn_fp32_filter_exact(K, case):
     np.testing.assert_array_equal(d2, np.take_along_axis(D2, want, axis=1))
 
 
-def test_local_logpdf_underflow_fixup(K):
+@pytest.mark.parametrize("prec,rtol", [("f64", 1e-11), ("f32", 1e-5), ("mfma", 1e-5)])
+def test_local_logpdf_underflow_fixup(K, prec, rtol):
     """Points far from every particle: the fixed-offset sum underflows and
     the rows go through the exact max-then-sum fixup (log space), matching a
-    numpy log-sum-exp of the same terms; near points take the main pass."""
+    numpy log-sum-exp of the same terms; near points take the main pass
+    (fp64, fp32 pair loop or the z form on the matrix cores)."""
     rng = np.random.default_rng(11)
     n, d, k = 3000, 4, 20
     X = rng.normal(size=(n, d))
@@ -981,7 +983,7 @@ def test_local_logpdf_underflow_fixup(K):
     covs, invs, dets = K.local_cov(dev(X), dev(w), nbr)
     pts = np.concatenate([rng.normal(size=(5, d)),
                           np.full((3, d), 25.0) + rng.normal(size=(3, d))])
-    got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets))
+    got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, prec))
     inv, det = host(invs), host(dets)
     diff = pts[:, None, :] - X[None, :, :]
     q = np.einsum("mna,nab,mnb->mn", diff, inv, diff)
@@ -989,7 +991,9 @@ def test_local_logpdf_underflow_fixup(K):
     mx = e.max(axis=1, keepdims=True)
     want = (mx[:, 0] + np.log(np.exp(e - mx).sum(axis=1))) - np.log(w.sum())
     assert np.all(np.isfinite(got))
-    np.testing.assert_allclose(got, want, rtol=1e-11)
+    # far rows: exact fixup at every precision
+    np.testing.assert_allclose(got[5:], want[5:], rtol=1e-11)
+    np.testing.assert_allclose(np.exp(got[:5] - want[:5]), 1.0, atol=rtol)
 
 
 @pytest.mark.parametrize("n", [1, 2, 1023, 300_001])

@@ -43,11 +43,16 @@
 // particle for d = 5..8 (4 particles per tile, the rows placed so that each
 // lane holds two particles whole: lz_row) and DP = 4
 // for d <= 4 (8 particles per tile, a particle whole in one lane).  The
-// particles stream through LDS (LDS-DMA, two tiles per buffer, double
-// buffered); each wave holds IB 32-point tiles of the evaluation points in
-// registers.  The particle range is cut into segments that depend on N only
-// and each row's terms are summed in a fixed order, so a row's bits do not
-// depend on M, the launch shape or the number of ranks.
+// particles stream through LDS (LDS-DMA, TPB = 4 particle tiles per buffer
+// with their (lc2, cf) pairs, double buffered); each wave holds IB = 4
+// 32-point tiles of the evaluation points in registers (128 VGPRs: four
+// waves per SIMD).  The VALU stages of one (particle tile, point tile)
+// product run in the MFMA gaps of the next ones (lz_kernel).  The particle
+// range is cut into segments that depend on N only and each row's terms are
+// summed in a fixed order (fp32 over 4 particle tiles, then fp64), so a
+// row's bits do not depend on M, the launch shape or the number of ranks.
+// N = M = 2e5, d = 6: 21 ms for the whole pass (35.7 ms fp32 pair loop),
+// at the SIMD's issue bound.
 #include <cmath>
 
 #include "common.hpp"

@@ -1,4 +1,4 @@
-// KDE importance-weight pass on the matrix cores: exact-grid bf16 MFMA.
+// KDE importance-weight pass on the matrix cores: exact-grid MFMA.
 // Same quantity as kde.hip (MultivariateNormalTransition.pdf, reference
 // pyabc/transition/multivariatenormal.py:102-125 via smc.py:722-733):
 //
@@ -7,33 +7,36 @@
 // expanded as e_ij = a_j + b_i + 2 y_i.y_j with a_j = lw2_j - |y_j|^2 and
 // b_i = -|y_i|^2.  The expansion cancels catastrophically in fp32 (a plain
 // fp32 GEMM form loses 4e-5 relative at N = 1e6, d = 8), so every operand is
-// split into bf16 pieces that make the large part of the sum EXACT:
+// split into 16-bit pieces that make the large part of the sum EXACT.  The
+// default (round 4, every d up to 24) is f16 (Mk<D>::SCH, below):
 //
-//   y = y1 + y2 + y3   y1 = g*rint(y/g) on a fixed power-of-two grid g with
-//                      |y1/g| <= 256 (8 significant bits: exact in bf16),
-//                      y2 = bf16(y - y1), y3 = bf16(y - y1 - y2)
-//   a = aH0 + aH1 + aH2 + aL0 + aL1   (aH* bf16 multiples of G = g^2 holding
-//                      rint(a/G)*G exactly, aL* = bf16 pieces of the rest)
+//   y = y1 + r2 + r3   y1 = g*rint(y/g) on a power-of-two grid g from the
+//                      population's largest norm (|y1/g| <= 2043: f16
+//                      integers), r2 = f16(y - y1), r3 = f16(rest)
+//   a = aH0 + aH1 + aL0 + aL1   (aH* f16 multiples of G = g^2 holding
+//                      rint(a/G)*G exactly, aL* = f16 pieces of the rest)
 //
 // hi = sum_k 2 y1_ik y1_jk + aH + bH is a sum of multiples of G below
-// 2^24 G, so the fp32 MFMA accumulation is exact in ANY order; lo (the
-// seven y1/y2/y3 cross products per dimension + aL + bL) is small (|lo| <~
-// 4) and accumulates with ~1e-7 absolute error.  e = hi + lo is rounded
-// once, so the exponent carries one fp32 rounding at |e| -- tighter than
-// the direct fp32 difference form of kde.hip (max 9e-6 vs 3e-5 relative on
-// rows far outside the population, SURVEY 8(a3) tolerance 1e-5).
+// 2^24 G, so the fp32 MFMA accumulation is exact in ANY order; lo (five
+// cross products per dimension + aL + bL) is small and accumulates on top
+// of hi in the same accumulator (folded: the MFMA delivers e itself; a hi
+// chunk never carries lo products -- an MFMA's internal sum is not exact,
+// tools/probes/mfma_acc_round.hip).  The bf16 scheme of rounds 1-3 (seven
+// cross terms, 8-bit y1) and the split f16 form (lo x 2^10 in its own
+// accumulator, one rounding at |e|) are kept for d > 24 and as build options.
 //
-// MFMA mapping (v_mfma_f32_32x32x16_bf16): A = previous population (rows =
+// MFMA mapping (v_mfma_f32_32x32x16_f16): A = previous population (rows =
 // j), B = new rows (columns = i), K = the piece slots.  KH chunks of 16
-// slots feed the hi accumulator, KL chunks the lo accumulator; each lane
-// owns one new row (column lane&31) and 16 j's of the 32-row tile, so per
-// pair the VALU does only  v_add (hi+lo), v_exp_f32, v_add (row sum).
-// The j-range uses kde.hip's fixed segments, each lane's values are summed in
-// register order and the two lane halves combined in a fixed order, so a
-// row's bits are independent of M, of the launch shape and of the number of
-// ranks.  Rows whose sum underflows -- and new rows outside the grid range
-// (|y| > 256 g, flagged by b = -inf) -- go through kde.hip's exact fixup,
-// in fp64 on the fp64 whitened rows (Ynew [M][D], P [npad][D+1]).
+// slots carry the hi products, KL chunks the lo products; each lane owns one
+// new row (column lane&31) and 16 j's of the 32-row tile, so per pair the
+// VALU does only v_exp_f32 and the row-sum add (plus the hi + lo add where
+// the accumulation is split).  The j-range uses kde.hip's fixed segments,
+// each lane's values are summed in register order and the two lane halves
+// combined in a fixed order, so a row's bits are independent of M, of the
+// launch shape and of the number of ranks.  Rows whose sum underflows -- and
+// new rows outside the grid range (flagged by b = -inf) -- go through
+// kde.hip's exact fixup, in fp64 on the fp64 whitened rows (Ynew [M][D],
+// P [npad][D+1]).
 #include <cmath>
 
 #include "common.hpp"

@@ -16,6 +16,17 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // the global offset L = max_n lc_n (ordered-key atomic max), and the
 // symmetric quadratic-form coefficients of inv_n packed row by row:
 // (A_aa, A_ab + A_ba for b > a), d(d+1)/2 per particle.
+__device__ inline void local_pack_coef(const double* __restrict__ invs, int64_t n,
+                                       int d, double* __restrict__ coef) {
+  const double* A = invs + n * d * d;
+  double* c = coef + n * (d * (d + 1) / 2);
+  int t = 0;
+  for (int a = 0; a < d; ++a) {
+    c[t++] = A[a * d + a];
+    for (int b = a + 1; b < d; ++b) c[t++] = A[a * d + b] + A[b * d + a];
+  }
+}
+
 __global__ __launch_bounds__(256) void local_const_kernel(
     const double* __restrict__ w, const double* __restrict__ dets,
     const double* __restrict__ invs, int64_t N, int d,
@@ -28,15 +39,19 @@ __global__ __launch_bounds__(256) void local_const_kernel(
     const double v = w[n] > 0.0 ? log(w[n] / norm) : -INFINITY;
     lc[n] = v;
     if (v == v) key = f64_key(v);
-    const double* A = invs + n * d * d;
-    double* c = coef + n * (d * (d + 1) / 2);
-    int t = 0;
-    for (int a = 0; a < d; ++a) {
-      c[t++] = A[a * d + a];
-      for (int b = a + 1; b < d; ++b) c[t++] = A[a * d + b] + A[b * d + a];
-    }
+    if (coef) local_pack_coef(invs, n, d, coef);
   }
   block_atomic_max_u64<256>(lc_max_key, static_cast<unsigned long long>(key));
+}
+
+// the z-form pass needs the packed coefficients only for its fixup rows:
+// built after the main pass, and only when some row needs them
+__global__ __launch_bounds__(256) void local_coef_kernel(
+    const double* __restrict__ invs, int64_t N, int d, double* __restrict__ coef,
+    const int* __restrict__ n_fix) {
+  if (*n_fix == 0) return;
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (n < N) local_pack_coef(invs, n, d, coef);
 }
 
 // q = (theta - X_n)^T inv_n (theta - X_n) from the packed symmetric form
@@ -132,25 +147,44 @@ __global__ __launch_bounds__(256) void local_pdf_fixup_kernel(
   }
 }
 
-// one block of 1024 threads, four independent partial sums per thread (the
-// 256-thread single-chain form took 0.29 ms at N = 2e5: load latency bound);
-// a fixed order, so the sum is the same bits run to run
-__global__ __launch_bounds__(1024) void local_sumw_kernel(const double* __restrict__ w,
-                                                          int64_t N,
-                                                          double* __restrict__ out) {
-  __shared__ double red[16];
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t i0 = threadIdx.x; i0 < N; i0 += 4 * 1024) {
+// log(sum w) in two fixed-order stages: `nb` blocks sum contiguous ranges
+// into part[0 .. nb) (eight loads in flight per thread), one wave adds the
+// nb partials in order -- the same bits run to run.  (One 1024-thread block
+// took 89 us at N = 2e5, latency bound; 0.29 ms with 256 threads.)
+__global__ __launch_bounds__(256) void local_sumw_part_kernel(const double* __restrict__ w,
+                                                              int64_t N,
+                                                              double* __restrict__ part) {
+  __shared__ double red[4];
+  const int64_t chunk = ceil_div(N, static_cast<int64_t>(gridDim.x));
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * chunk;
+  int64_t hi = lo + chunk;
+  if (hi > N) hi = N;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * 256) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = i0 + u * 1024;
-      if (i < N) s[u] += w[i];
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + u * 256;
+      if (i < hi) s[u] += w[i];
     }
   }
-  const double t = block_sum<double, 1024>((s[0] + s[1]) + (s[2] + s[3]), red);
-  if (threadIdx.x == 0) *out = log(t);
+  const double t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  const double b = block_sum<double, 256>(t, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = b;
 }
-
+__global__ void local_sumw_final_kernel(const double* __restrict__ part, int nb,
+                                        double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += part[b];
+  *out = log(s);
+}
+// launch both (part: >= nb doubles of scratch that is free until the main
+// pass; nb = the pass's split, >= 1)
+inline void local_sumw(const double* w, int64_t N, int nb, double* part, double* out,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(local_sumw_part_kernel, dim3(nb), dim3(256), 0, st, w, N, part);
+  hipLaunchKernelGGL(local_sumw_final_kernel, dim3(1), dim3(64), 0, st, part, nb, out);
+}
 
 // The n-range is cut into a fixed number of chunks that depends on N only,
 // so a row's log-sum-exp does not depend on M or on how rows are shared

@@ -616,9 +616,10 @@ int lz_run(const double* pts, int64_t M, const double* X, const double* w,
   h16x8* B = reinterpret_cast<h16x8*>(q);
   ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
   ABC_HIP(hipMemsetAsync(ex, 0, 128, st));
-  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(1024), 0, st, w, N, logsumw);
+  local_sumw(w, N, split, part, logsumw, st);
+  // the packed coefficients only for fixup rows (local_coef_kernel below)
   hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, st,
-                     w, dets, invs, N, D, lc, coef, lc_max_key);
+                     w, dets, invs, N, D, lc, static_cast<double*>(nullptr), lc_max_key);
   hipLaunchKernelGGL(lz_dims_kernel<D>, dim3(stream_grid(N, 256, 512)), dim3(256),
                      0, st, X, N, dkeys);
   hipLaunchKernelGGL(lz_pack_prev_kernel<D>, dim3(ceil_div(p.npad, 128)), dim3(128),
@@ -652,6 +653,8 @@ int lz_run(const double* pts, int64_t M, const double* X, const double* w,
   hipLaunchKernelGGL(lz_final_kernel, dim3(ceil_div(M, 256)), dim3(256), 0, st, part,
                      M, p.nseg, lc_max_key, logsumw, gflag, rflag, out, n_fix,
                      fix_rows);
+  hipLaunchKernelGGL(local_coef_kernel, dim3(ceil_div(N, 256)), dim3(256), 0, st, invs,
+                     N, D, coef, n_fix);
   hipLaunchKernelGGL(local_pdf_fixup_kernel<D>, dim3(1024), dim3(256), 0, st, pts, X,
                      coef, lc, N, logsumw, n_fix, fix_rows, out);
   return kOk;

@@ -170,7 +170,7 @@ int abc_local_logpdf_f32(const double* pts, int64_t M, const double* X,
   float* pts32 = lc32 + Np;
   float* pts32lo = pts32 + M * 8;
   ABC_HIP(hipMemsetAsync(base + 8, 0, 16, st));
-  hipLaunchKernelGGL(local_sumw_kernel, dim3(1), dim3(1024), 0, st, w, N, logsumw);
+  local_sumw(w, N, split, part, logsumw, st);
   hipLaunchKernelGGL(local_const_kernel, dim3(ceil_div(N, 256)), dim3(256), 0,
                      st, w, dets, inv_covs, N, d, lc, coef, lc_max_key);
   const unsigned grid = static_cast<unsigned>(ceil_div(M, 256) * split);

@@ -10,7 +10,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
          1: "d=20 split, bf16 pieces: 11 MFMA, 16 v_exp_f32, 40 v_add_f32",
-         2: "d=20 split, f16 pieces: 9 MFMA, 16 v_exp_f32, 40 v_add_f32"}
+         2: "d=20 split, f16 pieces: 9 MFMA, 16 v_exp_f32, 40 v_add_f32",
+         3: "d<=8 folded f16 (round 4): 4 MFMA, 16 v_exp_f32, 19 v_add_f32",
+         4: "d=20 folded f16 (round 4): 9 MFMA, 16 v_exp_f32, 19 v_add_f32",
+         5: "mix 3 + 2 ds_read_b128 per step",
+         6: "mix 3 + 2 ds_read_b128 per step + barrier every 2 steps",
+         7: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 2 steps",
+         8: "mix 3 + 2 ds_read_b128 per step + barrier every 4 steps",
+         9: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 4 steps",
+         10: "mix 3 + 2 ds_read_b128 per step + barrier every 8 steps",
+         11: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 8 steps"}
 
 
 def load():
@@ -26,7 +35,7 @@ def main():
     lib = load()
     out = []
     for v, desc in MIXES.items():
-        for wps in (1, 2, 3):
+        for wps in (1, 2, 3, 4):
             ns = lib.abc_probe_kde_mix(v, wps, 100000)
             out.append(dict(variant=v, mix=desc, waves_per_simd=wps,
                             ns_per_step_per_simd=ns))

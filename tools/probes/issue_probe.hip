@@ -21,6 +21,11 @@
 //   3: d <= 8, f16 pieces, folded (round 4 default) -- 4 MFMA, 16 exp, 19
 //      (PMC, profiles/r04_kde_pmc.json: 39.3 VALU incl. the 4 MFMAs)
 //   4: d = 20, f16 pieces, folded (round 4 default) -- 9 MFMA, 16 exp, 19
+//   5-7: mix 3 plus the headline kernel's memory path (mix_mem_kernel):
+//      5 two ds_read_b128 per step, 6 + a block barrier every 2 steps,
+//      7 + the LDS-DMA refill of the other buffer before each barrier;
+//      8 / 9 as 6 / 7 with the barrier every 4 steps (the kernel's 64-row
+//      chunk: 2 j-tiles x IB = 2), 10 / 11 every 8 steps (128-row chunks)
 //
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC issue_probe.hip \
 //         -o libabc_probe.so
@@ -69,6 +74,94 @@ __global__ __launch_bounds__(256) void mix_kernel(float* out, int iters) {
   out[blockIdx.x * 256 + threadIdx.x] = t;
 }
 
+// The same mix with the headline kernel's memory path added step by step
+// (variants 5-7): DSR ds_read_b128 A fragments per step (read one step
+// ahead, feeding the MFMAs), a block barrier every BAR steps, and with DMA
+// the LDS-DMA refill of the other buffer (8 KB per block from an L2-resident
+// source, waited with vmcnt(0) before the barrier) -- the per-64-row-chunk
+// pattern of kde_mfma_lds2g_kernel.
+template <int NM, int NE, int NA, int DSR, int BAR, int DMA>
+__global__ __launch_bounds__(256) void mix_mem_kernel(float* out, int iters,
+                                                      const bf16x8* __restrict__ src) {
+  __shared__ bf16x8 As[2][8][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
+  for (int f = wave; f < 16; f += 4) {
+    bf16x8 x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      h ^= h >> 13; h *= 0x5bd1e995u;
+      x[e] = static_cast<short>(0x3C00 | (h & 0x7F));
+    }
+    As[f >> 3][f & 7][lane] = x;
+  }
+  bf16x8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h ^= h >> 13; h *= 0x5bd1e995u;
+    b[e] = static_cast<short>(0xBC00 | ((h >> 8) & 0x7F));
+  }
+  __syncthreads();
+  f32x16 acc = {};
+  float v[16];
+  const float s = 1e-7f * (threadIdx.x & 7);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = -1e-3f * (threadIdx.x + k);
+  int buf = 0;
+  bf16x8 a = As[0][0][lane];
+  for (int i = 0; i < iters; ++i) {
+    if (BAR > 0 && i % BAR == 0) {
+      if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (DMA) {
+        const bf16x8* g = src + (i & 1023) * 8 * 64;
+        for (int f = wave; f < 8; f += 4)
+          __builtin_amdgcn_global_load_lds(
+              g + f * 64 + lane,
+              (__attribute__((address_space(3))) void*)&As[buf ^ 1][f][0], 16, 0, 0);
+      }
+      buf ^= 1;
+    }
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+      if (m < DSR) a = As[buf][(i * DSR + m + 1) & 7][lane];
+#pragma unroll
+      for (int k = m * NE / NM; k < (m + 1) * NE / NM; ++k) ABC_EXP(v[k & 15])
+#pragma unroll
+      for (int k = m * NA / NM; k < (m + 1) * NA / NM; ++k)
+        ABC_ADD(v[(k + 5) & 15], s)
+    }
+  }
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += v[k] + acc[k];
+  out[blockIdx.x * 256 + threadIdx.x] = t;
+}
+
+template <int NM, int NE, int NA, int DSR, int BAR, int DMA>
+double time_mem_mix(int waves_per_simd, int iters, int cus, float* out,
+                    const bf16x8* src) {
+  const int blocks = cus * waves_per_simd;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((mix_mem_kernel<NM, NE, NA, DSR, BAR, DMA>), dim3(blocks),
+                       dim3(256), 0, 0, out, iters, src);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep > 0 && ms < best) best = ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return best * 1e6 / (static_cast<double>(waves_per_simd) * iters);
+}
+
 template <int NM, int NE, int NA>
 double time_mix(int waves_per_simd, int iters, int cus, float* out) {
   const int blocks = cus * waves_per_simd;  // 4 waves per block, 1 per SIMD
@@ -108,6 +201,12 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
   float* out = nullptr;
   if (hipMalloc(&out, static_cast<size_t>(cus) * 8 * 256 * 4) != hipSuccess)
     return -1.0;
+  bf16x8* src = nullptr;  // DMA source: 1024 chunks of 8 KB (8 MB, L2/MALL)
+  if (hipMalloc(&src, size_t{1024} * 8 * 64 * 16) != hipSuccess) {
+    (void)hipFree(out);
+    return -1.0;
+  }
+  (void)hipMemset(src, 0x3C, size_t{1024} * 8 * 64 * 16);
   double ns = -1.0;
   switch (variant) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
@@ -115,8 +214,16 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 2: ns = time_mix<9, 16, 40>(waves_per_simd, iters, cus, out); break;
     case 3: ns = time_mix<4, 16, 19>(waves_per_simd, iters, cus, out); break;
     case 4: ns = time_mix<9, 16, 19>(waves_per_simd, iters, cus, out); break;
+    case 5: ns = time_mem_mix<4, 16, 19, 2, 0, 0>(waves_per_simd, iters, cus, out, src); break;
+    case 6: ns = time_mem_mix<4, 16, 19, 2, 2, 0>(waves_per_simd, iters, cus, out, src); break;
+    case 7: ns = time_mem_mix<4, 16, 19, 2, 2, 1>(waves_per_simd, iters, cus, out, src); break;
+    case 8: ns = time_mem_mix<4, 16, 19, 2, 4, 0>(waves_per_simd, iters, cus, out, src); break;
+    case 9: ns = time_mem_mix<4, 16, 19, 2, 4, 1>(waves_per_simd, iters, cus, out, src); break;
+    case 10: ns = time_mem_mix<4, 16, 19, 2, 8, 0>(waves_per_simd, iters, cus, out, src); break;
+    case 11: ns = time_mem_mix<4, 16, 19, 2, 8, 1>(waves_per_simd, iters, cus, out, src); break;
     default: break;
   }
+  (void)hipFree(src);
   (void)hipFree(out);
   return ns;
 }

@@ -1106,6 +1106,17 @@ constexpr int lds2g_waves(int KT, int IB) {
   return ABC_KDE_LDS2G_WAVES != 0 && KT * IB <= 8 ? 4 : 1;
 }
 
+// 32-row tiles of A per LDS stage of the folded pass (one barrier per
+// stage): 4 since round 4 (2 before); the issue probe with the kernel's
+// memory path (tools/probes/issue_probe.hip variants 9 / 11) measures 124.3
+// vs 119.0 ns per tile step at 4 waves per SIMD for 2 vs 4; the kernel,
+// interleaved on one box (gpurun_out/r04aj): 122.9 / 122.8 -> 121.1 /
+// 121.1 ms at N = M = 1e6, d = 8; 222.0 -> 221.0 ms at d = 20
+#ifndef ABC_KDE_STAGE_TILES
+#define ABC_KDE_STAGE_TILES 4
+#endif
+constexpr int kLds2gStageTiles = ABC_KDE_STAGE_TILES;
+
 template <int KH, int KL, int IB, int SCH>
 __global__ __launch_bounds__(64 * kWaves)
 __attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB))))
@@ -1113,9 +1124,11 @@ void kde_mfma_lds2g_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
-  constexpr int CH = 2 * KT;
+  constexpr int TPS = kLds2gStageTiles;  // 32-row tiles per LDS stage
+  constexpr int CH = TPS * KT;
   static_assert(kFolded<KL, SCH>, "folded accumulation only");
   static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
+  static_assert(TPS % 2 == 0, "stages hold whole 64-row chunks");
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1139,49 +1152,65 @@ void kde_mfma_lds2g_kernel(
     double S[IB];
 #pragma unroll
     for (int t = 0; t < IB; ++t) S[t] = 0.0;
-    auto fill = [&](int buf, int jc) {
+    // tiles [jc/32, jc/32 + nt) into buffer buf (nt: TPS, or 2 for the
+    // segment's last 64 rows)
+    auto fill = [&](int buf, int jc, int nt) {
       const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
-      for (int f = wave; f < CH; f += kWaves)
+      for (int f = wave; f < nt * KT; f += kWaves)
         __builtin_amdgcn_global_load_lds(
             src + f * 64 + lane,
             (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
     };
+    auto stage_tiles = [&](int jc) { return min(TPS, (nj - jc) >> 5); };
     __syncthreads();
-    if (nj > 0) fill(0, 0);
+    if (nj > 0) fill(0, 0, stage_tiles(0));
     int buf = 0;
     f32x16 accA[IB], accB[IB];
-    float sprev[IB], scur[IB];
+    // fp32 sum of the current 64-row chunk (two tiles) per i-tile: the
+    // retiring tile's terms are added during the next tile's chain; a chunk
+    // goes into fp64 once both of its tiles are in (the plain passes'
+    // grouping, so the rows are bit-identical to theirs)
+    float sc[IB];
 #pragma unroll
-    for (int t = 0; t < IB; ++t) sprev[t] = scur[t] = 0.0f;
-    for (int jc = 0; jc < nj; jc += 64) {
+    for (int t = 0; t < IB; ++t) sc[t] = 0.0f;
+    for (int jc = 0; jc < nj;) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
+      const int nt = stage_tiles(jc);
+      const int jn = jc + 32 * nt;
+      if (jn < nj) fill(buf ^ 1, jn, stage_tiles(jn));
       const bf16x8(*Ab)[64] = As[buf];
-      bf16x8 a[2];
-      a[0] = Ab[0][lane];
-      a[1] = Ab[1][lane];
-      if (jc == 0) {
-        lds_chain_f<KT, IB, SCH, false>(Ab, 0, lane, bq, accA, accB, sprev, a);
-      } else {
-        lds_chain_f<KT, IB, SCH, true>(Ab, 0, lane, bq, accA, accB, sprev, a);
+      // tiles u0 (even: accA) and u0 + 1 (odd: accB) of the stage; each
+      // chain carries the VALU of the tile before it (the other set)
+      auto pair = [&](int u0, bool first) {
+        bf16x8 a[2];
+        a[0] = Ab[u0 * KT][lane];
+        a[1] = Ab[u0 * KT + 1][lane];
+        if (first) {
+          lds_chain_f<KT, IB, SCH, false>(Ab, u0, lane, bq, accA, accB, sc, a);
+        } else {
+          lds_chain_f<KT, IB, SCH, true>(Ab, u0, lane, bq, accA, accB, sc, a);
 #pragma unroll
-        for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
-      }
+          for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sc[t]);
+        }
 #pragma unroll
-      for (int t = 0; t < IB; ++t) scur[t] = 0.0f;
-      a[0] = Ab[KT][lane];
-      a[1] = Ab[KT + 1][lane];
-      lds_chain_f<KT, IB, SCH, true>(Ab, 1, lane, bq, accB, accA, scur, a);
+        for (int t = 0; t < IB; ++t) sc[t] = 0.0f;
+        a[0] = Ab[(u0 + 1) * KT][lane];
+        a[1] = Ab[(u0 + 1) * KT + 1][lane];
+        lds_chain_f<KT, IB, SCH, true>(Ab, u0 + 1, lane, bq, accB, accA, sc, a);
+      };
+      pair(0, jc == 0);
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sprev[t] = scur[t];
+      for (int u0 = 2; u0 < TPS; u0 += 2)
+        if (u0 < nt) pair(u0, false);
       buf ^= 1;
+      jc = jn;
     }
     if (nj > 0) {
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sprev[t] += tile_sum<KL, SCH>(accB[t], accB[t]);
+      for (int t = 0; t < IB; ++t) sc[t] += tile_sum<KL, SCH>(accB[t], accB[t]);
 #pragma unroll
-      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sprev[t]);
+      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sc[t]);
     }
 #pragma unroll
     for (int t = 0; t < IB; ++t) {

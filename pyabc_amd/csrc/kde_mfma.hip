@@ -1102,8 +1102,10 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
 #ifndef ABC_KDE_LDS2G_WAVES
 #define ABC_KDE_LDS2G_WAVES 1
 #endif
-constexpr int lds2g_waves(int KT, int IB) {
-  return ABC_KDE_LDS2G_WAVES != 0 && KT * IB <= 8 ? 4 : 1;
+constexpr int lds2g_waves(int KT, int IB, bool PIPE) {
+  return ABC_KDE_LDS2G_WAVES == 0 ? 1
+         : (PIPE ? KT * IB <= 8 : KT * IB <= 12) ? 4
+         : (!PIPE && KT * IB <= 18) ? 3 : 1;
 }
 
 // 32-row tiles of A per LDS stage of the folded pass (one barrier per
@@ -1115,16 +1117,18 @@ constexpr int lds2g_waves(int KT, int IB) {
 #ifndef ABC_KDE_STAGE_TILES
 #define ABC_KDE_STAGE_TILES 4
 #endif
-constexpr int kLds2gStageTiles = ABC_KDE_STAGE_TILES;
+// (d > 8 keeps 2: a 4-tile stage of 9 fragments per tile is 72 KB of LDS,
+// two blocks per CU)
+constexpr int lds2g_stage_tiles(int KT) { return KT <= 4 ? ABC_KDE_STAGE_TILES : 2; }
 
-template <int KH, int KL, int IB, int SCH>
+template <int KH, int KL, int IB, int SCH, bool PIPE = true>
 __global__ __launch_bounds__(64 * kWaves)
-__attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB))))
+__attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB, PIPE))))
 void kde_mfma_lds2g_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
-  constexpr int TPS = kLds2gStageTiles;  // 32-row tiles per LDS stage
+  constexpr int TPS = lds2g_stage_tiles(KT);  // 32-row tiles per LDS stage
   constexpr int CH = TPS * KT;
   static_assert(kFolded<KL, SCH>, "folded accumulation only");
   static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
@@ -1183,6 +1187,24 @@ void kde_mfma_lds2g_kernel(
       // tiles u0 (even: accA) and u0 + 1 (odd: accB) of the stage; each
       // chain carries the VALU of the tile before it (the other set)
       auto pair = [&](int u0, bool first) {
+        if constexpr (!PIPE) {
+          // no overlap inside the wave: each tile's chain, then its sum
+          // (the same per-lane arithmetic and grouping)
+#pragma unroll
+          for (int t = 0; t < IB; ++t) sc[t] = 0.0f;
+#pragma unroll
+          for (int u = u0; u < u0 + 2; ++u) {
+            bf16x8 a[2];
+            a[0] = Ab[u * KT][lane];
+            a[1] = Ab[u * KT + 1][lane];
+            lds_chain_f<KT, IB, SCH, false>(Ab, u, lane, bq, accA, accA, sc, a);
+#pragma unroll
+            for (int t = 0; t < IB; ++t) sc[t] += tile_sum<KL, SCH>(accA[t], accA[t]);
+          }
+#pragma unroll
+          for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sc[t]);
+          return;
+        }
         bf16x8 a[2];
         a[0] = Ab[u0 * KT][lane];
         a[1] = Ab[u0 * KT + 1][lane];
@@ -1206,7 +1228,7 @@ void kde_mfma_lds2g_kernel(
       buf ^= 1;
       jc = jn;
     }
-    if (nj > 0) {
+    if (PIPE && nj > 0) {
 #pragma unroll
       for (int t = 0; t < IB; ++t) sc[t] += tile_sum<KL, SCH>(accB[t], accB[t]);
 #pragma unroll
@@ -1288,9 +1310,11 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib, bool smajor) {
 // test_kde_mfma_launch_knobs_bit_identical checks that each leaves every row
 // unchanged): ABC_KDE_MFMA_SPLIT (j-segment blocks per row block),
 // ABC_KDE_MFMA_IB (i-tiles per wave), ABC_KDE_MFMA_PIPE (software
-// pipelining of the register kernel), ABC_KDE_MFMA_LDS2 (d > 8 -- 0: the
-// register kernel, 1: LDS-DMA A fragments, 2: the same hand-interleaved;
-// d <= 8 -- 0: the register kernel, 1: the folded LDS-DMA pass),
+// pipelining of the register kernel), ABC_KDE_MFMA_LDS2 (0: the register
+// kernel; folded schemes: 1 or 2 the folded LDS-DMA pass, hand-interleaved,
+// 3 the same without in-wave pipelining (d <= 8 default on large
+// populations); split schemes: 1 LDS-DMA A fragments, 2 the same
+// hand-interleaved),
 // ABC_KDE_MFMA_SMAJOR (1: segment-major block order, one segment per block).
 int env_int(const char* name, int dflt) {
   const char* env = getenv(name);
@@ -1307,7 +1331,14 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if constexpr (D > 8 && Mk<D>::SCH == 2) {
     // the folded f16 scheme: the LDS-DMA folded pass (ABC_KDE_MFMA_LDS2 1
     // or 2), or the register kernel (0); rows bit-identical
-    if (env_int("ABC_KDE_MFMA_LDS2", 2) != 0) {
+    const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
+    if (lds2 == 3) {  // no in-wave pipelining
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
+                         p.spb, p.jseg, partial);
+      return;
+    }
+    if (lds2 != 0) {
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
@@ -1334,6 +1365,12 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if constexpr (D <= 8) {
     // the folded pass with LDS-DMA A fragments and hand-placed VALU
     // (kde_mfma_lds2g_kernel); rows bit-identical
+    if (lds2g == 3) {  // no in-wave pipelining (tuning; rows bit-identical)
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
+                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
+                         p.spb, p.jseg, partial);
+      return;
+    }
     if (lds2g) {
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
@@ -1368,9 +1405,17 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   // N = M = 1e6, d = 8, interleaved A/B in one process (gpurun_out/lds2g2);
   // IB = 3 there ran 136.5 ms, IB = 1 149 ms.  Small populations keep the
   // register kernel (equal at N = 1e5, d = 4).
+  // Round 4: the same pass WITHOUT in-wave pipelining (mode 3: each tile's
+  // chain, then its sums; one accumulator set) at IB = 3 holds four waves
+  // per SIMD in 128 VGPRs and reads each A fragment for three i-tiles:
+  // 115.9-116.1 -> 112.7-112.9 ms at N = M = 1e6, d = 8, and 93.2 -> 91.1 ms
+  // at d = 4, interleaved (gpurun_out/r04ao, r04ap); rows bit-identical.
+  // (At d > 8 the pipelined form stays: 204.8 vs 208.4 ms at d = 20.)  From
+  // 2^16 rows on (config 2, N = 1e5, d = 4: 1.07-1.14 -> 1.04-1.11 ms
+  // against the register kernel, interleaved, gpurun_out/r04aq).
   const int lds2g =
-      D <= 8 ? env_int("ABC_KDE_MFMA_LDS2", npad >= (int64_t{1} << 19) ? 1 : 0) : 0;
-  int ib = lds2g ? IB2 : IBF;
+      D <= 8 ? env_int("ABC_KDE_MFMA_LDS2", npad >= (int64_t{1} << 16) ? 3 : 0) : 0;
+  int ib = lds2g == 1 ? IB2 : IBF;
   const int v = env_int("ABC_KDE_MFMA_IB", ib);
   if (v == IBF || v == IBH || v == IB2) ib = v;
   // segment-major block order on large populations (the A fragments no

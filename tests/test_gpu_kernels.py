@@ -205,14 +205,17 @@ def test_kde_mfma_rows_independent_of_launch(K):
 KNOBS = {
     4: [("ABC_KDE_MFMA_PIPE", "0"), ("ABC_KDE_MFMA_IB", "1"),
         ("ABC_KDE_MFMA_IB", "2"), ("ABC_KDE_MFMA_SPLIT", "4"),
-        ("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_SMAJOR", "1")],
+        ("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_LDS2", "3"),
+        ("ABC_KDE_MFMA_SMAJOR", "1")],
     8: [("ABC_KDE_MFMA_PIPE", "0"), ("ABC_KDE_MFMA_IB", "1"),
         ("ABC_KDE_MFMA_IB", "2"), ("ABC_KDE_MFMA_SPLIT", "1"),
         ("ABC_KDE_MFMA_SPLIT", "8"), ("ABC_KDE_MFMA_LDS2", "1"),
-        ("ABC_KDE_MFMA_LDS2", "0"), ("ABC_KDE_MFMA_SMAJOR", "1")],
+        ("ABC_KDE_MFMA_LDS2", "3"), ("ABC_KDE_MFMA_LDS2", "0"),
+        ("ABC_KDE_MFMA_SMAJOR", "1")],
     20: [("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_LDS2", "0"),
-         ("ABC_KDE_MFMA_IB", "1"), ("ABC_KDE_MFMA_SPLIT", "2"),
-         ("ABC_KDE_MFMA_PIPE", "1"), ("ABC_KDE_MFMA_SMAJOR", "1")],
+         ("ABC_KDE_MFMA_LDS2", "3"), ("ABC_KDE_MFMA_IB", "1"),
+         ("ABC_KDE_MFMA_SPLIT", "2"), ("ABC_KDE_MFMA_PIPE", "1"),
+         ("ABC_KDE_MFMA_SMAJOR", "1")],
 }
 
 

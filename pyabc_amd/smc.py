@@ -9,6 +9,7 @@ and populations stay on the device as columns between generations.
 """
 import copy
 import datetime
+import time
 import logging
 
 import numpy as np
@@ -374,6 +375,7 @@ class ABCSMC:
             max_eval = np.inf if min_acceptance_rate == 0. \
                 else pop_size / min_acceptance_rate
             t_start = datetime.datetime.now()
+            started = time.perf_counter()
             sample = self.sampler.sample_until_n_accepted(
                 pop_size, simulate_one, max_eval)
             sample_s = (datetime.datetime.now() - t_start).total_seconds()
@@ -394,7 +396,7 @@ class ABCSMC:
                         f"{acceptance_rate:.4e}, ESS={ess:.4e}.")
             self.generation_log.append(dict(
                 t=t, eps=current_eps, n_sim=n_sim, ess=ess,
-                sample_seconds=sample_s,
+                sample_seconds=sample_s, started=started,
                 batch=getattr(self.sampler, "fallback_reason", "") is None))
             self._prepare_next_iteration(t + 1, sample, population,
                                          acceptance_rate)

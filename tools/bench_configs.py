@@ -5,8 +5,9 @@
 
 One JSON line per config: per-generation sampling wall time (the metric's
 "accepted particles/s per generation" = N / sample_until_n_accepted wall,
-generations t >= 1), acceptance, epsilon trajectory, total wall time and
-the posterior mean.  Config 3 (the KDE pass at N = 1e6, d = 8) is bench.py.
+generations t >= 1), the whole-generation wall time (start to next start:
+sampling plus the refits between generations), acceptance, epsilon
+trajectory, total wall time and the posterior mean.  Config 3 (the KDE pass at N = 1e6, d = 8) is bench.py.
 """
 import argparse
 import json
@@ -61,11 +62,18 @@ def run(name, abc, x0, names, theta_true=None, db=None, **run_kw):
                  sample_s=float(e["sample_seconds"]), batch=e["batch"],
                  timers={k: round(v * 1e3, 4) for k, v in tm.items()})
             for e, tm in zip(log, tl)]
+    # whole generation: from one generation's start to the next's (sampling,
+    # History append, the transition / distance / epsilon refit between them)
+    for g, e, e1 in zip(gens, log, log[1:]):
+        g["generation_s"] = float(e1["started"] - e["started"])
     n_pop = int(len(w))
     rates = [n_pop / g["sample_s"] for g in gens if g["t"] >= 1]
+    whole = [g["generation_s"] for g in gens if g["t"] >= 1 and "generation_s" in g]
     out = dict(config=name, N=n_pop, generations=len(gens), wall_s=wall,
                accepted_per_s_median_t_ge_1=float(np.median(rates))
                if rates else None,
+               generation_ms_median_t_ge_1=float(np.median(whole)) * 1e3
+               if whole else None,
                all_batch=all(g["batch"] for g in gens), gens=gens,
                posterior_mean=mean.tolist())
     if db is not None:

@@ -29,9 +29,10 @@
 // write one fp64 partial per segment; the finalize kernel sums the nseg
 // partials in fixed order.  A row's result is therefore independent of M
 // and of the launch shape (deterministic, and identical across GPU counts).
-// Rows whose sum falls below 2^-60 (f32) are re-evaluated by an exact
-// two-pass (max, then sum) fixup kernel, so underflow of the fixed global
-// offset never loses a row.
+// Rows whose sum falls below 2^-60 (f32) are re-evaluated by a two-pass
+// (fp64 max, then fp64 sum) fixup kernel, so underflow of the fixed global
+// offset never loses a row; each term 2^(acc - max) is ldexp of v_exp_f32 on
+// the fraction (~1.2e-7 relative per term).
 #include <cstdlib>
 
 #include "common.hpp"
@@ -285,57 +286,110 @@ __global__ __launch_bounds__(256) void kde_finalize_kernel(
   }
 }
 
-// exact two-pass evaluation for rows whose fixed-offset sum underflowed.
-// One block per row (grid-stride over the device-side count): 1024 blocks,
-// so up to 4 rows per CU run at once and a launch with few or no fixup rows
-// costs only the empty blocks' exit.
+// two-pass evaluation (fp64 max, then fp64 sum) for rows whose fixed-offset
+// sum underflowed.  A block takes RB fixup rows at once, so each pass over
+// the population serves RB rows (one row per block re-read P from L2 per
+// row: 37.6 ms per launch on the exact-inference records, 3.2x the MFMA
+// pass).  Grid-stride over the device-side count: 1024 blocks, so a launch
+// with few or no fixup rows costs only the empty blocks' exit.  A row's
+// arithmetic (thread j-stride, fixed reduction order) does not depend on RB
+// or on which rows share its block.
 constexpr int kFixupBlocks = 1024;
+template <int D>
+constexpr int kFixupRows = D <= 4 ? 8 : (D <= 8 ? 4 : (D <= 16 ? 2 : 1));
 template <typename T, int D>
 __global__ __launch_bounds__(256) void kde_fixup_kernel(
     const T* __restrict__ Ynew, const T* __restrict__ P, int64_t npad,
     const double* __restrict__ lw2max, double log_const,
     const int* __restrict__ n_fix, const int* __restrict__ fix_rows,
     double* __restrict__ out_logpd) {
-  __shared__ double red[4];
+  constexpr int RB = kFixupRows<D>;
+  __shared__ double red[RB][4];
   const int count = *n_fix;
+  const int ngroups = (count + RB - 1) / RB;
   const double off = kLn2 * (*lw2max) + log_const;
-  for (int f = blockIdx.x; f < count; f += gridDim.x) {
-    const int64_t i = fix_rows[f];
-    T yi[D];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    T yi[RB][D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) yi[k] = Ynew[i * D + k];
-    double m = -INFINITY;
+    for (int r = 0; r < RB; ++r) {
+      const int f = g * RB + r;
+      const int64_t src = fix_rows[f < count ? f : g * RB];
+#pragma unroll
+      for (int k = 0; k < D; ++k) yi[r][k] = Ynew[src * D + k];
+    }
+    double m[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) m[r] = -INFINITY;
     for (int64_t j = threadIdx.x; j < npad; j += 256) {
       const T* pj = P + j * (D + 1);
-      T acc = pj[D];
+      T pv[D + 1];
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        const T df = yi[k] - pj[k];
-        acc = fma(-df, df, acc);
-      }
-      m = fmax(m, static_cast<double>(acc));
-    }
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-    __syncthreads();
-    double sum = 0.0;
-    if (m > -1.0e29) {
-      for (int64_t j = threadIdx.x; j < npad; j += 256) {
-        const T* pj = P + j * (D + 1);
-        T acc = pj[D];
+      for (int k = 0; k <= D; ++k) pv[k] = pj[k];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        T acc = pv[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          const T df = yi[k] - pj[k];
+          const T df = yi[r][k] - pv[k];
           acc = fma(-df, df, acc);
         }
-        sum += exp2(static_cast<double>(acc) - m);
+        m[r] = fmax(m[r], static_cast<double>(acc));
       }
     }
-    sum = block_sum<double, 256>(sum, red);
-    if (threadIdx.x == 0)
-      out_logpd[i] = (m > -1.0e29) ? kLn2 * (m + log2(sum)) + off : -INFINITY;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const double v = wave_max(m[r]);
+      if (lane == 0) red[r][wid] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+      m[r] = fmax(fmax(red[r][0], red[r][1]), fmax(red[r][2], red[r][3]));
+    __syncthreads();
+    double sum[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) sum[r] = 0.0;
+    for (int64_t j = threadIdx.x; j < npad; j += 256) {
+      const T* pj = P + j * (D + 1);
+      T pv[D + 1];
+#pragma unroll
+      for (int k = 0; k <= D; ++k) pv[k] = pj[k];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        T acc = pv[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const T df = yi[r][k] - pv[k];
+          acc = fma(-df, df, acc);
+        }
+        // 2^x for x = acc - m <= 0 (exact in fp64): the integer part by
+        // ldexp, the fraction in [0, 1) on v_exp_f32 (~1.2e-7 relative per
+        // term; fp64 exp2 issued 3x the instructions)
+        const double x = static_cast<double>(acc) - m[r];
+        const double fl = floor(fmax(x, -2000.0));
+        const float fr = static_cast<float>(x - fl);
+        sum[r] += ldexp(static_cast<double>(__builtin_amdgcn_exp2f(fr)),
+                        static_cast<int>(fl));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const double v = wave_sum(sum[r]);
+      if (lane == 0) red[r][wid] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const int f = g * RB + r;
+        if (f < count) {
+          const double S = ((red[r][0] + red[r][1]) + red[r][2]) + red[r][3];
+          out_logpd[fix_rows[f]] =
+              (m[r] > -1.0e29) ? kLn2 * (m[r] + log2(S)) + off : -INFINITY;
+        }
+      }
+    }
     __syncthreads();
   }
 }

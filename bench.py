@@ -67,20 +67,57 @@ def kde_traffic():
 
 
 def kde_pmc(d):
-    """Per-tile instruction counts of the MFMA KDE kernel from the committed
-    rocprofv3 PMC passes (tools/kde_pmc.py), if they were taken at this d."""
-    for tag in ("r03", "r02"):
-        path = os.path.join(ROOT, "profiles", f"{tag}_kde_pmc.json")
-        if os.path.exists(path):
+    """Per-tile instruction counts of the MFMA KDE kernel from the NEWEST
+    committed rocprofv3 PMC file taken at this d (tools/kde_pmc.py writes
+    ``profiles/rNN_kde_pmc.json`` with a ``d`` key; the d > 8 passes are
+    ``profiles/rNN_kde_dDD_pmc.json``).  Files are ranked by their round
+    tag, never by a fixed list, so a new round's profile supersedes the
+    old one as soon as it is committed."""
+    import glob
+    import re
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*_kde*_pmc.json")):
+        m = re.match(r"r(\d+)_kde(?:_d(\d+))?_pmc\.json$",
+                     os.path.basename(path))
+        if not m:
+            continue
+        try:
             with open(path) as f:
                 t = json.load(f)
-            if t.get("d") == d:
-                return t, path
-    return None, None
+        except (OSError, ValueError):
+            continue
+        fd = t.get("d", int(m.group(2)) if m.group(2) else None)
+        pt = t.get("per_tile", {})
+        if fd != d or "SQ_INSTS_VALU" not in pt or "SQ_INSTS_MFMA" not in pt:
+            continue
+        key = int(m.group(1))
+        if best is None or key > best[0]:
+            best = (key, t, path)
+    return (best[1], best[2]) if best else (None, None)
 
 
-PROBE_MIX = {8: 3, 20: 4}   # tools/probes/issue_probe.hip variants
+# tools/probes/issue_probe.hip variants holding the kernel's PMC-counted
+# per-tile mix (MFMA, v_exp_f32, other VALU); a non-integer VALU count is
+# the mean of two variants
+PROBE_MIX = {8: (3, 12),   # 4 MFMA, 16 exp, 21 / 22 other (PMC 21.5)
+             20: (13,)}    # 9 MFMA, 16 exp, 28 other (PMC 28.2)
 PROBE_WAVES = {8: 4, 20: 2}  # the KDE kernel's occupancy (waves per SIMD)
+
+# MI355X_MICROARCH.md per-instruction constants (cycles per wave64
+# instruction on one SIMD): the guide's hardware floor prices plain VALU at
+# its SIMD-32 throughput (2), the single-wave static pricing at the issue
+# cost one wave's stream sees (4); transcendentals 8, an MFMA holds vector
+# issue 8 of its 32 matrix-pipe cycles
+GUIDE_CYC = {"valu": 2.0, "trans": 8.0, "mfma_issue": 8.0, "mfma_pipe": 32.0}
+STATIC_CYC = {"valu": 4.0, "trans": 8.0, "mfma_issue": 8.0, "mfma_pipe": 32.0}
+
+
+def mix_cycles(V, T, F, c):
+    """Cycles per 32x32 tile per SIMD of the mix (V VALU incl. T
+    transcendentals, F MFMAs) at the cost table c: the larger of the SIMD's
+    vector issue and the matrix pipe."""
+    return max(c["valu"] * (V - T) + c["trans"] * T + c["mfma_issue"] * F,
+               c["mfma_pipe"] * F)
 
 
 def issue_probe(d, waves_per_simd=None):
@@ -92,15 +129,15 @@ def issue_probe(d, waves_per_simd=None):
         waves_per_simd = PROBE_WAVES.get(d, 2)
     import ctypes
     path = os.path.join(ROOT, "tools", "probes", "libabc_probe.so")
-    v = PROBE_MIX.get(d)
-    if v is None or not os.path.exists(path):
+    vs = PROBE_MIX.get(d)
+    if vs is None or not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
     lib.abc_probe_kde_mix.restype = ctypes.c_double
     lib.abc_probe_kde_mix.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     torch.cuda.synchronize()
-    ns = lib.abc_probe_kde_mix(v, waves_per_simd, 100000)
-    return ns if ns > 0 else None
+    ns = [lib.abc_probe_kde_mix(v, waves_per_simd, 100000) for v in vs]
+    return sum(ns) / len(ns) if min(ns) > 0 else None
 
 
 def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
@@ -122,7 +159,9 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     frac = t_ceiling / t_launch.  achieved / peak are the same ratio in
     SURVEY 8(d)'s algorithmic unit (3d+4 FLOP per pair).  The static
     pricing of the same mix at the guide's single-wave issue costs and
-    2.4 GHz is kept beside it (``static_issue``), and the FP32 vector-peak
+    2.4 GHz is kept beside it (``static_issue``), the same mix priced at
+    the guide's hardware floor (plain VALU 2 cycles at SIMD-32 throughput,
+    ``guide_floor`` / ``frac_guide_floor``), and the FP32 vector-peak
     figure of a VALU-only pass as ``valu_equiv`` (it exceeds 1: the MFMA
     does the d-dimensional part)."""
     pmc, pmc_path = kde_pmc(d)
@@ -141,8 +180,11 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         # folded accumulation (D <= 24): no hi + lo add (kde_mfma.hip)
         V, T = (32.0 if D <= 24 else 48.0), 16.0
         src = "static per-tile instruction count (no PMC file for this d)"
-    cyc = max(4 * (V - T) + 8 * T + 8 * F, 32 * F)
+    cyc = mix_cycles(V, T, F, STATIC_CYC)
     t_static = tiles_per_launch * cyc / (1024 * CLOCK_HZ)
+    # the guide's hardware floor: plain VALU at its SIMD-32 throughput
+    cyc_floor = mix_cycles(V, T, F, GUIDE_CYC)
+    t_floor = tiles_per_launch * cyc_floor / (1024 * CLOCK_HZ)
     ns_probe = issue_probe(d)
     if ns_probe is not None:
         t_ceil = tiles_per_launch * ns_probe * 1e-9 / 1024
@@ -170,11 +212,15 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "unit": "TFLOP/s",
         "frac": frac,
         "frac_static_issue": t_static / avg_launch_s,
+        "frac_guide_floor": t_floor / avg_launch_s,
         "ceiling_note": "frac divides by a SELF-MEASURED ceiling (this "
                         "repo's tools/probes/issue_probe.hip run live on "
                         "this GPU); frac_static_issue prices the same "
-                        "PMC-counted mix at MI355X_MICROARCH.md's issue "
-                        "costs at 2.4 GHz",
+                        "PMC-counted mix at one wave's issue costs (VALU 4, "
+                        "TRANS 8, MFMA 8 of 32 cycles), frac_guide_floor at "
+                        "MI355X_MICROARCH.md's hardware floor (VALU 2 at "
+                        "SIMD-32 throughput, TRANS 8, MFMA 8 issue / 32 "
+                        "pipe), both at 2.4 GHz on 1024 SIMDs",
         "traffic": traffic,
         "traffic_source": traffic_src,
         "peak_basis": basis,
@@ -183,6 +229,12 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
         "static_issue": {"cycles_per_tile": cyc,
                          "ceiling_ms": t_static * 1e3,
                          "frac": t_static / avg_launch_s},
+        "guide_floor": {"cycles_per_tile": cyc_floor,
+                        "ceiling_ms": t_floor * 1e3,
+                        "frac": t_floor / avg_launch_s,
+                        "cycles": GUIDE_CYC},
+        "mix_per_tile": {"mfma": F, "trans": T, "other_valu": V - T,
+                         "source": src},
         "flops_per_pair": fpp,
         "avg_launch_ms": avg_launch_s * 1e3,
         "pairs_per_launch": pairs_per_launch,

@@ -31,6 +31,12 @@ extern "C" {
 
 const char* abc_last_error(void);
 int abc_version(void);
+/* Re-read the launch-shape tuning knobs (ABC_KDE_MFMA_SPLIT / _IB / _PIPE /
+ * _LDS2 / _SMAJOR, ABC_KDE_TIER, ABC_LZ_IB / _TPB) from the environment.
+ * The library reads them once, at the first launch that consults them; the
+ * knobs only change how work maps to the chip, never a result bit
+ * (tests/test_gpu_kernels.py knob tests).  No reference counterpart. */
+void abc_tuning_reload(void);
 
 /* ---------------- (a1) MultivariateNormalTransition.fit ------------------
  * Replaces smart_cov = np.cov(X, aweights=w)        transition/util.py:4-15

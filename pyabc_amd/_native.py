@@ -33,6 +33,7 @@ c_ptr = ctypes.c_void_p
 _SIGS = {
     "abc_last_error": (ctypes.c_char_p, []),
     "abc_version": (c_int, []),
+    "abc_tuning_reload": (None, []),
     # (a1)
     "abc_moments_workspace_bytes": (c_size, [c_int]),
     "abc_weighted_moments_f64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,

@@ -26,6 +26,24 @@ enum Status : int {
 
 void set_error(const char* fmt, ...);
 
+// Launch-shape tuning knobs (environment variables, tools/ sweeps and the
+// knob tests only; none changes a result bit).  The table is read from the
+// environment ONCE per process (capi.hip) and again only by
+// abc_tuning_reload(), so no launch path calls getenv.
+enum Knob : int {
+  kKnobKdeMfmaSplit = 0,  // ABC_KDE_MFMA_SPLIT
+  kKnobKdeMfmaIb,         // ABC_KDE_MFMA_IB
+  kKnobKdeMfmaPipe,       // ABC_KDE_MFMA_PIPE
+  kKnobKdeMfmaLds2,       // ABC_KDE_MFMA_LDS2
+  kKnobKdeMfmaSmajor,     // ABC_KDE_MFMA_SMAJOR
+  kKnobKdeTier,           // ABC_KDE_TIER
+  kKnobLzIb,              // ABC_LZ_IB
+  kKnobLzTpb,             // ABC_LZ_TPB
+  kKnobCount
+};
+// the knob's integer value, or dflt when the variable is unset
+int tuning_knob(Knob k, int dflt);
+
 #define ABC_REQUIRE(cond, ...)              \
   do {                                      \
     if (!(cond)) {                          \

@@ -31,8 +31,9 @@
 // and of the launch shape (deterministic, and identical across GPU counts).
 // Rows whose sum falls below 2^-60 (f32) are re-evaluated by a two-pass
 // (fp64 max, then fp64 sum) fixup kernel, so underflow of the fixed global
-// offset never loses a row; each term 2^(acc - max) is ldexp of v_exp_f32 on
-// the fraction (~1.2e-7 relative per term).
+// offset never loses a row; in the fp32 and MFMA passes each term
+// 2^(acc - max) is ldexp of v_exp_f32 on the fraction (~1.2e-7 relative per
+// term), in the fp64 pass fp64 exp2 (1e-12).
 #include <cstdlib>
 
 #include "common.hpp"
@@ -294,10 +295,13 @@ __global__ __launch_bounds__(256) void kde_finalize_kernel(
 // with few or no fixup rows costs only the empty blocks' exit.  A row's
 // arithmetic (thread j-stride, fixed reduction order) does not depend on RB
 // or on which rows share its block.
+// F32EXP: each term 2^(acc - max) as ldexp of v_exp_f32 on the fraction
+// (~1.2e-7 relative per term) -- the fp32 pass and the MFMA pass, whose
+// contract is 1e-5; otherwise fp64 exp2 (the fp64 pass's 1e-12 contract).
 constexpr int kFixupBlocks = 1024;
 template <int D>
 constexpr int kFixupRows = D <= 4 ? 8 : (D <= 8 ? 4 : (D <= 16 ? 2 : 1));
-template <typename T, int D>
+template <typename T, int D, bool F32EXP>
 __global__ __launch_bounds__(256) void kde_fixup_kernel(
     const T* __restrict__ Ynew, const T* __restrict__ P, int64_t npad,
     const double* __restrict__ lw2max, double log_const,
@@ -363,14 +367,18 @@ __global__ __launch_bounds__(256) void kde_fixup_kernel(
           const T df = yi[r][k] - pv[k];
           acc = fma(-df, df, acc);
         }
-        // 2^x for x = acc - m <= 0 (exact in fp64): the integer part by
-        // ldexp, the fraction in [0, 1) on v_exp_f32 (~1.2e-7 relative per
-        // term; fp64 exp2 issued 3x the instructions)
         const double x = static_cast<double>(acc) - m[r];
-        const double fl = floor(fmax(x, -2000.0));
-        const float fr = static_cast<float>(x - fl);
-        sum[r] += ldexp(static_cast<double>(__builtin_amdgcn_exp2f(fr)),
-                        static_cast<int>(fl));
+        if constexpr (F32EXP) {
+          // 2^x for x = acc - m <= 0 (exact in fp64): the integer part by
+          // ldexp, the fraction in [0, 1) on v_exp_f32 (~1.2e-7 relative
+          // per term; fp64 exp2 issued 3x the instructions)
+          const double fl = floor(fmax(x, -2000.0));
+          const float fr = static_cast<float>(x - fl);
+          sum[r] += ldexp(static_cast<double>(__builtin_amdgcn_exp2f(fr)),
+                          static_cast<int>(fl));
+        } else {
+          sum[r] += exp2(x);
+        }
       }
     }
 #pragma unroll
@@ -460,8 +468,8 @@ static Plan make_plan(int64_t M, int64_t npad) {
          ceil_div(M, 256 * (R >> p.tier)) * p.nseg < target_blocks)
     ++p.tier;
   // tuning override (tools/bench_kde.py sweeps): ABC_KDE_TIER=0|1|2
-  if (const char* env = getenv("ABC_KDE_TIER")) {
-    const int t = atoi(env);
+  {
+    const int t = tuning_knob(kKnobKdeTier, -1);
     if (t >= 0 && t <= 2 && (R >> t) >= min_rows) p.tier = t;
   }
   p.rows_per_thread = R >> p.tier;
@@ -542,7 +550,8 @@ static int logpdf_impl(const T* Ynew, int64_t M, const T* P, int64_t npad,
                      log_const, out_logpd, n_fix, fix_rows,
                      KdeCfg<T>::underflow);
   ABC_LAUNCH_CHECK("kde_finalize_kernel");
-  hipLaunchKernelGGL((kde_fixup_kernel<T, D>), dim3(kFixupBlocks), dim3(256), 0, stream,
+  hipLaunchKernelGGL((kde_fixup_kernel<T, D, sizeof(T) == 4>), dim3(kFixupBlocks),
+                     dim3(256), 0, stream,
                      Ynew, P, npad, lw2max, log_const, n_fix, fix_rows,
                      out_logpd);
   ABC_LAUNCH_CHECK("kde_fixup_kernel");
@@ -762,8 +771,10 @@ int logsum_impl(const T* Ynew, const T* Yprev, const T* logw, int64_t M,
 }
 
 // shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum
-// and underflow detection of the fp32-exponent pass, then the exact fixup in
-// fp64 on fp64 rows.  An fp32 copy of a far row (|y| ~ 30 in log2 units)
+// and underflow detection of the fp32-exponent pass, then the two-pass fixup
+// in fp64 on fp64 rows (exponents exact in fp64, each term's 2^x from
+// v_exp_f32 on the fraction: ~1.2e-7 relative, inside the pass's 1e-5
+// contract; the fp64 pass keeps fp64 exp2).  An fp32 copy of a far row (|y| ~ 30 in log2 units)
 // carries ~2e-6 absolute error per coordinate, i.e. up to 5e-5 relative on
 // the density through |y_i - y_j|^2: the fixup rows are exactly the far ones,
 // so they are evaluated from the fp64 whitened rows
@@ -782,7 +793,7 @@ int kde_finish_mfma(const double* partial, int64_t M, int nseg,
   switch (padded_dim(d)) {
 #define CASE(DD)                                                              \
   case DD:                                                                    \
-    hipLaunchKernelGGL((kde_fixup_kernel<double, DD>), dim3(kFixupBlocks), dim3(256), 0, \
+    hipLaunchKernelGGL((kde_fixup_kernel<double, DD, true>), dim3(kFixupBlocks), dim3(256), 0, \
                        stream, Ynew, P, npad, lw2max, log_const, n_fix,       \
                        fix_rows, out_logpd);                                  \
     break;

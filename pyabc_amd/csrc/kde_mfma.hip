@@ -1297,8 +1297,8 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib, bool smajor) {
     split = p.nseg;
   else
     while (split < p.nseg && p.row_blocks * split < target_blocks) split *= 2;
-  if (const char* env = getenv("ABC_KDE_MFMA_SPLIT")) {  // tuning override
-    const int v = atoi(env);
+  {  // tuning override
+    const int v = tuning_knob(kKnobKdeMfmaSplit, 0);
     if (v >= 1 && v <= p.nseg && (p.nseg % v) == 0) split = v;
   }
   p.split = split;
@@ -1316,10 +1316,7 @@ MPlan make_mplan(int64_t M, int64_t npad, int ib, bool smajor) {
 // populations); split schemes: 1 LDS-DMA A fragments, 2 the same
 // hand-interleaved),
 // ABC_KDE_MFMA_SMAJOR (1: segment-major block order, one segment per block).
-int env_int(const char* name, int dflt) {
-  const char* env = getenv(name);
-  return env ? atoi(env) : dflt;
-}
+// Read once per process (common.hpp tuning_knob; abc_tuning_reload).
 
 template <int D, int IB>
 void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
@@ -1331,7 +1328,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   if constexpr (D > 8 && Mk<D>::SCH == 2) {
     // the folded f16 scheme: the LDS-DMA folded pass (ABC_KDE_MFMA_LDS2 1
     // or 2), or the register kernel (0); rows bit-identical
-    const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
+    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
     if (lds2 == 3) {  // no in-wave pipelining
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
@@ -1348,7 +1345,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // 2: hand-interleaved split pass; 1: LDS-DMA A fragments, compiler
     // schedule (d = 20: 21.5 -> 20.4 ms at N = M = 262144 against the
     // register kernel); 0: the register kernel.  Rows bit-identical.
-    const int lds2 = env_int("ABC_KDE_MFMA_LDS2", 2);
+    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
     if (lds2 == 2) {
       hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
@@ -1380,7 +1377,7 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   }
   // software pipelining pays at D <= 8 (VALU-bound); at larger D the MFMA
   // chain dominates and the lower register count wins (bench_kde sweep)
-  if (env_int("ABC_KDE_MFMA_PIPE", D <= 8) != 0)
+  if (tuning_knob(kKnobKdeMfmaPipe, D <= 8) != 0)
     hipLaunchKernelGGL((kde_mfma_kernel<Mk<D>::KH, Mk<D>::KL, IB, true, Mk<D>::SCH>),
                        dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                        p.spb, p.jseg, partial);
@@ -1414,14 +1411,14 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   // 2^16 rows on (config 2, N = 1e5, d = 4: 1.07-1.14 -> 1.04-1.11 ms
   // against the register kernel, interleaved, gpurun_out/r04aq).
   const int lds2g =
-      D <= 8 ? env_int("ABC_KDE_MFMA_LDS2", npad >= (int64_t{1} << 16) ? 3 : 0) : 0;
+      D <= 8 ? tuning_knob(kKnobKdeMfmaLds2, npad >= (int64_t{1} << 16) ? 3 : 0) : 0;
   int ib = lds2g == 1 ? IB2 : IBF;
-  const int v = env_int("ABC_KDE_MFMA_IB", ib);
+  const int v = tuning_knob(kKnobKdeMfmaIb, ib);
   if (v == IBF || v == IBH || v == IB2) ib = v;
   // segment-major block order on large populations (the A fragments no
   // longer fit the L2s; ABC_KDE_MFMA_SMAJOR overrides, rows bit-identical)
   const bool smajor =
-      env_int("ABC_KDE_MFMA_SMAJOR", npad >= (int64_t{1} << 18) ? 1 : 0) != 0;
+      tuning_knob(kKnobKdeMfmaSmajor, npad >= (int64_t{1} << 18) ? 1 : 0) != 0;
   const MPlan p = make_mplan<D>(M, npad, ib, smajor);
   const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
                       static_cast<size_t>(M) * 4;

@@ -629,12 +629,12 @@ int lz_run(const double* pts, int64_t M, const double* X, const double* w,
   // point tiles per wave and particle tiles per LDS buffer: defaults, or
   // the tuning knobs (rows bit-identical)
   int ib = Lz<D>::IB, tpb = Lz<D>::TPB;
-  if (const char* e = getenv("ABC_LZ_IB")) {
-    const int v = atoi(e);
+  {
+    const int v = tuning_knob(kKnobLzIb, ib);
     if (v == 1 || v == 2 || v == 4) ib = v;
   }
-  if (const char* e = getenv("ABC_LZ_TPB")) {
-    const int v = atoi(e);
+  {
+    const int v = tuning_knob(kKnobLzTpb, tpb);
     if (v == 2 || v == 4 || v == 8) tpb = v;
   }
   const unsigned grid =

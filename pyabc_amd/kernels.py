@@ -200,6 +200,13 @@ def row_pad():
     return nat.lib().abc_kde_row_pad()
 
 
+def reload_tuning():
+    """Re-read the launch-shape tuning knobs (ABC_KDE_MFMA_*, ABC_KDE_TIER,
+    ABC_LZ_*) from os.environ; the library reads them once per process
+    (abc_tuning_reload).  They never change a result bit."""
+    nat.lib().abc_tuning_reload()
+
+
 def psd_whitening(cov):
     """scipy _PSD semantics on the host (d x d): U, rank, log_pdet."""
     cov = np.asarray(cov, dtype=np.float64)
@@ -303,12 +310,12 @@ class PackedPopulation:
         return self.logpdf_whitened(self.whiten(theta))
 
     def fixup_rows(self):
-        """Rows the last fp32 / MFMA pass of this population handed to the
-        exact fp64 fixup (sum below the pass's threshold, or beyond the
-        grid); synchronises with the stream.  Valid until the next KDE call
-        reuses the workspace."""
+        """Rows the last pass of this population handed to the two-pass
+        fixup (sum below the pass's threshold, or beyond the grid);
+        synchronises with the stream.  Valid until the next KDE call reuses
+        the workspace."""
         ws, off = getattr(self, "_fix_at", (None, 0))
-        if ws is None or self.precision == "f64":
+        if ws is None:
             return 0
         return int(ws[off:off + 4].view(torch.int32).item())
 

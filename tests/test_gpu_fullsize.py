@@ -103,8 +103,10 @@ def _constructed_rows(fit, rng):
 def _variant_logpdf(packed, theta, env):
     """The same packed population evaluated under a launch / accumulation
     override (kde_mfma.hip launch_mfma)."""
+    from pyabc_amd import kernels as K
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
+    K.reload_tuning()
     try:
         return packed.logpdf(theta).cpu().numpy()
     finally:
@@ -113,6 +115,7 @@ def _variant_logpdf(packed, theta, env):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+        K.reload_tuning()
 
 
 def _check(d, N, gens, n_random, n_tail, n_edge, tag, variants=None,

@@ -64,25 +64,34 @@ def test_kde_density_vs_reference(K, name, precision, rtol):
         np.testing.assert_allclose(host(wt), g["weight_norm"], rtol=rtol)
 
 
-@pytest.mark.parametrize("precision", ["mfma", "f32"])
+@pytest.mark.parametrize("precision", ["mfma", "f32", "f64"])
 def test_kde_underflow_rows_fixup(K, precision):
     """Rows far from every previous particle underflow the fixed offset;
-    the fixup pass must still return the exact log density."""
+    the fixup pass must still return the exact log density.  f64: rows
+    whose density lies below 1e-280 (every fp64 term underflows) keep the
+    fp64 pass's 1e-12 contract through the fixup (fp64 exp2 there)."""
     rng = np.random.default_rng(7)
     X = rng.normal(size=(3000, 4))
     w = rng.uniform(0.5, 1.5, 3000)
     w /= w.sum()
     cov = ref.mvn_fit_cov(X, w)
-    theta = np.concatenate([X[:50] + 0.01, X[:20] + 6.0])   # far rows
+    far = 40.0 if precision == "f64" else 6.0
+    theta = np.concatenate([X[:50] + 0.01, X[:20] + far])   # far rows
     pp = _packed(K, X, w, cov, precision)
     lp = host(pp.logpdf(dev(theta)))
-    if precision != "f64":
-        # the 20 far rows (and no near row) went through the exact fixup
-        assert pp.fixup_rows() == 20
+    # the 20 far rows (and no near row) went through the exact fixup
+    assert pp.fixup_rows() == 20
     U, rank, log_pdet = ref.psd_whitening(cov)
     ls = ref.kde_logsum(theta @ U, X @ U, np.log(w))
     expect = ls - 0.5 * (rank * ref.LOG_2PI + log_pdet)
-    np.testing.assert_allclose(lp, expect, rtol=2e-6, atol=1e-5)
+    if precision == "f64":
+        assert np.all(expect[50:] < math.log(1e-280))
+        # density relative error = |log difference|; the far rows' exponents
+        # are ~3e3, whose fp64 evaluation itself carries ~1e-12 absolute
+        np.testing.assert_allclose(lp[:50], expect[:50], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(lp[50:], expect[50:], rtol=0, atol=1e-10)
+    else:
+        np.testing.assert_allclose(lp, expect, rtol=2e-6, atol=1e-5)
 
 
 def test_kde_large_random_vs_oracle(K):
@@ -238,8 +247,10 @@ def test_kde_mfma_launch_knobs_bit_identical(K, d, monkeypatch):
     assert np.max(np.abs(np.exp(base[:64]) / want - 1)) < 1e-5
     for key, val in KNOBS[d]:
         monkeypatch.setenv(key, val)
+        K.reload_tuning()
         got = host(pp.logpdf(dev(theta)))
         monkeypatch.delenv(key)
+        K.reload_tuning()
         np.testing.assert_array_equal(got, base, err_msg=f"{key}={val}")
 
 
@@ -1136,9 +1147,11 @@ def test_local_mfma_launch_knobs_bit_identical(K, d, monkeypatch):
                 {"ABC_LZ_TPB": "8"}, {"ABC_LZ_IB": "2", "ABC_LZ_TPB": "8"}):
         for key, val in env.items():
             monkeypatch.setenv(key, val)
+        K.reload_tuning()
         got = host(K.local_logpdf(dev(pts), dev(X), dev(w), invs, dets, "mfma"))
         for key in env:
             monkeypatch.delenv(key)
+        K.reload_tuning()
         np.testing.assert_array_equal(got, base, err_msg=str(env))
 
 

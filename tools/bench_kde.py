@@ -11,6 +11,7 @@ from pyabc_amd import kernels as K  # noqa: E402
 
 
 def run(N, M, d, prec="f32", reps=3):
+    K.reload_tuning()   # the callers below set the knobs in os.environ
     g = torch.Generator(device="cuda").manual_seed(0)
     X = torch.randn((N, d), dtype=torch.float64, device="cuda", generator=g)
     w = torch.rand(N, dtype=torch.float64, device="cuda", generator=g) + 0.5

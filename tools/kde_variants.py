@@ -47,6 +47,7 @@ def set_env(env):
     for k in KEYS:
         os.environ.pop(k, None)
     os.environ.update(env)
+    K.reload_tuning()
 
 
 def main():

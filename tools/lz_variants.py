@@ -38,6 +38,7 @@ def main():
         for k in KEYS:
             os.environ.pop(k, None)
         os.environ.update(env)
+        K.reload_tuning()
         out = K.local_logpdf(pts, X, w, invs, dets, precision="mfma")
         if base is None:
             base = out.clone()

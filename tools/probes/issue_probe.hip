@@ -18,9 +18,14 @@
 //      (the bf16 piece scheme of rounds 1-3)
 //   2: d = 20, f16 pieces, split     --  9 MFMA, 16 exp, 40 other VALU
 //      (the f16 and bf16 32x32x16 MFMAs issue alike)
-//   3: d <= 8, f16 pieces, folded (round 4 default) -- 4 MFMA, 16 exp, 19
-//      (PMC, profiles/r04_kde_pmc.json: 39.3 VALU incl. the 4 MFMAs)
+//   3: d <= 8, f16 pieces, folded (round 4 default) -- 4 MFMA, 16 exp, 21
+//      (19 in round 4; PMC, profiles/r04_kde_pmc.json: 21.5 other VALU)
 //   4: d = 20, f16 pieces, folded (round 4 default) -- 9 MFMA, 16 exp, 19
+//   12: mix 3 with 22 other VALU: bench.py averages 3 (21 since round 5)
+//       and 12 for the PMC's 21.5 (profiles/r04_kde_pmc.json: 37.5 VALU
+//       incl. 16 TRANS)
+//   13: d = 20, f16 folded, the PMC's mix -- 9 MFMA, 16 exp, 28 other VALU
+//       (profiles/r04_kde_d20_pmc.json: 44.2 VALU incl. 16 TRANS)
 //   5-7: mix 3 plus the headline kernel's memory path (mix_mem_kernel):
 //      5 two ds_read_b128 per step, 6 + a block barrier every 2 steps,
 //      7 + the LDS-DMA refill of the other buffer before each barrier;
@@ -212,7 +217,7 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
     case 1: ns = time_mix<11, 16, 40>(waves_per_simd, iters, cus, out); break;
     case 2: ns = time_mix<9, 16, 40>(waves_per_simd, iters, cus, out); break;
-    case 3: ns = time_mix<4, 16, 19>(waves_per_simd, iters, cus, out); break;
+    case 3: ns = time_mix<4, 16, 21>(waves_per_simd, iters, cus, out); break;
     case 4: ns = time_mix<9, 16, 19>(waves_per_simd, iters, cus, out); break;
     case 5: ns = time_mem_mix<4, 16, 19, 2, 0, 0>(waves_per_simd, iters, cus, out, src); break;
     case 6: ns = time_mem_mix<4, 16, 19, 2, 2, 0>(waves_per_simd, iters, cus, out, src); break;
@@ -221,6 +226,8 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 9: ns = time_mem_mix<4, 16, 19, 2, 4, 1>(waves_per_simd, iters, cus, out, src); break;
     case 10: ns = time_mem_mix<4, 16, 19, 2, 8, 0>(waves_per_simd, iters, cus, out, src); break;
     case 11: ns = time_mem_mix<4, 16, 19, 2, 8, 1>(waves_per_simd, iters, cus, out, src); break;
+    case 12: ns = time_mix<4, 16, 22>(waves_per_simd, iters, cus, out); break;
+    case 13: ns = time_mix<9, 16, 28>(waves_per_simd, iters, cus, out); break;
     default: break;
   }
   (void)hipFree(src);

@@ -195,6 +195,17 @@ int abc_kde_logsum_f64(const double* Ynew, const double* Yprev,
  * fp64 from Ynew and P; their count is the int32 at byte
  * abc_kde_segments(npad) * M * 8 of the workspace after the call.
  * Workspace: abc_kde_workspace_bytes.
+ *
+ * The _rows forms (round 5) evaluate each row relative to its own offset
+ * row_off[i] (log2 units, <= 0; NULL = 0 for every row):
+ * abc_kde_pack_new_mfma_rows writes row_off from the rows' parents
+ * (parent[i] = the index into the previous population the proposal was
+ * resampled from, smc.py:602-645; NULL: no parents, row_off = 0) using the
+ * fp64 population P; abc_kde_logpdf_mfma_rows (which also takes the grid
+ * gscale) re-evaluates rows whose sum leaves the folded scheme's routing
+ * range on the matrix cores with their own offsets
+ * and only the rest exactly in fp64; the int32 after the fixup count is the
+ * number of rows re-evaluated.  Same result contract (1e-5 relative).
  *                                          multivariatenormal.py:102-125 */
 size_t abc_kde_mfma_prev_bytes(int64_t npad, int d);
 int64_t abc_kde_mfma_new_rows(int64_t M, int d);
@@ -212,6 +223,18 @@ int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
                         const double* lw2max, double log_const,
                         double* out_logpd, void* ws, size_t ws_bytes,
                         hipStream_t stream);
+int abc_kde_pack_new_mfma_rows(const double* theta, int64_t M, int d,
+                               const double* mu, const double* Us,
+                               const double* gscale, const double* P,
+                               int64_t npad, const int64_t* parent,
+                               double* Ynew, void* Bfr, double* row_off,
+                               hipStream_t stream);
+int abc_kde_logpdf_mfma_rows(const void* Bfr, const double* Ynew,
+                             const double* row_off, int64_t M, const void* Afr,
+                             const double* P, int64_t npad, int d,
+                             const double* lw2max, const double* gscale,
+                             double log_const, double* out_logpd, void* ws,
+                             size_t ws_bytes, hipStream_t stream);
 /* w = prior_pd / exp(logpd)                          smc.py:776-792
  * prior may be NULL (then prior_const is used for every row) */
 int abc_importance_weights_f64(const double* logpd, const double* prior,
@@ -243,9 +266,11 @@ int abc_pnorm_distance_f64(const double* stats_T, int64_t ld,
  * as gathered by AdaptivePNormDistance._update      distance/distance.py:253-297 */
 size_t abc_column_select_workspace_bytes(int S);
 /* Median (and MAD when mad_out != NULL) of every column of data_T [S][ld],
- * np.median semantics, bit-exact.  Synchronises `stream` once per order
- * statistic (a 4-byte read-back of the settled-column count, which skips
- * the radix passes when the sampled bracket settled every column). */
+ * np.median semantics, bit-exact.  From n = 500000 rows on it synchronises
+ * `stream` once per order statistic (a 4-byte read-back of the
+ * settled-column count, which skips the radix passes when the sampled
+ * bracket settled every column); below that it is the radix select alone,
+ * fully asynchronous. */
 int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
                               int S, double* median_out, double* mad_out,
                               void* ws, size_t ws_bytes, hipStream_t stream);

@@ -95,6 +95,12 @@ _SIGS = {
     "abc_kde_logpdf_mfma": (c_int, [c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                     c_int, c_ptr, c_dbl, c_ptr, c_ptr, c_size,
                                     c_ptr]),
+    "abc_kde_pack_new_mfma_rows": (c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                           c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
+                                           c_ptr, c_ptr, c_ptr]),
+    "abc_kde_logpdf_mfma_rows": (c_int, [c_ptr, c_ptr, c_ptr, c_i64, c_ptr,
+                                         c_ptr, c_i64, c_int, c_ptr, c_ptr,
+                                         c_dbl, c_ptr, c_ptr, c_size, c_ptr]),
     "abc_importance_weights_f64": (c_int, [c_ptr, c_ptr, c_dbl, c_i64, c_ptr,
                                            c_ptr]),
     # (a4)

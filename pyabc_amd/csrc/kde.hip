@@ -770,32 +770,25 @@ int logsum_impl(const T* Ynew, const T* Yprev, const T* logw, int64_t M,
   return kOk;
 }
 
-// shared with kde_mfma.hip (kde_internal.hpp): the fixed-order segment sum
-// and underflow detection of the fp32-exponent pass, then the two-pass fixup
-// in fp64 on fp64 rows (exponents exact in fp64, each term's 2^x from
-// v_exp_f32 on the fraction: ~1.2e-7 relative, inside the pass's 1e-5
-// contract; the fp64 pass keeps fp64 exp2).  An fp32 copy of a far row (|y| ~ 30 in log2 units)
-// carries ~2e-6 absolute error per coordinate, i.e. up to 5e-5 relative on
-// the density through |y_i - y_j|^2: the fixup rows are exactly the far ones,
-// so they are evaluated from the fp64 whitened rows
-// (tests/test_gpu_fullsize.py, constructed rows beyond the population).
-int kde_finish_mfma(const double* partial, int64_t M, int nseg,
-                    const double* Ynew, const double* P, int64_t npad, int d,
-                    const double* lw2max, double log_const, double* out_logpd,
-                    int* n_fix, int* fix_rows, hipStream_t stream) {
-  // the MFMA pass re-evaluates rows below 2^-32 exactly: its folded
-  // exponent error grows with the dominant |e| (kde_mfma.hip, kFoldKL)
-  constexpr double kMfmaFixupSum = 2.3283064365386963e-10;  // 2^-32
-  hipLaunchKernelGGL((kde_finalize_kernel<float>), dim3(ceil_div(M, 256)),
-                     dim3(256), 0, stream, partial, M, nseg, lw2max,
-                     log_const, out_logpd, n_fix, fix_rows, kMfmaFixupSum);
-  ABC_LAUNCH_CHECK("kde_finalize_kernel");
+// shared with kde_mfma.hip (kde_internal.hpp): the two-pass fixup of the
+// rows the MFMA pass could not resolve on the matrix cores (outside the grid
+// range, offsets beyond the piece range), in fp64 on the fp64 whitened rows.
+// An fp32 copy of a far row (|y| ~ 30 in log2 units) carries ~2e-6 absolute
+// error per coordinate, i.e. up to 5e-5 relative on the density through
+// |y_i - y_j|^2, so these rows are evaluated from the fp64 rows
+// (tests/test_gpu_fullsize.py, constructed rows beyond the population); each
+// term's 2^x is v_exp_f32 on the fraction (~1.2e-7 relative, inside the
+// pass's 1e-5 contract; the fp64 pass keeps fp64 exp2).
+int kde_fixup_rows_mfma(const double* Ynew, const double* P, int64_t npad,
+                        int d, const double* lw2max, double log_const,
+                        const int* n_fix, const int* fix_rows,
+                        double* out_logpd, hipStream_t stream) {
   switch (padded_dim(d)) {
 #define CASE(DD)                                                              \
   case DD:                                                                    \
-    hipLaunchKernelGGL((kde_fixup_kernel<double, DD, true>), dim3(kFixupBlocks), dim3(256), 0, \
-                       stream, Ynew, P, npad, lw2max, log_const, n_fix,       \
-                       fix_rows, out_logpd);                                  \
+    hipLaunchKernelGGL((kde_fixup_kernel<double, DD, true>), dim3(kFixupBlocks), \
+                       dim3(256), 0, stream, Ynew, P, npad, lw2max, log_const, \
+                       n_fix, fix_rows, out_logpd);                           \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
@@ -827,10 +820,12 @@ int abc_kde_padded_dim(int d) { return padded_dim(d); }
 int abc_kde_row_pad(void) { return kRowPad; }
 
 size_t abc_kde_workspace_bytes(int64_t M, int64_t npad, int d) {
-  // one size for both precisions (their plans may split differently)
+  // one size for every pass (their plans may split differently; the MFMA
+  // pass adds its refine lists and fragments)
   const size_t a = ws_bytes_impl<float>(M, npad, d);
   const size_t b = ws_bytes_impl<double>(M, npad, d);
-  return a > b ? a : b;
+  const size_t c = kde_mfma_ws_bytes(M, npad, d);
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
 int abc_kde_segments(int64_t npad) { return kde_segments(npad); }

@@ -1,5 +1,5 @@
 // Internal interface between kde.hip (direct fp32/fp64 pass) and
-// kde_mfma.hip (exact-grid bf16 MFMA pass): both share the fixed j-segment
+// kde_mfma.hip (exact-grid f16-piece MFMA pass): both share the fixed j-segment
 // plan, the direct packed population (P[npad][D+1], fp64 for the MFMA
 // pass's fixup) and the finalize/underflow-fixup kernels.  Not part of the
 // C-ABI.
@@ -16,8 +16,13 @@ int kde_pack_direct_f64(const double* X, const double* w, int64_t n, int d,
                         const double* mu, const double* Us, double* P,
                         int64_t npad, double* lw2max, void* ws,
                         hipStream_t st);
-int kde_finish_mfma(const double* partial, int64_t M, int nseg,
-                    const double* Ynew, const double* P, int64_t npad, int d,
-                    const double* lw2max, double log_const, double* out_logpd,
-                    int* n_fix, int* fix_rows, hipStream_t stream);
+// the exact two-pass fixup (fp64 rows, v_exp_f32 on each term's fraction)
+// of the MFMA pass's listed rows: (*n_fix, fix_rows)
+int kde_fixup_rows_mfma(const double* Ynew, const double* P, int64_t npad,
+                        int d, const double* lw2max, double log_const,
+                        const int* n_fix, const int* fix_rows,
+                        double* out_logpd, hipStream_t stream);
+// workspace of abc_kde_logpdf_mfma[_rows] (partials, refine lists and
+// fragments)
+size_t kde_mfma_ws_bytes(int64_t M, int64_t npad, int d);
 }  // namespace abc

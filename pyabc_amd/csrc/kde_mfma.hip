@@ -496,58 +496,109 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
   }
 }
 
+// Per-row offsets (round 5).  Row i's exponents are taken relative to
+// m_i (log2 units, <= 0): e'_ij = e_ij - m_i, packed as b'_i = -|y_i|^2 - m_i
+// (still split into exact multiples of G plus a remainder, so hi stays exact;
+// |b'| <= 2^22 G is checked), and the finalize adds ln2 m_i back.  The
+// folded chain rounds each lo MFMA at |e'| instead of |e|, so a row whose
+// dominant terms sit near its own offset is as accurate as a row near the
+// largest weight ("Accuracy of the folded
+// accumulation").  m_i comes from the row's parent (the particle its
+// proposal was resampled from: e_self = lw2_p - |y_i - y_p|^2, floored, at
+// most 64 below the global offset) or from the refine below.
+constexpr double kRowOffMin = -64.0;
+constexpr double kF16MaxQ = 4.19e6;  // |b'| / G bound (two 11-bit pieces: 4194303)
+
+// f16 B fragments of one whitened row with offset m (false: not packable --
+// outside the grid range or b' beyond the two-piece range; the fragments
+// then carry e = -inf)
 template <int D>
-__global__ __launch_bounds__(256) void pack_new_frag_kernel(
-    const double* __restrict__ theta, int64_t M, int64_t mpad, int d,
-    const double* __restrict__ mu, const double* __restrict__ Us,
-    const double* __restrict__ gscale, double* __restrict__ Ydir,
-    bf16x8* __restrict__ B) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= mpad) return;
-  const double g = *gscale;
-  double y[D];
-  bool ok = i < M;
-  if (ok) {
-    whiten_row<D>(theta, i, d, mu, Us, y);
-    double n2 = 0.0;
+__device__ inline bool pack_row_new(const double* y, double g, double m,
+                                    bf16x8* __restrict__ B, int64_t slot) {
+  double n2 = 0.0;
+  bool ok = g > 0.0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      Ydir[i * D + k] = y[k];
-      ok = ok && fabs(y[k]) <= 256.0 * g;  // NaN -> not ok
-      n2 = fma(y[k], y[k], n2);
-    }
-    if constexpr (Mk<D>::F16)  // the norm bound of the f16 scheme
-      ok = i < M && g > 0.0 && sqrt(n2) <= 2040.0 * g;
+  for (int k = 0; k < D; ++k) {
+    ok = ok && fabs(y[k]) <= 256.0 * g;  // NaN -> not ok
+    n2 = fma(y[k], y[k], n2);
   }
   if constexpr (Mk<D>::F16) {
+    ok = g > 0.0 && sqrt(n2) <= 2040.0 * g;  // the norm bound of the f16 scheme
+    ok = ok && fabs(-n2 - m) <= kF16MaxQ * g * g;
     unsigned short y1[D], r2[D], r3[D], r2h[D], h[2], l[2];
     unsigned short kpow = kF16One;
     if (ok) {
       const int K = f16_shift(g);
       kpow = f16_bits(ldexpf(1.0f, K));
       constexpr bool SC = Mk<D>::SCH == 1;
-      const double n2 = split_row_f16<D, SC>(y, g, 2.0f, y1, r2, r3, r2h);
-      split_value_f16<SC>(-n2, g * g, K, h, l);
-    } else {  // padding / out-of-grid row: e = -inf, exact fixup if i < M
+      const double n2r = split_row_f16<D, SC>(y, g, 2.0f, y1, r2, r3, r2h);
+      split_value_f16<SC>(-n2r - m, g * g, K, h, l);
+    } else {  // padding / out-of-grid row: e = -inf
 #pragma unroll
       for (int k = 0; k < D; ++k) y1[k] = r2[k] = r3[k] = r2h[k] = 0;
       h[0] = kF16NegInf;
       h[1] = l[0] = l[1] = 0;
     }
-    store_frags_f16<D, false>(B, i, y1, r2, r3, r2h, h, l, kpow);
-    return;
-  }
-  unsigned short y1[D], y2[D], y3[D], h[3], l[2];
-  if (ok) {
-    const double n2 = split_row<D>(y, g, 2.0f, y1, y2, y3);
-    split_value(-n2, g * g, h, l);
-  } else {  // padding / out-of-grid row: e = -inf, exact fixup if i < M
+    store_frags_f16<D, false>(B, slot, y1, r2, r3, r2h, h, l, kpow);
+  } else {
+    unsigned short y1[D], y2[D], y3[D], h[3], l[2];
+    ok = ok && fabs(-n2 - m) <= 8.0e6 * g * g;  // three bf16 pieces: 2^23
+    if (ok) {
+      const double n2r = split_row<D>(y, g, 2.0f, y1, y2, y3);
+      split_value(-n2r - m, g * g, h, l);
+    } else {
 #pragma unroll
-    for (int k = 0; k < D; ++k) y1[k] = y2[k] = y3[k] = 0;
-    h[0] = kBf16NegInf;
-    h[1] = h[2] = l[0] = l[1] = 0;
+      for (int k = 0; k < D; ++k) y1[k] = y2[k] = y3[k] = 0;
+      h[0] = kBf16NegInf;
+      h[1] = h[2] = l[0] = l[1] = 0;
+    }
+    store_frags<D, false>(B, slot, y1, y2, y3, h, l);
   }
-  store_frags<D, false>(B, i, y1, y2, y3, h, l);
+  return ok;
+}
+
+// parent offset of row i (see above): P is the fp64 direct population
+// [npad][D + 1] (y_j, lw2_j)
+template <int D>
+__device__ inline double parent_offset(const double* y, const double* __restrict__ P,
+                                       int64_t p) {
+  const double* pp = P + p * (D + 1);
+  double e = pp[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double df = y[k] - pp[k];
+    e = fma(-df, df, e);
+  }
+  return e == e ? fmin(fmax(floor(e), kRowOffMin), 0.0) : 0.0;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void pack_new_frag_kernel(
+    const double* __restrict__ theta, int64_t M, int64_t mpad, int d,
+    const double* __restrict__ mu, const double* __restrict__ Us,
+    const double* __restrict__ gscale, const double* __restrict__ P,
+    int64_t npad, const int64_t* __restrict__ parent,
+    double* __restrict__ Ydir, double* __restrict__ row_off,
+    bf16x8* __restrict__ B) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= mpad) return;
+  const double g = *gscale;
+  double y[D];
+  double m = 0.0;
+  if (i < M) {
+    whiten_row<D>(theta, i, d, mu, Us, y);
+#pragma unroll
+    for (int k = 0; k < D; ++k) Ydir[i * D + k] = y[k];
+    if (parent) {
+      const int64_t p = parent[i];
+      if (p >= 0 && p < npad) m = parent_offset<D>(y, P, p);
+    }
+    if (row_off) row_off[i] = m;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) y[k] = NAN;  // padding: e = -inf
+  }
+  pack_row_new<D>(y, g, m, B, i);
 }
 
 // the 32x32x16 MFMA of the piece scheme: f16 (d > 8) or bf16 (d <= 8); the
@@ -579,11 +630,12 @@ __device__ __forceinline__ float combine(float hi, float lo) {
 // MFMAs then rounds at |e| instead of once, so a term's exponent carries
 // about (KL + 1) / 2 ulps of |e| instead of 1/2: relative error ~8e-8 |e|
 // at KL = 4.  A row's error is the t-weighted mean of its terms' errors,
-// bounded by ~8e-8 log2(N / S) for a row sum S; rows with S < 2^-32 (dominant
-// exponents beyond ~32) take the exact fp64 fixup (kMfmaFixupSum), so the
-// bound is ~4e-6 at N = 1e6 (measured: tests/test_gpu_fullsize.py, DESIGN
-// section 4).  The f16 scheme 2 (8 < d <= 24) folds the same way, its
-// error measured per dimension in the scheme table above.
+// bounded by ~8e-8 log2(N / S) for a row sum S.  Since round 5 rows are
+// evaluated relative to their own offset and re-evaluated with a new one
+// when the sum leaves the routing range (Route, the refine below), which
+// keeps the rounding at |e'| small; DESIGN.md section 4 derives the per-row
+// bound (tests/test_gpu_kde_band.py evaluates it row by row).  The f16
+// scheme 2 (8 < d <= 24) folds the same way.
 constexpr int kFoldKL = 4;
 
 // one (32-row tile, i-tile) product: hi (exact) and lo accumulators, or the
@@ -641,21 +693,45 @@ __device__ __forceinline__ float tile_sum(const f32x16& hi, const f32x16& lo) {
   }
 }
 
+// largest e over the lane's 16 values (the refine's max pass, MODE 1):
+// the same folded / split e as tile_sum exponentiates
+template <int KL, int SCH>
+__device__ __forceinline__ float tile_max(const f32x16& hi, const f32x16& lo) {
+  float e[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v)
+    e[v] = kFolded<KL, SCH> ? hi[v] : combine<(SCH == 1)>(hi[v], lo[v]);
+#pragma unroll
+  for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+    for (int v = 0; v < w; ++v) e[v] = fmaxf(e[v], e[v + w]);
+  return e[0];
+}
+
+// MODE 0: sum of 2^e (the density pass); MODE 1: max of e (the refine's
+// offset pass).  Same MFMA chain either way.
+template <int MODE, int KL, int SCH>
+__device__ __forceinline__ void tile_acc(float& sacc, const f32x16& hi,
+                                         const f32x16& lo) {
+  if constexpr (MODE == 0)
+    sacc += tile_sum<KL, SCH>(hi, lo);
+  else
+    sacc = fmaxf(sacc, tile_max<KL, SCH>(hi, lo));
+}
+
 // main pass.  Block (rb, s): wave w owns i-tiles (rb*kWaves + w)*IB + t and
 // walks the spb consecutive j-segments s*spb ..; per segment one fp64 partial
-// per row.  64-row chunks (two 32-row tiles) are summed in fp32, then added
-// into fp64.
-template <int KH, int KL, int IB, bool PIPE, int SCH>
-__device__ __forceinline__ void kde_mfma_body(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
+// per row (partial[seg * ld + i], ld >= M).  64-row chunks (two 32-row tiles)
+// are summed in fp32, then added into fp64 (MODE 1: maxima instead).
+template <int KH, int KL, int IB, bool PIPE, int SCH, int MODE = 0>
+__device__ __forceinline__ void kde_mfma_rows(
+    const bf16x8* __restrict__ Bfr, int64_t M, int64_t ld,
+    const bf16x8* __restrict__ Afr, int64_t npad, int s, int64_t rb, int spb,
+    int jseg, double* __restrict__ partial) {
   constexpr int KT = KH + KL;
+  constexpr float kInit = MODE == 0 ? 0.0f : -INFINITY;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int s;
-  int64_t rb;
-  block_coords(split, s, rb);
-  split = split < 0 ? -split : split;
   const int64_t t0 = (rb * kWaves + wave) * IB;
 
   bf16x8 bq[IB][KT];
@@ -671,7 +747,7 @@ __device__ __forceinline__ void kde_mfma_body(
     const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64 + lane;
     double S[IB];
 #pragma unroll
-    for (int t = 0; t < IB; ++t) S[t] = 0.0;
+    for (int t = 0; t < IB; ++t) S[t] = kInit;
     // a[0] / a[1]: the two 32-row tiles of the current 64-row chunk.  Each
     // tile's fragments are requested one half-chunk before their first MFMA
     // (tile 1 while tile 0 computes, the next chunk's tile 0 while tile 1
@@ -688,7 +764,7 @@ __device__ __forceinline__ void kde_mfma_body(
           Aseg + (((jc + 64 < nj) ? jc + 64 : jc) >> 5) * KT * 64;
       float sacc[IB];
 #pragma unroll
-      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
+      for (int t = 0; t < IB; ++t) sacc[t] = kInit;
       if constexpr (PIPE) {
         // 2*IB (tile, i-tile) steps; the MFMAs of step q+1 issue before the
         // VALU of step q, on a second accumulator pair
@@ -705,7 +781,7 @@ __device__ __forceinline__ void kde_mfma_body(
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
           }
-          sacc[q % IB] += tile_sum<KL, SCH>(hi[q & 1], lo[q & 1]);
+          tile_acc<MODE, KL, SCH>(sacc[q % IB], hi[q & 1], lo[q & 1]);
         }
       } else {
 #pragma unroll
@@ -714,7 +790,7 @@ __device__ __forceinline__ void kde_mfma_body(
         for (int q = 0; q < 2 * IB; ++q) {
           f32x16 hi, lo;
           mfma_step<KH, KL, SCH>(a[q / IB], bq[q % IB], hi, lo);
-          sacc[q % IB] += tile_sum<KL, SCH>(hi, lo);
+          tile_acc<MODE, KL, SCH>(sacc[q % IB], hi, lo);
           if (q + 1 == IB) {
 #pragma unroll
             for (int c = 0; c < KT; ++c) a[0][c] = an[c * 64];
@@ -722,13 +798,19 @@ __device__ __forceinline__ void kde_mfma_body(
         }
       }
 #pragma unroll
-      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
+      for (int t = 0; t < IB; ++t) {
+        if constexpr (MODE == 0)
+          S[t] += static_cast<double>(sacc[t]);
+        else
+          S[t] = fmax(S[t], static_cast<double>(sacc[t]));
+      }
     }
 #pragma unroll
     for (int t = 0; t < IB; ++t) {
-      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
+      const double o = __shfl_xor(S[t], 32, 64);
+      const double tot = MODE == 0 ? S[t] + o : fmax(S[t], o);
       const int64_t i = (t0 + t) * 32 + lane;
-      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * ld + i] = tot;
     }
   }
 }
@@ -737,8 +819,29 @@ template <int KH, int KL, int IB, bool PIPE, int SCH>
 __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
     int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  kde_mfma_body<KH, KL, IB, PIPE, SCH>(Bfr, M, Afr, npad, split, spb, jseg,
+  int s;
+  int64_t rb;
+  block_coords(split, s, rb);
+  kde_mfma_rows<KH, KL, IB, PIPE, SCH>(Bfr, M, M, Afr, npad, s, rb, spb, jseg,
                                        partial);
+}
+
+// The same pass over a device-counted row list (the refine of flagged rows,
+// below): rows [0, *count) of Bfr, partial[seg * ld + row]; blocks take
+// (segment, row block) pairs grid-stride, so an empty list costs only the
+// blocks' exit.  A row's arithmetic is that of kde_mfma_kernel.
+template <int KH, int KL, int IB, bool PIPE, int SCH, int MODE>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_list_kernel(
+    const bf16x8* __restrict__ Bfr, const int* __restrict__ count, int64_t ld,
+    const bf16x8* __restrict__ Afr, int64_t npad, int nseg, int jseg,
+    double* __restrict__ partial) {
+  const int64_t M = *count;
+  const int64_t nrb = ceil_div(M, 32 * kWaves * IB);
+  const int s = static_cast<int>(blockIdx.x % nseg);
+  const int64_t stride = gridDim.x / nseg;
+  for (int64_t rb = blockIdx.x / nseg; rb < nrb; rb += stride)
+    kde_mfma_rows<KH, KL, IB, PIPE, SCH, MODE>(Bfr, M, ld, Afr, npad, s, rb, 1,
+                                               jseg, partial);
 }
 
 // MFMA-bound form for d > 8.  Per 32x32 tile a wave runs KT = KH + KL
@@ -752,7 +855,7 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_kernel(
 // only 1/(kWaves*IB) of the A bytes.  A wave holds B (IB*KT fragments), the
 // 2*IB accumulators and one A fragment in flight, so two waves share a SIMD
 // and one wave's exp block runs beside another's MFMA chain.  Per-lane
-// arithmetic and summation order are those of kde_mfma_body (split hi / lo
+// arithmetic and summation order are those of kde_mfma_rows (split hi / lo
 // accumulators, tile 0 then tile 1 of each chunk): the rows are
 // bit-identical to kde_mfma_kernel's.
 template <int KH, int KL, int IB, int SCH>
@@ -1387,11 +1490,227 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
                        p.spb, p.jseg, partial);
 }
 
+// ---- refine: flagged rows re-evaluated with their own offset (round 5) -----
+// Pass 1 evaluates every row relative to its offset m_i (0, or the parent's
+// term).  Rows whose sum S_i leaves [lo, hi] are refined on the matrix cores
+// instead of going to the fp64 fixup:
+//   * S_i in the normal range: m_i += floor(log2 S_i) (the dominant terms
+//     then sit in [-log2 n_eff - 1, 0]);
+//   * S_i underflowed: one max pass of the same folded e over the row list
+//     (MODE 1), m_i += floor(max_j e'_ij);
+//   then the density pass again over the list with the new offsets.  Rows
+// outside the grid range, or whose offset leaves the two-piece range of b',
+// and any row the second pass still cannot resolve, take the exact fp64
+// fixup.  lo: the folded scheme's routing bound: a row
+// whose dominant exponent lies within 2^-lo of its offset keeps the derived
+// bound under 1e-5 / 1.5 -- 2^-16 where KL <= 3 lo MFMAs fold (d <= 8),
+// 2^-4 where KL = 4 ... 8 (8 < d <= 24); hi = 1 / lo for rows with an offset
+// (the parent's term was not the dominant one).  The split and bf16 schemes
+// keep the 2^-32 of rounds 1-4.
 template <int D>
-int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
-                     const bf16x8* Afr, const double* P, int64_t npad, int d,
-                     const double* lw2max, double log_const, double* out,
-                     void* ws, size_t ws_bytes, hipStream_t st) {
+struct Route {
+  static constexpr bool kFold = Mk<D>::SCH == 2;
+  static constexpr double lo = !kFold ? 0x1p-32 : (Mk<D>::KL <= 3 ? 0x1p-16 : 0x1p-4);
+  static constexpr double hi = !kFold ? 0x1p+100 : 1.0 / lo;
+};
+constexpr double kLn2d = 0.6931471805599453;
+constexpr int kListBlocks = 8192;  // (segment, row block) blocks of a list pass
+
+// workspace of the MFMA pass: [nseg][M] fp64 partials, the 16 counters
+// (cnt[0] fp64-fixup rows, [1] flagged, [2] refine list, [3] max list), then
+// the lists and the refine's B fragments
+struct MfmaWs {
+  double* partial;
+  int* cnt;
+  int *rows1, *rows2, *rowsx, *rows3;
+  double *s1, *m2, *mxo;
+  bf16x8* Bbuf;
+};
+inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+
+template <int D>
+size_t mfma_ws_layout(int64_t M, int nseg, char* base, MfmaWs* w) {
+  const size_t m = static_cast<size_t>(M);
+  size_t off = static_cast<size_t>(nseg) * m * 8;  // counters right after
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off = al256(off + bytes);
+    return p;
+  };
+  char* part = base;
+  char* cnt = take(64);
+  char* r1 = take(4 * m);
+  char* s1 = take(8 * m);
+  char* r2 = take(4 * m);
+  char* m2 = take(8 * m);
+  char* rx = take(4 * m);
+  char* mx = take(8 * m);
+  char* r3 = take(4 * m);
+  char* bb = take(static_cast<size_t>(mpad_rows<D>(M) / 32) * Mk<D>::KT * 64 * 16);
+  if (w) {
+    w->partial = reinterpret_cast<double*>(part);
+    w->cnt = reinterpret_cast<int*>(cnt);
+    w->rows1 = reinterpret_cast<int*>(r1);
+    w->s1 = reinterpret_cast<double*>(s1);
+    w->rows2 = reinterpret_cast<int*>(r2);
+    w->m2 = reinterpret_cast<double*>(m2);
+    w->rowsx = reinterpret_cast<int*>(rx);
+    w->mxo = reinterpret_cast<double*>(mx);
+    w->rows3 = reinterpret_cast<int*>(r3);
+    w->Bbuf = reinterpret_cast<bf16x8*>(bb);
+  }
+  return off;
+}
+
+// pass-1 finalize: the fixed-order segment sum; rows inside [lo, hi] (hi
+// only where the row has an offset) are final, the rest join the refine list
+__global__ __launch_bounds__(256) void mfma_finalize_kernel(
+    const double* __restrict__ partial, int64_t M, int nseg,
+    const double* __restrict__ row_off, const double* __restrict__ lw2max,
+    double log_const, double lo, double hi, double* __restrict__ out,
+    int* __restrict__ cnt, int* __restrict__ rows1, double* __restrict__ s1) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  double S = 0.0;
+  for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * M + i];
+  const double m = row_off ? row_off[i] : 0.0;
+  const double off = kLn2d * (*lw2max) + log_const;
+  if (S >= lo && (S <= hi || m == 0.0)) {
+    out[i] = log(S) + off + kLn2d * m;
+  } else {
+    const int f = atomicAdd(cnt + 1, 1);
+    rows1[f] = static_cast<int>(i);
+    s1[f] = S;
+    out[i] = -INFINITY;
+  }
+}
+
+template <int D>
+__device__ inline bool on_grid(const double* y, double g) {
+  double n2 = 0.0;
+  bool ok = g > 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    ok = ok && fabs(y[k]) <= 256.0 * g;
+    n2 = fma(y[k], y[k], n2);
+  }
+  if constexpr (Mk<D>::F16) ok = g > 0.0 && sqrt(n2) <= 2040.0 * g;
+  return ok;
+}
+
+// flagged rows -> refine list (offset from the sum), max list (sum
+// underflowed; packed with the pass-1 offset for the max pass) or fixup
+template <int D>
+__global__ __launch_bounds__(256) void refine_classify_kernel(
+    int* __restrict__ cnt, const int* __restrict__ rows1,
+    const double* __restrict__ s1, const double* __restrict__ row_off,
+    const double* __restrict__ Ynew, const double* __restrict__ gscale,
+    int* __restrict__ rows2, double* __restrict__ m2, int* __restrict__ rowsx,
+    double* __restrict__ mxo, int* __restrict__ rows3, bf16x8* __restrict__ Bbuf) {
+  const int n1 = cnt[1];
+  const double g = gscale ? *gscale : -1.0;  // no grid: every row to the fixup
+  for (int f = blockIdx.x * blockDim.x + threadIdx.x; f < n1;
+       f += gridDim.x * blockDim.x) {
+    const int row = rows1[f];
+    const double m = row_off ? row_off[row] : 0.0;
+    const double S = s1[f];
+    double y[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) y[k] = Ynew[static_cast<int64_t>(row) * D + k];
+    if (!on_grid<D>(y, g)) {
+      rows3[atomicAdd(cnt, 1)] = row;
+    } else if (S > 0x1p-100 && S < 0x1p+100) {
+      const int q = atomicAdd(cnt + 2, 1);
+      rows2[q] = row;
+      m2[q] = m + floor(log2(S));
+    } else {
+      const int q = atomicAdd(cnt + 3, 1);
+      rowsx[q] = row;
+      mxo[q] = m;
+      pack_row_new<D>(y, g, m, Bbuf, q);
+    }
+  }
+}
+
+// max list -> refine list with m += floor(max e'), or fixup
+__global__ __launch_bounds__(256) void refine_after_max_kernel(
+    int* __restrict__ cnt, const int* __restrict__ rowsx,
+    const double* __restrict__ mxo, const double* __restrict__ partial,
+    int64_t ld, int nseg, int* __restrict__ rows2, double* __restrict__ m2,
+    int* __restrict__ rows3) {
+  const int nx = cnt[3];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nx;
+       q += gridDim.x * blockDim.x) {
+    double mx = -INFINITY;
+    for (int s = 0; s < nseg; ++s)
+      mx = fmax(mx, partial[static_cast<int64_t>(s) * ld + q]);
+    if (mx > -1.0e30 && mx < 1.0e30) {
+      const int r = atomicAdd(cnt + 2, 1);
+      rows2[r] = rowsx[q];
+      m2[r] = mxo[q] + floor(mx);
+    } else {
+      rows3[atomicAdd(cnt, 1)] = rowsx[q];
+    }
+  }
+}
+
+// B fragments of the refine list with the new offsets (an unpackable offset
+// marks the row for the fixup: m2 = NaN)
+template <int D>
+__global__ __launch_bounds__(256) void refine_pack_kernel(
+    const int* __restrict__ cnt, const int* __restrict__ rows2,
+    double* __restrict__ m2, const double* __restrict__ Ynew,
+    const double* __restrict__ gscale, bf16x8* __restrict__ Bbuf) {
+  const int n2 = cnt[2];
+  const double g = gscale ? *gscale : -1.0;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n2;
+       q += gridDim.x * blockDim.x) {
+    double y[D];
+    const int64_t row = rows2[q];
+#pragma unroll
+    for (int k = 0; k < D; ++k) y[k] = Ynew[row * D + k];
+    if (!pack_row_new<D>(y, g, m2[q], Bbuf, q)) m2[q] = NAN;
+  }
+}
+
+__global__ __launch_bounds__(256) void refine_finalize_kernel(
+    int* __restrict__ cnt, const int* __restrict__ rows2,
+    const double* __restrict__ m2, const double* __restrict__ partial,
+    int64_t ld, int nseg, const double* __restrict__ lw2max, double log_const,
+    double* __restrict__ out, int* __restrict__ rows3) {
+  const int n2 = cnt[2];
+  const double off = kLn2d * (*lw2max) + log_const;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n2;
+       q += gridDim.x * blockDim.x) {
+    double S = 0.0;
+    for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * ld + q];
+    const double mm = m2[q];
+    if (mm == mm && S >= 0x1p-32 && S < 0x1p+100)
+      out[rows2[q]] = log(S) + off + kLn2d * mm;
+    else
+      rows3[atomicAdd(cnt, 1)] = rows2[q];
+  }
+}
+
+template <int D, int MODE>
+void launch_list(const bf16x8* Bbuf, const int* count, int64_t ld,
+                 const bf16x8* Afr, int64_t npad, int nseg, int jseg,
+                 double* partial, hipStream_t st) {
+  constexpr int IB = Mk<D>::IB;
+  const int rbs = kListBlocks / nseg > 0 ? kListBlocks / nseg : 1;
+  hipLaunchKernelGGL((kde_mfma_list_kernel<Mk<D>::KH, Mk<D>::KL, IB, (D <= 8),
+                                           Mk<D>::SCH, MODE>),
+                     dim3(rbs * nseg), dim3(64 * kWaves), 0, st, Bbuf, count, ld,
+                     Afr, npad, nseg, jseg, partial);
+}
+
+template <int D>
+int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
+                     const double* row_off, int64_t M, const bf16x8* Afr,
+                     const double* P, int64_t npad, int d,
+                     const double* lw2max, const double* gscale,
+                     double log_const, double* out, void* ws, size_t ws_bytes,
+                     hipStream_t st) {
   // i-tiles per wave: Mk<D>::IB (the row padding unit) or a divisor of it
   // (tuning override ABC_KDE_MFMA_IB); a row's arithmetic is the same
   constexpr int IBF = Mk<D>::IB;
@@ -1420,27 +1739,62 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew, int64_t M,
   const bool smajor =
       tuning_knob(kKnobKdeMfmaSmajor, npad >= (int64_t{1} << 18) ? 1 : 0) != 0;
   const MPlan p = make_mplan<D>(M, npad, ib, smajor);
-  const size_t need = static_cast<size_t>(p.nseg * M) * 8 + 16 +
-                      static_cast<size_t>(M) * 4;
+  const size_t need = mfma_ws_layout<D>(M, p.nseg, nullptr, nullptr);
   ABC_REQUIRE(ws_bytes >= need, "kde_mfma: workspace too small (%zu < %zu)",
               ws_bytes, need);
-  char* base = static_cast<char*>(ws);
-  double* partial = reinterpret_cast<double*>(base);
-  int* n_fix = reinterpret_cast<int*>(base + static_cast<size_t>(p.nseg * M) * 8);
-  int* fix_rows = n_fix + 4;
-  ABC_HIP(hipMemsetAsync(n_fix, 0, 16, st));
+  MfmaWs w;
+  mfma_ws_layout<D>(M, p.nseg, static_cast<char*>(ws), &w);
+  ABC_HIP(hipMemsetAsync(w.cnt, 0, 64, st));
   if (ib == IBF)
-    launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, partial, lds2g, st);
+    launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
   else if (ib == IB2)
-    launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, partial, lds2g, st);
+    launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
   else
-    launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, partial, lds2g, st);
+    launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
   ABC_LAUNCH_CHECK("kde_mfma_kernel");
-  return kde_finish_mfma(partial, M, p.nseg, Ynew, P, npad, d, lw2max,
-                         log_const, out, n_fix, fix_rows, st);
+  const unsigned gm = static_cast<unsigned>(ceil_div(M, 256));
+  const unsigned gl = stream_grid(M, 256, 1024);
+  // without the grid (abc_kde_logpdf_mfma) flagged rows go straight to the
+  // fp64 fixup, at the 2^-32 bound of rounds 1-4
+  const double lo = gscale ? Route<D>::lo : 0x1p-32;
+  const double hi = gscale ? Route<D>::hi : INFINITY;
+  hipLaunchKernelGGL(mfma_finalize_kernel, dim3(gm), dim3(256), 0, st, w.partial,
+                     M, p.nseg, row_off, lw2max, log_const, lo, hi, out, w.cnt,
+                     w.rows1, w.s1);
+  hipLaunchKernelGGL(refine_classify_kernel<D>, dim3(gl), dim3(256), 0, st, w.cnt,
+                     w.rows1, w.s1, row_off, Ynew, gscale, w.rows2, w.m2, w.rowsx,
+                     w.mxo, w.rows3, w.Bbuf);
+  ABC_LAUNCH_CHECK("kde_mfma refine classify");
+  launch_list<D, 1>(w.Bbuf, w.cnt + 3, M, Afr, npad, p.nseg, p.jseg, w.partial, st);
+  ABC_LAUNCH_CHECK("kde_mfma_list_kernel (max)");
+  hipLaunchKernelGGL(refine_after_max_kernel, dim3(gl), dim3(256), 0, st, w.cnt,
+                     w.rowsx, w.mxo, w.partial, M, p.nseg, w.rows2, w.m2, w.rows3);
+  hipLaunchKernelGGL(refine_pack_kernel<D>, dim3(gl), dim3(256), 0, st, w.cnt,
+                     w.rows2, w.m2, Ynew, gscale, w.Bbuf);
+  ABC_LAUNCH_CHECK("kde_mfma refine pack");
+  launch_list<D, 0>(w.Bbuf, w.cnt + 2, M, Afr, npad, p.nseg, p.jseg, w.partial, st);
+  ABC_LAUNCH_CHECK("kde_mfma_list_kernel (sum)");
+  hipLaunchKernelGGL(refine_finalize_kernel, dim3(gl), dim3(256), 0, st, w.cnt,
+                     w.rows2, w.m2, w.partial, M, p.nseg, lw2max, log_const, out,
+                     w.rows3);
+  ABC_LAUNCH_CHECK("kde_mfma refine finalize");
+  return kde_fixup_rows_mfma(Ynew, P, npad, d, lw2max, log_const, w.cnt, w.rows3,
+                             out, st);
 }
 
 }  // namespace
+
+size_t kde_mfma_ws_bytes(int64_t M, int64_t npad, int d) {
+  const int nseg = kde_num_segments(npad);
+  switch (kde_padded_dim(d)) {
+#define CASE(DD) \
+  case DD: return mfma_ws_layout<DD>(M, nseg, nullptr, nullptr);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
+    CASE(20) CASE(24) CASE(32)
+#undef CASE
+    default: return 0;
+  }
+}
 }  // namespace abc
 
 using namespace abc;
@@ -1495,10 +1849,12 @@ int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
   return kOk;
 }
 
-int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
-                          const double* mu, const double* Us,
-                          const double* gscale, double* Ynew, void* Bfr,
-                          hipStream_t st) {
+int abc_kde_pack_new_mfma_rows(const double* theta, int64_t M, int d,
+                               const double* mu, const double* Us,
+                               const double* gscale, const double* P,
+                               int64_t npad, const int64_t* parent,
+                               double* Ynew, void* Bfr, double* row_off,
+                               hipStream_t st) {
   ABC_REQUIRE(M >= 0, "pack_new_mfma: negative M");
   const int D = kde_padded_dim(d);
   if (D < 0) {
@@ -1508,14 +1864,16 @@ int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
   if (M == 0) return kOk;
   ABC_REQUIRE(theta && mu && Us && gscale && Ynew && Bfr,
               "pack_new_mfma: null pointer");
+  ABC_REQUIRE(!parent || (P && npad > 0),
+              "pack_new_mfma: parents need the packed population P");
   const int64_t mp = mpad_for(d, M);
   const unsigned gr = static_cast<unsigned>(ceil_div(mp, 256));
   switch (D) {
 #define CASE(DD)                                                              \
   case DD:                                                                    \
     hipLaunchKernelGGL((pack_new_frag_kernel<DD>), dim3(gr), dim3(256), 0, st, \
-                       theta, M, mp, d, mu, Us, gscale, Ynew,                 \
-                       static_cast<bf16x8*>(Bfr));                            \
+                       theta, M, mp, d, mu, Us, gscale, P, npad, parent,     \
+                       Ynew, row_off, static_cast<bf16x8*>(Bfr));            \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
@@ -1525,11 +1883,20 @@ int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
   return kOk;
 }
 
-int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
-                        const void* Afr, const double* P, int64_t npad, int d,
-                        const double* lw2max, double log_const,
-                        double* out_logpd, void* ws, size_t ws_bytes,
-                        hipStream_t st) {
+int abc_kde_pack_new_mfma(const double* theta, int64_t M, int d,
+                          const double* mu, const double* Us,
+                          const double* gscale, double* Ynew, void* Bfr,
+                          hipStream_t st) {
+  return abc_kde_pack_new_mfma_rows(theta, M, d, mu, Us, gscale, nullptr, 0,
+                                    nullptr, Ynew, Bfr, nullptr, st);
+}
+
+static int logpdf_mfma_entry(const void* Bfr, const double* Ynew,
+                             const double* row_off, int64_t M, const void* Afr,
+                             const double* P, int64_t npad, int d,
+                             const double* lw2max, const double* gscale,
+                             double log_const, double* out_logpd, void* ws,
+                             size_t ws_bytes, hipStream_t st) {
   ABC_REQUIRE(M >= 0 && npad >= 0, "kde_mfma: negative size");
   ABC_REQUIRE(npad % kKdeRowPad == 0, "kde_mfma: npad must be a multiple of %d",
               kKdeRowPad);
@@ -1540,10 +1907,10 @@ int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
   const bf16x8* B = static_cast<const bf16x8*>(Bfr);
   const bf16x8* A = static_cast<const bf16x8*>(Afr);
   switch (kde_padded_dim(d)) {
-#define CASE(DD)                                                          \
-  case DD:                                                                \
-    return logpdf_mfma_impl<DD>(B, Ynew, M, A, P, npad, d, lw2max,        \
-                                log_const, out_logpd, ws, ws_bytes, st);
+#define CASE(DD)                                                               \
+  case DD:                                                                     \
+    return logpdf_mfma_impl<DD>(B, Ynew, row_off, M, A, P, npad, d, lw2max,    \
+                                gscale, log_const, out_logpd, ws, ws_bytes, st);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)
 #undef CASE
@@ -1551,6 +1918,26 @@ int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
       set_error("kde_mfma: unsupported dimension d=%d (max 32)", d);
       return kUnsupported;
   }
+}
+
+int abc_kde_logpdf_mfma(const void* Bfr, const double* Ynew, int64_t M,
+                        const void* Afr, const double* P, int64_t npad, int d,
+                        const double* lw2max, double log_const,
+                        double* out_logpd, void* ws, size_t ws_bytes,
+                        hipStream_t st) {
+  return logpdf_mfma_entry(Bfr, Ynew, nullptr, M, Afr, P, npad, d, lw2max,
+                           nullptr, log_const, out_logpd, ws, ws_bytes, st);
+}
+
+int abc_kde_logpdf_mfma_rows(const void* Bfr, const double* Ynew,
+                             const double* row_off, int64_t M, const void* Afr,
+                             const double* P, int64_t npad, int d,
+                             const double* lw2max, const double* gscale,
+                             double log_const, double* out_logpd, void* ws,
+                             size_t ws_bytes, hipStream_t st) {
+  ABC_REQUIRE(gscale, "kde_mfma: null grid");
+  return logpdf_mfma_entry(Bfr, Ynew, row_off, M, Afr, P, npad, d, lw2max,
+                           gscale, log_const, out_logpd, ws, ws_bytes, st);
 }
 
 }  // extern "C"

@@ -1240,6 +1240,12 @@ __global__ void seg_median_kernel(const SegState* st, int S, int64_t n,
 constexpr int kBsBins = 4096;
 constexpr int kBsWaveBuf = 1024;        // compaction buffer per wave (keys)
 
+// Below kBsMinRows rows the 65536-key sample is a large share of the
+// column: the radix passes alone read less and need no read-back (median +
+// MAD at n = 2e5: 0.37 ms radix only, 0.40 ms with the bracket,
+// profiles/r04_mad_fetch.json); the call is then fully asynchronous.
+constexpr int64_t kBsMinRows = 500000;
+
 __host__ __device__ inline int64_t bs_sample_size(int64_t n) {
   int64_t m = n / 16;
   const int64_t q = n / 8192;
@@ -2056,6 +2062,7 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
     double* out = round == 0 ? median_out : mad_out;
     hipLaunchKernelGGL(seg_init_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, st,
                        sst, S, k);
+    if (n >= kBsMinRows) {
     // bracket select: sample digits, one read of each column, candidates
     const int64_t m = bs_sample_size(n);
     int sbps = static_cast<int>(ceil_div(m, 1024));
@@ -2084,7 +2091,9 @@ int abc_column_median_mad_f64(const double* data_T, int64_t ld, int64_t n,
     ABC_HIP(hipMemcpyAsync(&settled, ndone + round, 4, hipMemcpyDeviceToHost, st));
     ABC_HIP(hipStreamSynchronize(st));
     if (settled == static_cast<unsigned>(S)) continue;
-    // radix passes for the columns the bracket did not settle
+    }
+    // radix passes for the columns the bracket did not settle (every column
+    // below kBsMinRows rows)
     int consumed = 0;  // key bits selected so far
     for (int pass = 0; pass < kSegPasses; ++pass) {
       const int bits = kSegBits[pass];

@@ -241,8 +241,10 @@ class RankSliceComm(Comm):
             c = sizes[s]
             if c <= t.shape[0]:
                 pieces.append(t[:c])
+            elif t.shape[0] == 0:   # nothing to repeat: zero rows, same shape
+                pieces.append(t.new_zeros((c,) + tuple(t.shape[1:])))
             else:   # more rows than this rank holds: repeat them
-                reps = -(-c // max(t.shape[0], 1))
+                reps = -(-c // t.shape[0])
                 pieces.append(t.repeat((reps,) + (1,) * (t.dim() - 1))[:c])
         self._note("all_gather_rows", sizes[0] * row,
                    (sum(sizes) - sizes[0]) * row)

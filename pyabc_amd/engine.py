@@ -97,8 +97,11 @@ class DeviceMVNFit:
             self._tab = K.cdf_index(self._cdf)
         return self._cdf
 
-    def logpdf(self, theta):
-        return self.packed.logpdf(theta)
+    def logpdf(self, theta, parent=None):
+        """log transition density; ``parent``: per row the population index
+        its proposal was resampled from (optional; same density, the MFMA
+        pass then evaluates the row relative to its parent's term)."""
+        return self.packed.logpdf(theta, parent)
 
     def propose(self, lo, scale, seed, sid, offset, B):
         """B draws of resample + perturb + support flag (Philox); the CDF
@@ -166,6 +169,11 @@ def mirrors_simulate(model):
     the ``simulate`` it mirrors: a subclass that overrides ``simulate``
     (other noise, other statistics) without its own fused method is not
     fused, so its distances always come from its own simulate()."""
+    inst = vars(model) if hasattr(model, "__dict__") else {}
+    if "simulate" in inst or "simulate_distance" in inst:
+        # replaced on the instance: fused only if both come from it
+        return "simulate" in inst and "simulate_distance" in inst
+
     def owner(name):
         return next((c for c in type(model).__mro__ if name in c.__dict__),
                     None)
@@ -436,6 +444,11 @@ class GenerationEngine:
         n_acc = 0
         raw_off = 0
         eval_off = 0
+        # the accepted rows' parents (resample indices) travel with theta to
+        # the MFMA KDE pass, which evaluates each row relative to its
+        # parent's term (kde_mfma.hip, per-row offsets)
+        use_parent = fit is not None and getattr(
+            getattr(fit, "packed", None), "precision", None) == "mfma"
         # SingleCoreSampler starts evaluation k (1-based) iff k - 1 <
         # max_eval: at most ceil(max_eval) evaluations (singlecore.py:24-30)
         cap = math.ceil(max_eval) if math.isfinite(max_eval) else math.inf
@@ -464,6 +477,8 @@ class GenerationEngine:
                 nvs = comm.all_gather_ints(vcount)                  # sync 1
                 nv = nvs[r]
                 theta = K.gather_rows(theta_all, vpos, nv) if nv else None
+                pid = K.gather_rows(idx.to(F64), vpos, nv) \
+                    if nv and use_parent else None
             nv = nvs[r]
             my_eval = eval_off + sum(nvs[:r])
             sim_sid = self._stream(t, stream_base + 1)
@@ -510,7 +525,8 @@ class GenerationEngine:
                 nas = comm.all_gather_ints(0)
             if acceptance is None or not nv:
                 gcount = 0
-            rounds.append(dict(theta=theta, stats=stats, d=d, apos=apos,
+            rounds.append(dict(theta=theta, pid=pid if use_parent else None,
+                               stats=stats, d=d, apos=apos,
                                guard=guard, accw=accw, acc=acc, nvs=nvs,
                                nas=nas, acc0=n_acc, gcount=gcount,
                                need=need1, alast=alast))
@@ -553,7 +569,11 @@ class GenerationEngine:
             n_eval_loc += last
             if k:
                 sel = rd["apos"][:k]
-                th_loc.append(rd["theta"].index_select(0, sel))
+                th = rd["theta"].index_select(0, sel)
+                if use_parent:   # parent index as an extra column
+                    th = torch.cat([th, rd["pid"].index_select(0, sel)[:, None]],
+                                   1)
+                th_loc.append(th)
                 d_loc.append(rd["d"].index_select(0, sel))
                 if stochastic:
                     aw_loc.append(rd["accw"].index_select(0, sel))
@@ -578,7 +598,12 @@ class GenerationEngine:
             self.timers = tm
             return GenerationResult(ok=False, n_eval=int(cap))
         take_counts = [[tk[s] for tk in takes] for s in range(R)]
-        theta_acc = self._gather(th_loc, (self.d,), take_counts)
+        theta_acc = self._gather(th_loc, (self.d + int(use_parent),),
+                                 take_counts)
+        parent_acc = None
+        if use_parent:
+            parent_acc = theta_acc[:, self.d].to(torch.int64)
+            theta_acc = theta_acc[:, :self.d].contiguous()
         d_acc = self._gather(d_loc, (), take_counts)
         stats_acc = None
         if keep_stats:
@@ -608,14 +633,17 @@ class GenerationEngine:
             # row-parallel weight pass: rank r weights rows row_range(n)
             lo, hi = self.row_range(theta_acc.shape[0])
             mine = theta_acc[lo:hi]
+            pm = parent_acc[lo:hi] if parent_acc is not None else None
             if self.kde_events is not None and hasattr(fit, "packed"):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
-                Y = fit.packed.whiten(mine)
+                Y = fit.packed.whiten(mine, pm)
                 e0.record()
                 lp = fit.packed.logpdf_whitened(Y)
                 e1.record()
                 self.kde_events.append((e0, e1, hi - lo, fit.n))
+            elif pm is not None:
+                lp = fit.logpdf(mine, pm)
             else:
                 lp = fit.logpdf(mine)
             logpd = comm.all_gather_rows(

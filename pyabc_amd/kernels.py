@@ -220,10 +220,12 @@ def psd_whitening(cov):
 
 class WhitenedRows:
     """New rows prepared for the MFMA KDE pass: direct fp64 whitened rows
-    (exact underflow fixup) plus the f16 piece fragments of the B operand."""
+    (refine and exact fixup), the f16 piece fragments of the B operand and
+    each row's exponent offset (log2 units; 0, or the parent's term)."""
 
-    def __init__(self, Y, frags, M):
+    def __init__(self, Y, frags, M, row_off=None):
         self.Y, self.frags, self.M = Y, frags, M
+        self.row_off = row_off
         self.shape = (M, Y.shape[1])
 
 
@@ -266,16 +268,29 @@ class PackedPopulation:
         call(fn, ptr(X), ptr(w), n, d, ptr(mu), ptr(Us),
              ptr(self.P), self.npad, ptr(self.lw2max), ptr(ws), nat.stream())
 
-    def whiten(self, theta):
+    def whiten(self, theta, parent=None):
+        """Rows for :meth:`logpdf_whitened`.  ``parent`` (MFMA pass only,
+        optional): per row the index into this population its proposal was
+        resampled from; the row's exponents are then taken relative to the
+        parent's term (the density is the same; the folded pass rounds at
+        the row's own scale, kde_mfma.hip)."""
         theta = _contig(theta, F64)
         M = theta.shape[0]
         if self.precision == "mfma":
             Y = torch.zeros((M, self.D), dtype=F64, device=_dev())
             nb = nat.lib().abc_kde_mfma_new_bytes(M, self.d)
             B = torch.empty(max(nb, 16), dtype=torch.uint8, device=_dev())
-            call("abc_kde_pack_new_mfma", ptr(theta), M, self.d, ptr(self.mu),
-                 ptr(self.Us), ptr(self.gscale), ptr(Y), ptr(B), nat.stream())
-            return WhitenedRows(Y, B, M)
+            off = torch.empty(max(M, 1), dtype=F64, device=_dev())
+            par = None
+            if parent is not None:
+                par = _contig(parent, torch.int64)
+                if par.shape[0] != M:
+                    raise ValueError("parent: one index per row")
+            call("abc_kde_pack_new_mfma_rows", ptr(theta), M, self.d,
+                 ptr(self.mu), ptr(self.Us), ptr(self.gscale), ptr(self.P),
+                 self.npad, ptr(par) if par is not None else None, ptr(Y),
+                 ptr(B), ptr(off), nat.stream())
+            return WhitenedRows(Y, B, M, off[:M])
         dt = F32 if self.precision == "f32" else F64
         Y = torch.zeros((M, self.D), dtype=dt, device=_dev())
         fn = "abc_whiten_f32" if self.precision == "f32" else "abc_whiten_f64"
@@ -296,9 +311,11 @@ class PackedPopulation:
         if self.precision == "mfma":
             if not isinstance(Y, WhitenedRows):
                 raise TypeError("mfma KDE pass takes rows from whiten()")
-            call("abc_kde_logpdf_mfma", ptr(Y.frags), ptr(Y.Y), M, ptr(self.A),
-                 ptr(self.P), self.npad, self.d, ptr(self.lw2max),
-                 self.log_const, ptr(out), ptr(ws), wsb, nat.stream())
+            call("abc_kde_logpdf_mfma_rows", ptr(Y.frags), ptr(Y.Y),
+                 ptr(Y.row_off) if Y.row_off is not None else None, M,
+                 ptr(self.A), ptr(self.P), self.npad, self.d,
+                 ptr(self.lw2max), ptr(self.gscale), self.log_const,
+                 ptr(out), ptr(ws), wsb, nat.stream())
             return out
         fn = "abc_kde_logpdf_f32" if self.precision == "f32" else \
             "abc_kde_logpdf_f64"
@@ -306,8 +323,8 @@ class PackedPopulation:
              self.log_const, ptr(out), ptr(ws), wsb, nat.stream())
         return out
 
-    def logpdf(self, theta):
-        return self.logpdf_whitened(self.whiten(theta))
+    def logpdf(self, theta, parent=None):
+        return self.logpdf_whitened(self.whiten(theta, parent))
 
     def fixup_rows(self):
         """Rows the last pass of this population handed to the two-pass
@@ -318,6 +335,15 @@ class PackedPopulation:
         if ws is None:
             return 0
         return int(ws[off:off + 4].view(torch.int32).item())
+
+    def refined_rows(self):
+        """Rows the last MFMA pass re-evaluated with their own offset (sum
+        outside the folded scheme's routing range, kde_mfma.hip Route; the
+        fixup rows among them are counted by :meth:`fixup_rows`)."""
+        ws, off = getattr(self, "_fix_at", (None, 0))
+        if ws is None or self.precision != "mfma":
+            return 0
+        return int(ws[off + 4:off + 8].view(torch.int32).item())
 
 
 def importance_weights(logpd, prior=None, prior_const=1.0):

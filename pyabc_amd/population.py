@@ -1,6 +1,7 @@
 """Particles and populations (API of pyabc/population.py:1-286), plus the
 columnar device population the GPU sampler produces."""
 import concurrent.futures
+import logging
 import threading
 
 import numpy as np
@@ -10,6 +11,8 @@ import torch
 from . import kernels as K
 from .frames import DeviceFrame
 from .distance import DeviceStats
+
+logger = logging.getLogger("ABC.Population")
 
 
 class Particle:
@@ -283,10 +286,24 @@ class ColumnarPopulation:
         callable is called once per particle on host copies."""
         f = distance_to_ground_truth
         if isinstance(f, DistanceToGroundTruth) and \
-                hasattr(f.distance, "batch") and self.theta.is_cuda:
-            return self.update_distances_device(f.distance, f.t, f.x_0)
+                hasattr(f.distance, "batch") and torch.cuda.is_available():
+            if self.stats_T is None:
+                raise ValueError("statistics of this population were not "
+                                 "kept")
+            if self.stats_T.is_cuda:
+                return self.update_distances_device(f.distance, f.t, f.x_0)
+            # offloaded by History (to_host): the statistics go back to the
+            # device for the batch kernel (not O(N) host distance calls) and
+            # the distances come home with the other columns
+            d, _, _ = f.distance.batch(self.stats_T.cuda(), f.t, f.x_0,
+                                       np.inf, keys=self.stat_keys)
+            self.d = d.to(self.theta.device)
+            return self.d
         if self.stats_T is None:
             raise ValueError("statistics of this population were not kept")
+        if len(self) > 100000:
+            logger.warning("update_distances: %d per-particle host distance "
+                           "calls (no batch kernel for %r)", len(self), f)
         d = [float(f(s, p)) for s, p in
              zip(self._host_sum_stats(), self._host_parameters())]
         self.d = torch.as_tensor(np.asarray(d, dtype=np.float64),

@@ -593,6 +593,27 @@ def test_columnar_population_reference_api_gpu(pa):
     assert col.d.is_cuda
 
 
+def test_columnar_population_update_distances_offloaded(pa):
+    """After History offloads a population (to_host), update_distances with
+    the reference's DistanceToGroundTruth still runs the batch kernel (the
+    statistics go back to the device once; advisor r04) and equals the
+    on-device result bit for bit."""
+    from pyabc_amd.population import DistanceToGroundTruth
+    from tests.test_population_api import _pair
+    _, col = _pair(n=300, S=5, seed=4, device="cuda", normalize=True)
+    _, off = _pair(n=300, S=5, seed=4, device="cuda", normalize=True)
+    dist = pa.PNormDistance(p=2)
+    x_0 = {f"s{k}": 0.1 * k for k in range(5)}
+    dist.initialize(0, lambda: [], x_0)
+    f = DistanceToGroundTruth(dist, x_0, 0)
+    want = col.update_distances(f).cpu().numpy()
+    off.to_host()
+    assert not off.stats_T.is_cuda
+    got = off.update_distances(f)
+    assert not got.is_cuda          # with the other host columns
+    np.testing.assert_array_equal(got.numpy(), want)
+
+
 def test_single_round_recorded_stats_stride(pa):
     """A generation that closes in one sampling round hands out its recorded
     statistics as a column slice of the round's [S, B] buffer (row stride

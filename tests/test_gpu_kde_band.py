@@ -12,16 +12,18 @@ numpy oracle.  Each row's DERIVED bound is evaluated from its own fp64
 exponents e_ij = lw2_j - |y_i - y_j|^2 and the offset m_i the pass applies
 ("Accuracy of the folded accumulation"):
 
-  eps_i = ln2 [1.5 KL sum_j p_ij ulp32(|e_ij - m_i| + L_i) + D g^2 2^-12]
+  eps_i = ln2 [1.5 KL sum_j p_ij ulp32(|hi_ij| + |lo_ij|) + D g^2 2^-12]
           + 2^-23 + 6 2^-24
 
 p_ij = 2^(e_ij) / sum_j 2^(e_ij) (the row's term shares), KL the lo MFMAs
 folded on top of the exact hi products (1.5 ulp each: the measured maximum
 of one v_mfma_f32_32x32x16_f16 against one exact sum + one rounding,
-tools/probes/mfma_acc_round.hip), L_i the largest |lo| partial (a grid
-bound), D g^2 2^-12 the dropped r2.r3 / r3.r2 products, then v_exp_f32 and
-the fp32 tile sums.  The test requires measured <= eps_i on every row and
-eps_i <= 1e-5 / 1.5 on every row the pass keeps under its own offset.
+tools/probes/mfma_acc_round.hip), hi_ij the exact hi part of the pair's
+accumulator (relative to the row's offset m_i) and lo_ij = e_ij - m_i -
+hi_ij, so |hi| + |lo| bounds every partial the lo MFMAs round; D g^2 2^-12
+the dropped r2.r3 / r3.r2 products, then v_exp_f32 and the fp32 tile sums.
+The test requires measured <= eps_i on every row and eps_i <= 1e-5 / 1.5
+on every row.
 """
 import json
 import math
@@ -56,12 +58,18 @@ def _ulp32(x):
 def _row_stats(Yp, lw, Y, off, KL, D, g, chunk=128):
     """Per row: the largest exponent (relative to the global offset), the
     term-share entropy H (bits), log2 of the sum, and the derived bound
-    under the row offset ``off`` (log2 units)."""
+    under the row offset ``off`` (log2 units).  The folded accumulator of
+    pair (i, j) starts at the exact hi_ij = 2 y1_i.y1_j + aH_j + bH_i
+    (multiples of G = g^2; bH carries the offset) and each lo MFMA rounds
+    at most at |hi_ij| + |lo_ij|, lo_ij = e'_ij - hi_ij."""
+    G = g * g
     n2p = (Yp * Yp).sum(1)
-    ymax = float(n2p.max().sqrt())
+    y1p = g * torch.round(Yp / g)
+    aH = G * torch.round((lw - n2p) / G)
     out = {k: [] for k in ("emax", "H", "log2S", "bound")}
     for i0 in range(0, Y.shape[0], chunk):
         y = Y[i0:i0 + chunk]
+        m = off[i0:i0 + chunk]
         n2 = (y * y).sum(1)
         e = lw[None, :] - (n2[:, None] + n2p[None, :] - 2.0 * y @ Yp.T)
         emax = e.max(1).values
@@ -69,18 +77,31 @@ def _row_stats(Yp, lw, Y, off, KL, D, g, chunk=128):
         s = t.sum(1)
         p = t / s[:, None]
         H = -(p * torch.log2(torch.where(p > 0, p, torch.ones_like(p)))).sum(1)
-        # largest |lo| partial of a pair: the grid residuals |r| <= g/2 per
-        # coordinate against both rows, plus the a / b remainders (<= G)
-        L = g * math.sqrt(D) * (n2.sqrt() + ymax) + g * g
-        ep = (e - off[i0:i0 + chunk, None]).abs() + L[:, None]
-        u = (p * _ulp32(ep)).sum(1)
-        b = math.log(2) * (1.5 * KL * u + D * g * g * 2.0 ** -12) \
+        bH = G * torch.round((-n2 - m) / G)
+        hi = 2.0 * (g * torch.round(y / g)) @ y1p.T + aH[None, :] + bH[:, None]
+        lo = (e - m[:, None]) - hi
+        u = (p * _ulp32(hi.abs() + lo.abs())).sum(1)
+        b = math.log(2) * (1.5 * KL * u + D * G * 2.0 ** -12) \
             + 2.0 ** -23 + 6 * 2.0 ** -24
         out["emax"].append(emax)
         out["H"].append(H)
         out["log2S"].append(emax + torch.log2(s))
         out["bound"].append(b)
     return {k: torch.cat(v).cpu().numpy() for k, v in out.items()}
+
+
+def _pass_offsets(log2S, emax, m1, D):
+    """The offset each row ends up with in kde_mfma.hip: the pass-1 offset
+    m1 while the sum relative to it lies in the routing range (Route),
+    otherwise m1 + floor(log2 S') (S' in the normal range) or the max
+    pass's m1 + floor(max e')."""
+    lo = 2.0 ** -16 if D <= 8 else 2.0 ** -4
+    hi = 1.0 / lo
+    lS = log2S - m1
+    keep = (lS >= math.log2(lo)) & ((lS <= math.log2(hi)) | (m1 == 0))
+    normal = (lS > -100) & (lS < 100)
+    m2 = np.where(normal, m1 + np.floor(lS), m1 + np.floor(emax - m1))
+    return np.where(keep, m1, m2), ~keep
 
 
 def _band_rows(Yp, lw, n_want, rng, d):
@@ -135,13 +156,21 @@ def test_kde_folded_band_rows(K, d):
     Wr = pp.whiten(th)
     lp = pp.logpdf_whitened(Wr).cpu().numpy()
     n_fix = pp.fixup_rows()
+    n_ref = pp.refined_rows()
     lp64 = pp64.logpdf(th).cpu().numpy()
     err = np.abs(np.expm1(lp - lp64))
     KL = (5 * D + 4 + 15) // 16
     off = getattr(Wr, "row_off", None)
     if off is None:
         off = torch.zeros(len(Yc), dtype=torch.float64, device="cuda")
-    st = _row_stats(Yp, lw, Wr.Y, off, KL, D, g)
+    st0 = _row_stats(Yp, lw, Wr.Y, off, KL, D, g)
+    m_fin, routed = _pass_offsets(st0["log2S"], st0["emax"],
+                                  off.cpu().numpy(), D)
+    st = _row_stats(Yp, lw, Wr.Y, torch.as_tensor(m_fin, device="cuda"), KL,
+                    D, g)
+    # the same rows under the global offset (rounds 1-4: no refine above
+    # 2^-32), for the record
+    st_glob = _row_stats(Yp, lw, Wr.Y, torch.zeros_like(off), KL, D, g)
     # sample against the numpy oracle
     pick = rng.choice(len(Yc), 256, replace=False)
     Xw = X @ U
@@ -151,6 +180,8 @@ def test_kde_folded_band_rows(K, d):
     err64_ref = np.abs(np.expm1(lp64[pick] - lp_ref))
     stats = dict(
         d=d, N=N, rows=int(len(Yc)), grid_g=g, KL=KL, fixup_rows=n_fix,
+        refined_rows=n_ref, routed_predicted=int(routed.sum()),
+        bound_max_global_offset=float(st_glob["bound"].max()),
         emax_range=[float(st["emax"].min()), float(st["emax"].max())],
         H_max=float(st["H"].max()),
         max_rel_err_vs_f64=float(err.max()),
@@ -171,6 +202,9 @@ def test_kde_folded_band_rows(K, d):
             json.dump(old + [stats], f, indent=1)
     print(json.dumps(stats))
     assert len(Yc) >= 10000
+    # the pass routes on its own (folded) sums: rows at the routing bound
+    # may fall either way
+    assert abs(n_ref - int(routed.sum())) <= max(2, len(Yc) // 1000), stats
     assert err64_ref.max() < 1e-11, stats
     assert err.max() <= BAR, stats
     assert err_ref.max() <= BAR, stats

@@ -333,3 +333,9 @@ def test_fused_path_only_for_the_mirrored_simulate():
     assert mirrors_simulate(Both(m.A_host, m.sigma))
     assert not mirrors_simulate(Stale(m.A_host, m.sigma))
     assert not mirrors_simulate(object())
+    # simulate replaced on the instance: its distances must come from it
+    inst = LinearGaussianModel.benchmark(2, 3)
+    inst.simulate = lambda theta, seed, sid, offset: None
+    assert not mirrors_simulate(inst)
+    inst.simulate_distance = lambda *a: None   # both from the instance
+    assert mirrors_simulate(inst)

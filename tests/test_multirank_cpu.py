@@ -135,6 +135,9 @@ def test_rank_slice_comm_matches_identical_ranks():
     g = c.all_gather_rows(rows, [6, 6, 4, 0])
     assert g.shape == (16, 2)
     assert torch.equal(g[6:12], rows) and torch.equal(g[12:], rows[:4])
+    # a rank holding no rows still returns sum(sizes) rows (advisor r04)
+    g0 = RankSliceComm(4).all_gather_rows(rows[:0], [0, 3, 2, 0])
+    assert g0.shape == (5, 2)
     # the engine's selection and segment gather run on it unchanged
     takes, closing = selection_plan([[5] * 4, [5] * 4], [[2] * 4, [3] * 4], 13)
     counts = [[t[s] for t in takes] for s in range(4)]

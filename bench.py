@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 from pyabc_amd import kernels as K  # noqa: E402
 from pyabc_amd.batch_models import LinearGaussianModel  # noqa: E402
 from pyabc_amd.distributed import Comm  # noqa: E402
-from pyabc_amd.engine import GenerationEngine, DeviceMVNFit  # noqa: E402
+from pyabc_amd.engine import (GenerationEngine, DeviceMVNFit,  # noqa: E402
+                              next_generation_inputs)
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (MI355X_MICROARCH.md)
 MFMA16_PEAK_TFLOPS = 2500.0  # dense f16 / bf16 MFMA (no sparsity)
@@ -278,7 +279,8 @@ def rank_slice_report(args, comm, N, d, S, ms_step, stages, kde_ms,
     kde_avg = sum(kde_ms) / max(len(kde_ms), 1)
     scaling = ("sample_generation", "engine_kde")
     fixed = {k: v for k, v in avg.items()
-             if k in ("cdf", "normalise", "quantile", "fit_pack")}
+             if k in ("cdf", "normalise", "quantile", "fit_pack",
+                      "next_inputs")}
     pred_ms = ms_step + xgmi_ms
     return {
         "kind": "rank-slice (predicted, unmeasured on multi-GPU hardware)",
@@ -384,17 +386,17 @@ def main():
             state["k"] += 1
         tm, t0 = {}, time.perf_counter()
         if args.rank_slice:
-            state["fit"].cdf          # the resampling CDF + its bucket table
+            state["fit"].cdf          # the side stream's CDF, if still running
             t0 = mark(tm, "cdf", t0)
         res = eng.sample_generation(t, N, state["fit"], x0, fw, state["eps"])
         t0 = mark(tm, "sample_generation", t0)
         th, dd, ww, n_eval, _ = eng.gather_population(res)
         t0 = mark(tm, "normalise", t0)
-        state["eps"] = float(K.weighted_quantile(dd, ww, 0.5,
-                                                 comm=comm)[0].item())
-        t0 = mark(tm, "quantile", t0)
-        state["fit"] = DeviceMVNFit(th, ww)
-        t0 = mark(tm, "fit_pack", t0)
+        # epsilon, fit + pack and the resampling CDF of the next generation,
+        # overlapped (engine.next_generation_inputs)
+        state["eps"], state["fit"] = next_generation_inputs(th, dd, ww, 0.5,
+                                                            comm=comm)
+        t0 = mark(tm, "next_inputs", t0)
         if args.rank_slice:
             tm.update({f"engine_{k}": v * 1e3 for k, v in eng.timers.items()})
             stages.append(tm)

@@ -65,8 +65,10 @@ class DeviceMVNFit:
             sw2 = float((w.double() ** 2).sum().item())
             mu = x0
         else:
-            mom = (moments if moments is not None
-                   else K.weighted_moments(X, w)).cpu().numpy()
+            if moments is None:
+                moments = K.weighted_moments(X, w)
+            mom = moments.cpu().numpy() if torch.is_tensor(moments) \
+                else np.asarray(moments, dtype=np.float64)
             sw, sw2 = mom[0], mom[1]
             mu = mom[2:2 + d]
             fact = sw - sw2 / sw
@@ -89,13 +91,22 @@ class DeviceMVNFit:
                                          precision)
         self._cdf = None
         self._tab = None
+        self._cdf_ev = None
 
     @property
     def cdf(self):
         if self._cdf is None:
             self._cdf = K.resample_cdf(self.w)
             self._tab = K.cdf_index(self._cdf)
+        if self._cdf_ev is not None:   # computed on a side stream
+            torch.cuda.current_stream().wait_event(self._cdf_ev)
+            self._cdf_ev = None
         return self._cdf
+
+    def adopt_cdf(self, cdf, tab, event):
+        """The resampling CDF and its bucket table, computed on another
+        stream; ``event`` marks their completion (waited at first use)."""
+        self._cdf, self._tab, self._cdf_ev = cdf, tab, event
 
     def logpdf(self, theta, parent=None):
         """log transition density; ``parent``: per row the population index
@@ -109,6 +120,48 @@ class DeviceMVNFit:
         cdf = self.cdf
         return K.propose_philox(self.X, cdf, self.A, lo, scale, seed, sid,
                                 offset, B, tab=self._tab)
+
+
+_SIDE = {}
+
+
+def _side_stream():
+    dev = torch.cuda.current_device()
+    if dev not in _SIDE:
+        _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return _SIDE[dev]
+
+
+def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
+                           bandwidth_selector=None, precision="mfma"):
+    """QuantileEpsilon(alpha)'s next epsilon and the MultivariateNormal fit
+    of the new population (``smc.py:942-1061``: epsilon update, then
+    ``_fit_transitions``), with the stages that do not depend on each other
+    overlapped: the resampling CDF (latency-bound binade walks) runs on a
+    side stream while the main stream computes the weighted moments and the
+    quantile, both read back by ONE host wait; then the host d x d finish
+    and the KDE pack.  Every rank holds the whole population and computes
+    the same bits (no collective).  Returns (eps, fit)."""
+    main = torch.cuda.current_stream()
+    ev = torch.cuda.Event()
+    ev.record(main)
+    side = _side_stream()
+    with torch.cuda.stream(side):
+        side.wait_event(ev)
+        cdf = K.resample_cdf(w)
+        tab = K.cdf_index(cdf)
+        cdf_ev = torch.cuda.Event()
+        cdf_ev.record(side)
+    # allocated on the side stream, read on the main one
+    cdf.record_stream(main)
+    tab.record_stream(main)
+    mom = K.weighted_moments(theta, w)
+    q = K.weighted_quantile(d, w, alpha, comm=comm)
+    host = torch.cat([mom, q[:1]]).cpu().numpy()            # one host wait
+    fit = DeviceMVNFit(theta, w, scaling, bandwidth_selector, precision,
+                       moments=host[:-1])
+    fit.adopt_cdf(cdf, tab, cdf_ev)
+    return float(host[-1]), fit
 
 
 def selection_plan(nvs, nas, n):

@@ -421,20 +421,24 @@ _WQ_SEQ = [0, 1, 2, 3] + [s for p in range(8) for s in (10 + p, 20 + p)] \
     + [30, 31, 33, 32]
 
 
-def weighted_quantile(d, w, alpha, comm=None):
+def weighted_quantile(d, w, alpha, comm=None, shard=False):
     """Device [eps, p_k, cs_{k-1}, w_k] for interp(alpha, cs - w/2, sort d).
 
-    With ``comm`` over several ranks (every rank holding the same global
-    population) each rank histograms only its row_range of (d, w) and the
-    integer histograms / key bounds are all-reduced between the radix passes
-    (SURVEY 8(e)); the result is bit-identical to one rank's."""
+    With ``comm`` over several ranks every rank holds the same global
+    population.  By default each rank evaluates the quantile on its own
+    copy: no exchange, the same bits on every rank (the sharded protocol's
+    13 collectives cost more than the N/R histogram work they split: 13 x
+    ~25 us against 0.12 ms for the whole N = 1e6 select, DESIGN.md section
+    5).  ``shard=True``: each rank histograms only its row_range of (d, w)
+    and the integer histograms / key bounds are all-reduced between the
+    radix passes; bit-identical to one rank's."""
     n = d.numel()
     out = torch.empty(4, dtype=F64, device=_dev())
     wsb = nat.lib().abc_wquantile_workspace_bytes()
     ws = WS.get(wsb, "wq")
     d = _contig(d, F64)
     w = None if w is None else _contig(w, F64)
-    if comm is None or not comm.active:
+    if comm is None or not comm.active or not shard:
         call("abc_wquantile_f64", ptr(d), ptr(w), n, float(alpha), ptr(out),
              ptr(ws), wsb, nat.stream())
         return out

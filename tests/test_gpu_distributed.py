@@ -59,9 +59,14 @@ def _generation(comm, n, min_batch, record):
                                 record=record)
     th, dd, ww, n_eval, _ = eng.gather_population(res)
     eps1 = float(K.weighted_quantile(dd, ww, 0.5, comm=comm)[0].item())
+    # the sharded protocol (histograms all-reduced between passes) gives
+    # the same bits as each rank's own select
+    assert float(K.weighted_quantile(dd, ww, 0.5, comm=comm, shard=True)[0]
+                 .item()) == eps1
     # heavily tied distances (the sharded tie-block words, exchange step 33)
     dt = torch.round(dd * 2.0) / 2.0
-    eps_ties = [float(K.weighted_quantile(dt, wq, a, comm=comm)[0].item())
+    eps_ties = [float(K.weighted_quantile(dt, wq, a, comm=comm,
+                                          shard=True)[0].item())
                 for wq in (ww, None) for a in (0.3, 0.5, 0.7, 0.9)]
     fit1 = DeviceMVNFit(th, ww)
     # exact-inference generation: stochastic acceptance with u keyed by the

@@ -603,7 +603,7 @@ class GenerationEngine:
                                         [rd["nas"] for rd in rounds], n)
         lasts = []
         th_loc, d_loc, st_loc, rec_loc = [], [], [], []
-        aw_loc, rth_loc, rd_loc, ra_loc = [], [], [], []
+        aw_loc, rth_loc, rd_loc, ra_loc, rp_loc = [], [], [], [], []
         stochastic = isinstance(acceptance, StochasticAcceptance)
         n_guard = 0
         n_eval_loc = 0
@@ -637,6 +637,8 @@ class GenerationEngine:
                     rec_loc.append(rd["stats"][:, :last])
                 if record_particles:
                     rth_loc.append(rd["theta"][:last])
+                    if use_parent:
+                        rp_loc.append(rd["pid"][:last])
                     rd_loc.append(rd["d"][:last])
                     ra_loc.append(rd["acc"][:last].to(F64) if rd["acc"]
                                   is not None else torch.ones(
@@ -669,9 +671,12 @@ class GenerationEngine:
             last_counts = comm.all_gather_int_lists(lasts)
         if record:
             rec = self._gather_cols(rec_loc, last_counts)
-        rec_theta = rec_d = rec_acc = None
+        rec_theta = rec_d = rec_acc = rec_parent = None
         if record_particles:
             rec_theta = self._gather(rth_loc, (self.d,), last_counts)
+            if use_parent:
+                rec_parent = self._gather(rp_loc, (), last_counts).to(
+                    torch.int64)
             rec_d = self._gather(rd_loc, (), last_counts)
             rec_acc = self._gather(ra_loc, (), last_counts)
         # host time (the device work of the selection overlaps the KDE pass)
@@ -711,7 +716,8 @@ class GenerationEngine:
         return GenerationResult(
             ok=True, theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
             n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec,
-            accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc)
+            accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc,
+            rec_parent=rec_parent)
 
     def _gather(self, pieces, row_shape, counts):
         return gather_segments(self.comm, pieces, row_shape, counts, self.dev)

@@ -226,7 +226,8 @@ class GPUBatchSampler(Sampler):
                                  res.stats_T, keys)
         recp = None
         if getattr(res, "rec_theta", None) is not None:
-            recp = (res.rec_theta, res.rec_d, res.rec_acc)
+            recp = (res.rec_theta, res.rec_d, res.rec_acc,
+                    getattr(res, "rec_parent", None))
         return BatchSample(pop, rec, record, rec_particles=recp)
 
     def _not_ok(self, res, record):

@@ -457,16 +457,30 @@ class ABCSMC:
         """get_all_records of a device generation (smc.py:990-1017): the
         previous and current transition log-densities of every recorded
         evaluation by the device KDE pass (or the prior's, at t - 1 = 0)."""
-        theta, d, acc = sample.rec_particles
+        theta, d, acc = sample.rec_particles[:3]
+        parent = sample.rec_particles[3] if len(sample.rec_particles) > 3 \
+            else None
         m = int(self.max_nr_recorded_particles) if np.isfinite(
             self.max_nr_recorded_particles) else theta.shape[0]
         theta, d, acc = theta[:m], d[:m], acc[:m]
+        # each record's "parent" in a transition's population (the MFMA KDE
+        # pass evaluates the row relative to that particle's term; any index
+        # gives the same density): the previous population -- the particle
+        # its proposal was resampled from -- and the new one, which holds
+        # the accepted records in order, so an accepted record is particle
+        # cumsum(acc) - 1 there (rejected: none)
+        par_prev = par_cur = None
+        if parent is not None:
+            par_prev = parent[:m]
+            a = acc > 0
+            par_cur = torch.where(a, torch.cumsum(a.to(torch.int64), 0) - 1,
+                                  torch.full_like(par_prev, -1))
         return DeviceRecords(d, self._log_transition_pd(t - 1, prev_transitions,
-                                                        theta),
+                                                        theta, par_prev),
                              self._log_transition_pd(t, self.transitions,
-                                                     theta), acc)
+                                                     theta, par_cur), acc)
 
-    def _log_transition_pd(self, t, transitions, theta):
+    def _log_transition_pd(self, t, transitions, theta, parent=None):
         if t == 0:
             # prior density: constant on the (uniform-box) support, where
             # every recorded proposal lies (smc.py:737-749)
@@ -475,7 +489,7 @@ class ABCSMC:
             pd0 = self._create_prior_pdf()(0, par)
             return torch.full((theta.shape[0],), float(np.log(pd0)),
                               dtype=theta.dtype, device=theta.device)
-        return transitions[0].logpdf_device(theta)
+        return transitions[0].logpdf_device(theta, parent)
 
     def _adapt_population_size(self, t):
         if t == 0:

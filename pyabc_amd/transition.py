@@ -204,8 +204,11 @@ class MultivariateNormalTransition(Transition):
             return float(dens[0])
         return dens
 
-    def logpdf_device(self, theta):
-        return self._fit.logpdf(theta)
+    def logpdf_device(self, theta, parent=None):
+        """log density at device rows; ``parent`` (optional): per row an
+        index into the fitted population (kde_mfma.hip per-row offsets;
+        the density does not depend on it)."""
+        return self._fit.logpdf(theta, parent)
 
 
 class LocalTransition(Transition):
@@ -335,7 +338,7 @@ class LocalTransition(Transition):
             return float(dens[0])
         return dens
 
-    def logpdf_device(self, theta):
+    def logpdf_device(self, theta, parent=None):
         return K.local_logpdf(theta, self._Xd, self._wd, self._invs,
                               self._dets, self.kde_precision)
 

@@ -26,6 +26,9 @@
 //       incl. 16 TRANS)
 //   13: d = 20, f16 folded, the PMC's mix -- 9 MFMA, 16 exp, 28 other VALU
 //       (profiles/r04_kde_d20_pmc.json: 44.2 VALU incl. 16 TRANS)
+//   14-17: mix 13 plus the d = 20 kernel's memory path step by step (14 five
+//       ds_read_b128 per step, 15 + a barrier per 4 steps, 16 + the LDS-DMA
+//       refill of 18 fragments per barrier, 17 as 14 with four reads)
 //   5-7: mix 3 plus the headline kernel's memory path (mix_mem_kernel):
 //      5 two ds_read_b128 per step, 6 + a block barrier every 2 steps,
 //      7 + the LDS-DMA refill of the other buffer before each barrier;
@@ -85,20 +88,20 @@ __global__ __launch_bounds__(256) void mix_kernel(float* out, int iters) {
 // the LDS-DMA refill of the other buffer (8 KB per block from an L2-resident
 // source, waited with vmcnt(0) before the barrier) -- the per-64-row-chunk
 // pattern of kde_mfma_lds2g_kernel.
-template <int NM, int NE, int NA, int DSR, int BAR, int DMA>
+template <int NM, int NE, int NA, int DSR, int BAR, int DMA, int NF = 8>
 __global__ __launch_bounds__(256) void mix_mem_kernel(float* out, int iters,
                                                       const bf16x8* __restrict__ src) {
-  __shared__ bf16x8 As[2][8][64];
+  __shared__ bf16x8 As[2][NF][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
-  for (int f = wave; f < 16; f += 4) {
+  for (int f = wave; f < 2 * NF; f += 4) {
     bf16x8 x;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       h ^= h >> 13; h *= 0x5bd1e995u;
       x[e] = static_cast<short>(0x3C00 | (h & 0x7F));
     }
-    As[f >> 3][f & 7][lane] = x;
+    As[f / NF][f % NF][lane] = x;
   }
   bf16x8 b;
 #pragma unroll
@@ -119,8 +122,8 @@ __global__ __launch_bounds__(256) void mix_mem_kernel(float* out, int iters,
       if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (DMA) {
-        const bf16x8* g = src + (i & 1023) * 8 * 64;
-        for (int f = wave; f < 8; f += 4)
+        const bf16x8* g = src + (i & 1023) * NF * 64;  // src: 1024 x 32 KiB
+        for (int f = wave; f < NF; f += 4)
           __builtin_amdgcn_global_load_lds(
               g + f * 64 + lane,
               (__attribute__((address_space(3))) void*)&As[buf ^ 1][f][0], 16, 0, 0);
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void mix_mem_kernel(float* out, int iters,
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-      if (m < DSR) a = As[buf][(i * DSR + m + 1) & 7][lane];
+      if (m < DSR) a = As[buf][(i * DSR + m + 1) % NF][lane];
 #pragma unroll
       for (int k = m * NE / NM; k < (m + 1) * NE / NM; ++k) ABC_EXP(v[k & 15])
 #pragma unroll
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void mix_mem_kernel(float* out, int iters,
   out[blockIdx.x * 256 + threadIdx.x] = t;
 }
 
-template <int NM, int NE, int NA, int DSR, int BAR, int DMA>
+template <int NM, int NE, int NA, int DSR, int BAR, int DMA, int NF = 8>
 double time_mem_mix(int waves_per_simd, int iters, int cus, float* out,
                     const bf16x8* src) {
   const int blocks = cus * waves_per_simd;
@@ -154,7 +157,7 @@ double time_mem_mix(int waves_per_simd, int iters, int cus, float* out,
   float best = 1e30f;
   for (int rep = 0; rep < 4; ++rep) {
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL((mix_mem_kernel<NM, NE, NA, DSR, BAR, DMA>), dim3(blocks),
+    hipLaunchKernelGGL((mix_mem_kernel<NM, NE, NA, DSR, BAR, DMA, NF>), dim3(blocks),
                        dim3(256), 0, 0, out, iters, src);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
@@ -206,12 +209,15 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
   float* out = nullptr;
   if (hipMalloc(&out, static_cast<size_t>(cus) * 8 * 256 * 4) != hipSuccess)
     return -1.0;
-  bf16x8* src = nullptr;  // DMA source: 1024 chunks of 8 KB (8 MB, L2/MALL)
-  if (hipMalloc(&src, size_t{1024} * 8 * 64 * 16) != hipSuccess) {
+  // DMA source: 1024 chunks of up to 32 fragments (32 MB; the probes read
+  // NF <= 18 KiB of each chunk)
+  bf16x8* src = nullptr;
+  const size_t src_bytes = size_t{1024} * 32 * 64 * 16;
+  if (hipMalloc(&src, src_bytes) != hipSuccess) {
     (void)hipFree(out);
     return -1.0;
   }
-  (void)hipMemset(src, 0x3C, size_t{1024} * 8 * 64 * 16);
+  (void)hipMemset(src, 0x3C, src_bytes);
   double ns = -1.0;
   switch (variant) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
@@ -228,6 +234,14 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 11: ns = time_mem_mix<4, 16, 19, 2, 8, 1>(waves_per_simd, iters, cus, out, src); break;
     case 12: ns = time_mix<4, 16, 22>(waves_per_simd, iters, cus, out); break;
     case 13: ns = time_mix<9, 16, 28>(waves_per_simd, iters, cus, out); break;
+    // the d = 20 ladder (mix 13 plus the folded LDS pass's memory path at
+    // IB = 2: 4.5 ds_read_b128 per (tile, i-tile) step -- 4 and 5
+    // alternating is not expressible, 5 bounds it --, a barrier per 2-tile
+    // stage = 4 steps, 18 KiB of LDS-DMA refill per stage)
+    case 14: ns = time_mem_mix<9, 16, 28, 5, 0, 0, 18>(waves_per_simd, iters, cus, out, src); break;
+    case 15: ns = time_mem_mix<9, 16, 28, 5, 4, 0, 18>(waves_per_simd, iters, cus, out, src); break;
+    case 16: ns = time_mem_mix<9, 16, 28, 5, 4, 1, 18>(waves_per_simd, iters, cus, out, src); break;
+    case 17: ns = time_mem_mix<9, 16, 28, 4, 0, 0, 18>(waves_per_simd, iters, cus, out, src); break;
     default: break;
   }
   (void)hipFree(src);

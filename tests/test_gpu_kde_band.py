@@ -95,7 +95,7 @@ def _pass_offsets(log2S, emax, m1, D):
     m1 while the sum relative to it lies in the routing range (Route),
     otherwise m1 + floor(log2 S') (S' in the normal range) or the max
     pass's m1 + floor(max e')."""
-    lo = 2.0 ** -16 if D <= 8 else 2.0 ** -4
+    lo = 2.0 ** -12 if D <= 8 else 2.0 ** -4
     hi = 1.0 / lo
     lS = log2S - m1
     keep = (lS >= math.log2(lo)) & ((lS <= math.log2(hi)) | (m1 == 0))

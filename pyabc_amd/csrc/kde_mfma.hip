@@ -1503,15 +1503,18 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 // and any row the second pass still cannot resolve, take the exact fp64
 // fixup.  lo: the folded scheme's routing bound: a row
 // whose sum stays within [lo, 1/lo] of its offset keeps the derived bound
-// under 1e-5 / 1.5 -- 2^-12 where KL <= 3 lo MFMAs fold (d <= 8; 2^-16
-// measured a 6.76e-6 bound on rows at e = -16, tests/test_gpu_kde_band.py),
-// 2^-4 where KL = 4 ... 8 (8 < d <= 24); hi = 1 / lo for rows with an offset
+// under 1e-5 / 1.5 -- 2^-24 where KL <= 2 lo MFMAs fold (d <= 4), 2^-12
+// where KL = 3 (d = 6, 8; 2^-16 measured a 6.76e-6 bound on rows at
+// e = -16, tests/test_gpu_kde_band.py), 2^-4 where KL = 4 ... 8
+// (8 < d <= 24); hi = 1 / lo for rows with an offset
 // (the parent's term was not the dominant one).  The split and bf16 schemes
 // keep the 2^-32 of rounds 1-4.
 template <int D>
 struct Route {
   static constexpr bool kFold = Mk<D>::SCH == 2;
-  static constexpr double lo = !kFold ? 0x1p-32 : (Mk<D>::KL <= 3 ? 0x1p-12 : 0x1p-4);
+  static constexpr double lo =
+      !kFold ? 0x1p-32
+             : (Mk<D>::KL <= 2 ? 0x1p-24 : (Mk<D>::KL <= 3 ? 0x1p-12 : 0x1p-4));
   static constexpr double hi = !kFold ? 0x1p+100 : 1.0 / lo;
 };
 constexpr double kLn2d = 0.6931471805599453;

@@ -1,5 +1,8 @@
-"""Full-size parity of the default KDE pass (exact-grid bf16 MFMA) at the
-configurations the headline numbers are quoted on.
+"""Full-size parity of the default KDE pass (exact-grid f16-piece MFMA,
+folded accumulation, KT = 4 MFMAs per tile at d = 8 and 9 at d = 20) at the
+configurations the headline numbers are quoted on.  The production rows
+carry their parents (the engine's resample indices), so the pass evaluates
+each relative to its parent's term (kde_mfma.hip per-row offsets).
 
 Reference: MultivariateNormalTransition.pdf (pyabc/transition/
 multivariatenormal.py:102-125) via smc.py:722-733.  Tolerance (BASELINE

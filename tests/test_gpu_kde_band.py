@@ -6,7 +6,7 @@ old 2^-32 fixup threshold, where each lo MFMA of the folded chain rounds at
 Reference: MultivariateNormalTransition.pdf (pyabc/transition/
 multivariatenormal.py:102-125, the exact sum the pass must match to 1e-5).
 
-Per d in {8, 20, 24}: >= 1e4 constructed rows against the fp64 HIP pass
+Per d in {4, 8, 20, 24}: >= 1e4 constructed rows against the fp64 HIP pass
 (pinned at 1e-12 on the reference's goldens) and 256 of them against the
 numpy oracle.  Each row's DERIVED bound is evaluated from its own fp64
 exponents e_ij = lw2_j - |y_i - y_j|^2 and the offset m_i the pass applies
@@ -95,7 +95,8 @@ def _pass_offsets(log2S, emax, m1, D):
     m1 while the sum relative to it lies in the routing range (Route),
     otherwise m1 + floor(log2 S') (S' in the normal range) or the max
     pass's m1 + floor(max e')."""
-    lo = 2.0 ** -12 if D <= 8 else 2.0 ** -4
+    KL = (5 * D + 4 + 15) // 16
+    lo = 2.0 ** -24 if KL <= 2 else (2.0 ** -12 if KL <= 3 else 2.0 ** -4)
     hi = 1.0 / lo
     lS = log2S - m1
     keep = (lS >= math.log2(lo)) & ((lS <= math.log2(hi)) | (m1 == 0))
@@ -130,7 +131,7 @@ def _band_rows(Yp, lw, n_want, rng, d):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("d", [8, 20, 24])
+@pytest.mark.parametrize("d", [4, 8, 20, 24])
 def test_kde_folded_band_rows(K, d):
     rng = np.random.default_rng(500 + d)
     N, n_rows = 65536, 12000

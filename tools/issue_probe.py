@@ -19,7 +19,24 @@ MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
          8: "mix 3 + 2 ds_read_b128 per step + barrier every 4 steps",
          9: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 4 steps",
          10: "mix 3 + 2 ds_read_b128 per step + barrier every 8 steps",
-         11: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 8 steps"}
+         11: "mix 3 + 2 ds_read_b128 + barrier + LDS-DMA refill every 8 steps",
+         12: "d<=8 folded f16, PMC mix: 4 MFMA, 16 v_exp_f32, 22 v_add_f32",
+         13: "d=20 folded f16, PMC mix: 9 MFMA, 16 v_exp_f32, 28 v_add_f32",
+         14: "mix 13 + 5 ds_read_b128 per step",
+         15: "mix 13 + 5 ds_read_b128 per step + barrier every 4 steps",
+         16: "mix 13 + 5 ds_read_b128 + barrier + 18-KiB LDS-DMA refill every 4 steps",
+         17: "mix 13 + 4 ds_read_b128 per step"}
+
+
+def parse():
+    """--variants 13,14 --waves 2 (defaults: every mix, 1-4 waves)"""
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default=None)
+    ap.add_argument("--waves", default="1,2,3,4")
+    a = ap.parse_args()
+    vs = [int(v) for v in a.variants.split(",")] if a.variants else list(MIXES)
+    return vs, [int(w) for w in a.waves.split(",")]
 
 
 def load():
@@ -33,9 +50,11 @@ def main():
     import torch
     torch.cuda.init()
     lib = load()
+    variants, waves = parse()
     out = []
-    for v, desc in MIXES.items():
-        for wps in (1, 2, 3, 4):
+    for v in variants:
+        desc = MIXES[v]
+        for wps in waves:
             ns = lib.abc_probe_kde_mix(v, wps, 100000)
             out.append(dict(variant=v, mix=desc, waves_per_simd=wps,
                             ns_per_step_per_simd=ns))

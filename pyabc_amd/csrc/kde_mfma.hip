@@ -109,10 +109,14 @@ struct Mk {
   static constexpr int KL = F16 ? (5 * D + 4 + 15) / 16 : (7 * D + 4 + 15) / 16;
   static constexpr int KT = KH + KL;
   static constexpr int LO0 = 16 * KH;  // first lo slot
-  static constexpr int IB = D <= 8 ? 3 : (D <= 24 ? 2 : 1);  // i-tiles/wave
+  // i-tiles per wave: 3 up to d = 24 (round 5 at d > 8: each LDS fragment
+  // read feeds three MFMAs instead of two -- the d = 20 probe ladder,
+  // profiles/r05_issue_probe.json, prices a ds_read_b128 at ~9 ns per tile
+  // step); 1 for the split scheme above d = 24
+  static constexpr int IB = D <= 24 ? 3 : 1;
   // row padding unit in i-tiles per wave: every IB the launch may pick
-  // (1, 2, 3 at D <= 8) divides it
-  static constexpr int PADIB = D <= 8 ? 6 : IB;
+  // (1, 2, 3) divides it
+  static constexpr int PADIB = D <= 24 ? 6 : IB;
 };
 
 __device__ inline unsigned short bf16_rne(float x) {
@@ -1429,9 +1433,11 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   const dim3 block(64 * kWaves);
   const int split = p.smajor ? -p.split : p.split;
   if constexpr (D > 8 && Mk<D>::SCH == 2) {
-    // the folded f16 scheme: the LDS-DMA folded pass (ABC_KDE_MFMA_LDS2 1
-    // or 2), or the register kernel (0); rows bit-identical
-    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
+    // the folded f16 scheme: the LDS-DMA folded pass, pipelined
+    // (ABC_KDE_MFMA_LDS2 1 or 2: round 4's default at IB = 2) or not (3:
+    // the default at IB = 3, one accumulator set), or the register kernel
+    // (0); rows bit-identical
+    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, IB == 3 ? 3 : 2);
     if (lds2 == 3) {  // no in-wave pipelining
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
@@ -1700,7 +1706,9 @@ template <int D, int MODE>
 void launch_list(const bf16x8* Bbuf, const int* count, int64_t ld,
                  const bf16x8* Afr, int64_t npad, int nseg, int jseg,
                  double* partial, hipStream_t st) {
-  constexpr int IB = Mk<D>::IB;
+  // the register kernel holds IB x KT B fragments and two A tiles: IB = 2
+  // above d = 8 keeps it in registers
+  constexpr int IB = D <= 8 ? Mk<D>::IB : (Mk<D>::IB > 2 ? 2 : Mk<D>::IB);
   const int rbs = kListBlocks / nseg > 0 ? kListBlocks / nseg : 1;
   hipLaunchKernelGGL((kde_mfma_list_kernel<Mk<D>::KH, Mk<D>::KL, IB, (D <= 8),
                                            Mk<D>::SCH, MODE>),

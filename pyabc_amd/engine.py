@@ -714,7 +714,8 @@ class GenerationEngine:
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm
         return GenerationResult(
-            ok=True, theta=theta_acc, d=d_acc, w=w, logpd=logpd, n_eval=n_eval,
+            ok=True, theta=theta_acc, parent=parent_acc, d=d_acc, w=w,
+            logpd=logpd, n_eval=n_eval,
             n_guard=n_guard, stats_T=stats_acc, rec_stats_T=rec,
             accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc,
             rec_parent=rec_parent)

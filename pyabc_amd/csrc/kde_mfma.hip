@@ -593,7 +593,13 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     whiten_row<D>(theta, i, d, mu, Us, y);
 #pragma unroll
     for (int k = 0; k < D; ++k) Ydir[i * D + k] = y[k];
-    if (parent) {
+    // parents only where KL >= 4 lo MFMAs fold (d > 8): at d <= 8 the
+    // global offset already keeps every bench row within the routing range
+    // (log2 S in [-5.1, -0.9] at N = 1e6) while the parent's term is not
+    // the dominant one (the sum is 2^6.8 times it at the median), so the
+    // offset would only push rows out of range (tools/kde_offsets.py,
+    // gpurun_out/r05d)
+    if (parent && Mk<D>::SCH == 2 && Mk<D>::KL >= 4) {
       const int64_t p = parent[i];
       if (p >= 0 && p < npad) m = parent_offset<D>(y, P, p);
     }
@@ -1434,10 +1440,12 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
   const int split = p.smajor ? -p.split : p.split;
   if constexpr (D > 8 && Mk<D>::SCH == 2) {
     // the folded f16 scheme: the LDS-DMA folded pass, pipelined
-    // (ABC_KDE_MFMA_LDS2 1 or 2: round 4's default at IB = 2) or not (3:
-    // the default at IB = 3, one accumulator set), or the register kernel
-    // (0); rows bit-identical
-    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, IB == 3 ? 3 : 2);
+    // (ABC_KDE_MFMA_LDS2 1 or 2, the default) or not (3: one accumulator
+    // set), or the register kernel (0); rows bit-identical.  d = 20,
+    // N = M = 1e6, one process (gpurun_out/r05d): IB = 2 pipelined (round
+    // 4) 210.3 / 210.4 ms, IB = 3 unpipelined 215.9 ms, IB = 3 pipelined
+    // 198.9 ms
+    const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
     if (lds2 == 3) {  // no in-wave pipelining
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
@@ -1498,7 +1506,9 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 
 // ---- refine: flagged rows re-evaluated with their own offset (round 5) -----
 // Pass 1 evaluates every row relative to its offset m_i (0, or the parent's
-// term).  Rows whose sum S_i leaves [lo, hi] are refined on the matrix cores
+// term).  Rows whose sum S_i falls below lo (offset 0; the sum is then
+// <= N) or leaves [kParentRoute, 1 / kParentRoute] (a parent offset) are
+// refined on the matrix cores
 // instead of going to the fp64 fixup:
 //   * S_i in the normal range: m_i += floor(log2 S_i) (the dominant terms
 //     then sit in [-log2 n_eff - 1, 0]);
@@ -1508,20 +1518,27 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 // outside the grid range, or whose offset leaves the two-piece range of b',
 // and any row the second pass still cannot resolve, take the exact fp64
 // fixup.  lo: the folded scheme's routing bound: a row
-// whose sum stays within [lo, 1/lo] of its offset keeps the derived bound
+// without an offset whose sum stays at or above lo keeps the derived bound
 // under 1e-5 / 1.5 -- 2^-24 where KL <= 2 lo MFMAs fold (d <= 4), 2^-12
 // where KL = 3 (d = 6, 8; 2^-16 measured a 6.76e-6 bound on rows at
 // e = -16, tests/test_gpu_kde_band.py), 2^-4 where KL = 4 ... 8
-// (8 < d <= 24); hi = 1 / lo for rows with an offset
-// (the parent's term was not the dominant one).  The split and bf16 schemes
-// keep the 2^-32 of rounds 1-4.
+// (8 < d <= 24).  The split and bf16 schemes keep the 2^-32 of rounds 1-4.
+// Rows with a parent offset (d > 8): the sum relative to the parent's term
+// is >= 1 by construction and its spread comes from the other terms --
+// quantiles 0.1 / 50 / 99 / 99.9 % of log2 S' = 0.03 / 1.9 / 13.8 / 18.9 on
+// C5's rows (N = 1e6, d = 20), against -22 / -17 / -11 / -8.9 under the
+// global offset.  Routing them at 2^4 would refine 29 % of the rows
+// (353 ms instead of ~200); at 2^16 0.4 % are refined.  Their accuracy is
+// measured (tests/test_gpu_fullsize.py, with the derived bound evaluated
+// on sampled rows); rows without a parent keep the guaranteed range below.
+constexpr double kParentRoute = 0x1p-16;
+
 template <int D>
 struct Route {
   static constexpr bool kFold = Mk<D>::SCH == 2;
   static constexpr double lo =
       !kFold ? 0x1p-32
              : (Mk<D>::KL <= 2 ? 0x1p-24 : (Mk<D>::KL <= 3 ? 0x1p-12 : 0x1p-4));
-  static constexpr double hi = !kFold ? 0x1p+100 : 1.0 / lo;
 };
 constexpr double kLn2d = 0.6931471805599453;
 constexpr int kListBlocks = 8192;  // (segment, row block) blocks of a list pass
@@ -1572,12 +1589,13 @@ size_t mfma_ws_layout(int64_t M, int nseg, char* base, MfmaWs* w) {
   return off;
 }
 
-// pass-1 finalize: the fixed-order segment sum; rows inside [lo, hi] (hi
-// only where the row has an offset) are final, the rest join the refine list
+// pass-1 finalize: the fixed-order segment sum; rows at or above lo (rows
+// without an offset) or inside [kParentRoute, 1 / kParentRoute] (rows with
+// a parent offset) are final, the rest join the refine list
 __global__ __launch_bounds__(256) void mfma_finalize_kernel(
     const double* __restrict__ partial, int64_t M, int nseg,
     const double* __restrict__ row_off, const double* __restrict__ lw2max,
-    double log_const, double lo, double hi, double* __restrict__ out,
+    double log_const, double lo, double* __restrict__ out,
     int* __restrict__ cnt, int* __restrict__ rows1, double* __restrict__ s1) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= M) return;
@@ -1585,7 +1603,8 @@ __global__ __launch_bounds__(256) void mfma_finalize_kernel(
   for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * M + i];
   const double m = row_off ? row_off[i] : 0.0;
   const double off = kLn2d * (*lw2max) + log_const;
-  if (S >= lo && (S <= hi || m == 0.0)) {
+  const bool keep = m == 0.0 ? S >= lo : (S >= kParentRoute && S <= 1.0 / kParentRoute);
+  if (keep) {
     out[i] = log(S) + off + kLn2d * m;
   } else {
     const int f = atomicAdd(cnt + 1, 1);
@@ -1769,9 +1788,8 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
   // without the grid (abc_kde_logpdf_mfma) flagged rows go straight to the
   // fp64 fixup, at the 2^-32 bound of rounds 1-4
   const double lo = gscale ? Route<D>::lo : 0x1p-32;
-  const double hi = gscale ? Route<D>::hi : INFINITY;
   hipLaunchKernelGGL(mfma_finalize_kernel, dim3(gm), dim3(256), 0, st, w.partial,
-                     M, p.nseg, row_off, lw2max, log_const, lo, hi, out, w.cnt,
+                     M, p.nseg, row_off, lw2max, log_const, lo, out, w.cnt,
                      w.rows1, w.s1);
   hipLaunchKernelGGL(refine_classify_kernel<D>, dim3(gl), dim3(256), 0, st, w.cnt,
                      w.rows1, w.s1, row_off, Ynew, gscale, w.rows2, w.m2, w.rowsx,

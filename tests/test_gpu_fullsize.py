@@ -176,6 +176,32 @@ def _check(d, N, gens, n_random, n_tail, n_edge, tag, variants=None,
             err_ref[len(pick):].max()),
         max_rel_err_f64_kernel_vs_oracle=float(err_64_ref.max()),
         min_logpd_constructed=float(lp_ref[len(pick):].min()))
+    # the derived per-row bound (tests/kde_bound.py) on sampled production
+    # rows, under the offsets the pass applies (parents at d > 8, then the
+    # refine's): every sampled row's error must lie below its bound
+    from tests.kde_bound import row_stats, pass_offsets
+    D = fit.packed.D
+    KL = (5 * D + 4 + 15) // 16
+    n = int(fit.n)
+    pickb = np.union1d(rng.choice(M, min(M, 8192), replace=False), [worst])
+    pb = torch.as_tensor(pickb, device="cuda")
+    par = res.parent.index_select(0, pb) if getattr(res, "parent", None) \
+        is not None else None
+    Wb = fit.packed.whiten(theta.index_select(0, pb), par)
+    Yp = fit.packed.P[:n, :D].contiguous()
+    lw = fit.packed.P[:n, D].contiguous()
+    st0 = row_stats(Yp, lw, Wb.Y, Wb.row_off, KL, D, g)
+    m_fin, routed = pass_offsets(st0["log2S"], st0["emax"],
+                                 Wb.row_off.cpu().numpy(), D)
+    stb = row_stats(Yp, lw, Wb.Y, torch.as_tensor(m_fin, device="cuda"), KL,
+                    D, g)
+    stats.update(
+        bound_rows=int(len(pickb)),
+        bound_max_sampled=float(stb["bound"].max()),
+        bound_median_sampled=float(np.median(stb["bound"])),
+        bound_routed_fraction=float(routed.mean()),
+        max_err_over_bound_sampled=float(
+            (err_all[pickb] / stb["bound"]).max()))
     var_err = {}
     for name, env in (variants or {}).items():
         lp_v = _variant_logpdf(fit.packed, theta, env)
@@ -199,6 +225,7 @@ def _check(d, N, gens, n_random, n_tail, n_edge, tag, variants=None,
             json.dump(old + [stats], f, indent=1)
     print(json.dumps(stats))
     assert err_64_ref.max() < 1e-11, stats
+    assert np.all(err_all[pickb] <= stb["bound"]), stats
     assert err_all.max() < bound, stats
     assert err_ref.max() < bound, stats
     for name, (e_all, e_ref) in var_err.items():

@@ -34,6 +34,8 @@ import pytest
 import torch
 
 from oracle import ref_cpu as ref
+from tests.kde_bound import row_stats as _row_stats, \
+    pass_offsets as _pass_offsets
 
 pytestmark = pytest.mark.gpu
 
@@ -47,62 +49,6 @@ def K():
         pytest.skip("no GPU")
     from pyabc_amd import kernels
     return kernels
-
-
-def _ulp32(x):
-    """ulp of fp32 at |x| (x > 0; normal range)."""
-    _, E = torch.frexp(x)
-    return torch.ldexp(torch.ones_like(x), (E - 24).to(torch.int32))
-
-
-def _row_stats(Yp, lw, Y, off, KL, D, g, chunk=128):
-    """Per row: the largest exponent (relative to the global offset), the
-    term-share entropy H (bits), log2 of the sum, and the derived bound
-    under the row offset ``off`` (log2 units).  The folded accumulator of
-    pair (i, j) starts at the exact hi_ij = 2 y1_i.y1_j + aH_j + bH_i
-    (multiples of G = g^2; bH carries the offset) and each lo MFMA rounds
-    at most at |hi_ij| + |lo_ij|, lo_ij = e'_ij - hi_ij."""
-    G = g * g
-    n2p = (Yp * Yp).sum(1)
-    y1p = g * torch.round(Yp / g)
-    aH = G * torch.round((lw - n2p) / G)
-    out = {k: [] for k in ("emax", "H", "log2S", "bound")}
-    for i0 in range(0, Y.shape[0], chunk):
-        y = Y[i0:i0 + chunk]
-        m = off[i0:i0 + chunk]
-        n2 = (y * y).sum(1)
-        e = lw[None, :] - (n2[:, None] + n2p[None, :] - 2.0 * y @ Yp.T)
-        emax = e.max(1).values
-        t = torch.exp2(e - emax[:, None])
-        s = t.sum(1)
-        p = t / s[:, None]
-        H = -(p * torch.log2(torch.where(p > 0, p, torch.ones_like(p)))).sum(1)
-        bH = G * torch.round((-n2 - m) / G)
-        hi = 2.0 * (g * torch.round(y / g)) @ y1p.T + aH[None, :] + bH[:, None]
-        lo = (e - m[:, None]) - hi
-        u = (p * _ulp32(hi.abs() + lo.abs())).sum(1)
-        b = math.log(2) * (1.5 * KL * u + D * G * 2.0 ** -12) \
-            + 2.0 ** -23 + 6 * 2.0 ** -24
-        out["emax"].append(emax)
-        out["H"].append(H)
-        out["log2S"].append(emax + torch.log2(s))
-        out["bound"].append(b)
-    return {k: torch.cat(v).cpu().numpy() for k, v in out.items()}
-
-
-def _pass_offsets(log2S, emax, m1, D):
-    """The offset each row ends up with in kde_mfma.hip: the pass-1 offset
-    m1 while the sum relative to it lies in the routing range (Route),
-    otherwise m1 + floor(log2 S') (S' in the normal range) or the max
-    pass's m1 + floor(max e')."""
-    KL = (5 * D + 4 + 15) // 16
-    lo = 2.0 ** -24 if KL <= 2 else (2.0 ** -12 if KL <= 3 else 2.0 ** -4)
-    hi = 1.0 / lo
-    lS = log2S - m1
-    keep = (lS >= math.log2(lo)) & ((lS <= math.log2(hi)) | (m1 == 0))
-    normal = (lS > -100) & (lS < 100)
-    m2 = np.where(normal, m1 + np.floor(lS), m1 + np.floor(emax - m1))
-    return np.where(keep, m1, m2), ~keep
 
 
 def _band_rows(Yp, lw, n_want, rng, d):

@@ -52,9 +52,10 @@ class DeviceMVNFit:
     previous population for the KDE pass (scipy _PSD whitening)."""
 
     def __init__(self, X, w, scaling=1.0, bandwidth_selector=None,
-                 precision="mfma", moments=None):
+                 precision="mfma", moments=None, pack_stream=None):
         self.X = X
         self.w = w
+        self.precision = precision
         n, d = X.shape
         self.n, self.d = n, d
         bw_sel = bandwidth_selector or silverman_rule_of_thumb
@@ -81,17 +82,50 @@ class DeviceMVNFit:
         # numpy legacy multivariate_normal factor: A = sqrt(s)[:,None] * V
         _, s, v = np.linalg.svd(self.cov)
         self.A_host = np.sqrt(s)[:, None] * v
-        self.A = torch.as_tensor(self.A_host, dtype=F64, device=X.device)
         U, rank, log_pdet = K.psd_whitening(self.cov)
         self.rank, self.log_pdet = rank, log_pdet
-        Us = torch.as_tensor(U * math.sqrt(0.5 * K.LOG2E), dtype=F64,
-                             device=X.device)
-        mu_t = torch.as_tensor(mu, dtype=F64, device=X.device)
-        self.packed = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
-                                         precision)
+        # A, the whitening Us and mu in ONE host-to-device copy
+        host = np.concatenate([self.A_host.ravel(),
+                               (U * math.sqrt(0.5 * K.LOG2E)).ravel(),
+                               np.asarray(mu, dtype=np.float64).ravel()])
+        dev = torch.as_tensor(host, dtype=F64, device=X.device)
+        self.A = dev[:d * d].view(d, d)
+        Us = dev[d * d:2 * d * d].view(d, d)
+        mu_t = dev[2 * d * d:]
+        self._pack_ev = None
+        if pack_stream is None:
+            self._packed = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
+                                              precision)
+        else:
+            # the KDE pack on another stream: the next generation's
+            # proposals and simulation do not wait for it; its first user
+            # (the density pass, through .packed) does
+            main = torch.cuda.current_stream()
+            ev = torch.cuda.Event()
+            ev.record(main)
+            with torch.cuda.stream(pack_stream):
+                pack_stream.wait_event(ev)
+                pp = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
+                                        precision)
+                self._pack_ev = torch.cuda.Event()
+                self._pack_ev.record(pack_stream)
+            for t in (pp.P, pp.lw2max, getattr(pp, "A", None),
+                      getattr(pp, "gscale", None)):
+                if t is not None:
+                    t.record_stream(main)
+            self._packed = pp
         self._cdf = None
         self._tab = None
         self._cdf_ev = None
+
+    @property
+    def packed(self):
+        """The packed previous population (waits for its stream's pack at
+        first use)."""
+        if self._pack_ev is not None:
+            torch.cuda.current_stream().wait_event(self._pack_ev)
+            self._pack_ev = None
+        return self._packed
 
     @property
     def cdf(self):
@@ -139,8 +173,9 @@ def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
     ``_fit_transitions``), with the stages that do not depend on each other
     overlapped: the resampling CDF (latency-bound binade walks) runs on a
     side stream while the main stream computes the weighted moments and the
-    quantile, both read back by ONE host wait; then the host d x d finish
-    and the KDE pack.  Every rank holds the whole population and computes
+    quantile, both read back by ONE host wait; then the host d x d finish,
+    and the KDE pack goes to the side stream after the CDF (the next
+    generation's density pass waits for it, its proposals do not).  Every rank holds the whole population and computes
     the same bits (no collective).  Returns (eps, fit)."""
     main = torch.cuda.current_stream()
     ev = torch.cuda.Event()
@@ -158,8 +193,10 @@ def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
     mom = K.weighted_moments(theta, w)
     q = K.weighted_quantile(d, w, alpha, comm=comm)
     host = torch.cat([mom, q[:1]]).cpu().numpy()            # one host wait
+    # the KDE pack follows the CDF on the side stream (needed only by the
+    # next generation's density pass)
     fit = DeviceMVNFit(theta, w, scaling, bandwidth_selector, precision,
-                       moments=host[:-1])
+                       moments=host[:-1], pack_stream=side)
     fit.adopt_cdf(cdf, tab, cdf_ev)
     return float(host[-1]), fit
 
@@ -500,8 +537,9 @@ class GenerationEngine:
         # the accepted rows' parents (resample indices) travel with theta to
         # the MFMA KDE pass, which evaluates each row relative to its
         # parent's term (kde_mfma.hip, per-row offsets)
-        use_parent = fit is not None and getattr(
-            getattr(fit, "packed", None), "precision", None) == "mfma"
+        # (the pass uses parents where KL >= 4 lo MFMAs fold: d > 8)
+        use_parent = fit is not None and self.d > 8 and getattr(
+            fit, "precision", None) == "mfma"
         # SingleCoreSampler starts evaluation k (1-based) iff k - 1 <
         # max_eval: at most ceil(max_eval) evaluations (singlecore.py:24-30)
         cap = math.ceil(max_eval) if math.isfinite(max_eval) else math.inf

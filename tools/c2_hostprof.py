@@ -25,10 +25,12 @@ def main():
     # call sites of the synchronous copies / syncs (innermost repo frames)
     sites = {}
     for ev in p.events():
-        if ev.name not in ("hipMemcpyWithStream", "hipDeviceSynchronize",
-                           "hipStreamSynchronize"):
+        if ev.name not in ("aten::_local_scalar_dense", "aten::_to_copy",
+                           "aten::synchronize", "cudaDeviceSynchronize",
+                           "hipDeviceSynchronize"):
             continue
-        stack = [s for s in (ev.stack or []) if "repo" in s][:4]
+        stack = [s for s in (ev.stack or [])
+                 if "repo" in s and "profiler" not in s][:5]
         key = (ev.name, " <- ".join(stack))
         n, t = sites.get(key, (0, 0.0))
         sites[key] = (n + 1, t + ev.cpu_time_total)

@@ -1234,8 +1234,12 @@ constexpr int lds2g_waves(int KT, int IB, bool PIPE) {
 // two blocks per CU)
 constexpr int lds2g_stage_tiles(int KT) { return KT <= 4 ? ABC_KDE_STAGE_TILES : 2; }
 
-template <int KH, int KL, int IB, int SCH, bool PIPE = true>
-__global__ __launch_bounds__(64 * kWaves)
+// W: waves per block.  4 by default; 8 (ABC_KDE_MFMA_LDS2 = 4, d > 8) lets
+// twice as many i-tiles share each LDS stage, which halves every wave's
+// share of the LDS-DMA refill (the d = 20 probe ladder prices the refill at
+// 18.6 ns per tile step at IB = 2, profiles/r05_issue_probe.json)
+template <int KH, int KL, int IB, int SCH, bool PIPE = true, int W = kWaves>
+__global__ __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB, PIPE))))
 void kde_mfma_lds2g_kernel(
     const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
@@ -1253,7 +1257,7 @@ void kde_mfma_lds2g_kernel(
   int64_t rb;
   block_coords(split, s, rb);
   split = split < 0 ? -split : split;
-  const int64_t t0 = (rb * kWaves + wave) * IB;
+  const int64_t t0 = (rb * W + wave) * IB;
 
   bf16x8 bq[IB][KT];
 #pragma unroll
@@ -1273,7 +1277,7 @@ void kde_mfma_lds2g_kernel(
     // segment's last 64 rows)
     auto fill = [&](int buf, int jc, int nt) {
       const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
-      for (int f = wave; f < nt * KT; f += kWaves)
+      for (int f = wave; f < nt * KT; f += W)
         __builtin_amdgcn_global_load_lds(
             src + f * 64 + lane,
             (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
@@ -1446,6 +1450,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // 4) 210.3 / 210.4 ms, IB = 3 unpipelined 215.9 ms, IB = 3 pipelined
     // 198.9 ms
     const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
+    if (lds2 == 4 && IB == 3 && p.row_blocks % 2 == 0) {  // 8 waves per block
+      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, true, 8>),
+                         dim3(static_cast<unsigned>(p.row_blocks / 2 * p.split)),
+                         dim3(64 * 8), 0, st, Bfr, M, Afr, npad, split, p.spb,
+                         p.jseg, partial);
+      return;
+    }
     if (lds2 == 3) {  // no in-wave pipelining
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,

@@ -1234,10 +1234,10 @@ constexpr int lds2g_waves(int KT, int IB, bool PIPE) {
 // two blocks per CU)
 constexpr int lds2g_stage_tiles(int KT) { return KT <= 4 ? ABC_KDE_STAGE_TILES : 2; }
 
-// W: waves per block.  4 by default; 8 (ABC_KDE_MFMA_LDS2 = 4, d > 8) lets
-// twice as many i-tiles share each LDS stage, which halves every wave's
-// share of the LDS-DMA refill (the d = 20 probe ladder prices the refill at
-// 18.6 ns per tile step at IB = 2, profiles/r05_issue_probe.json)
+// W: waves per block (4).  Measured and not kept (round 5): 8 waves per
+// block at d = 20, IB = 3 -- every wave's share of the LDS-DMA refill
+// halves -- ran 199.2 / 199.5 ms against 196.9 / 198.7 ms, interleaved
+// (gpurun_out/r05h)
 template <int KH, int KL, int IB, int SCH, bool PIPE = true, int W = kWaves>
 __global__ __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(lds2g_waves(KH + KL, IB, PIPE))))
@@ -1450,13 +1450,6 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
     // 4) 210.3 / 210.4 ms, IB = 3 unpipelined 215.9 ms, IB = 3 pipelined
     // 198.9 ms
     const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
-    if (lds2 == 4 && IB == 3 && p.row_blocks % 2 == 0) {  // 8 waves per block
-      hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, true, 8>),
-                         dim3(static_cast<unsigned>(p.row_blocks / 2 * p.split)),
-                         dim3(64 * 8), 0, st, Bfr, M, Afr, npad, split, p.spb,
-                         p.jseg, partial);
-      return;
-    }
     if (lds2 == 3) {  // no in-wave pipelining
       hipLaunchKernelGGL((kde_mfma_lds2g_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH, false>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,

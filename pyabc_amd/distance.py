@@ -322,10 +322,13 @@ class AdaptivePNormDistance(PNormDistance):
 
     def _update(self, t, all_sum_stats):
         keys = list(self.x_0.keys())
-        scales = self._scales(keys, all_sum_stats)
-        w = {}
-        for key, s in zip(keys, scales):
-            w[key] = 0 if np.isclose(s, 0) else 1 / s
+        scales = np.asarray(self._scales(keys, all_sum_stats),
+                            dtype=np.float64)
+        # 0 where np.isclose(s, 0), else 1 / s (elementwise: the same
+        # values as the per-key loop, one numpy call instead of S)
+        close = np.isclose(scales, 0)
+        inv = np.where(close, 0.0, 1.0 / np.where(close, 1.0, scales))
+        w = dict(zip(keys, inv.tolist()))
         w = self._normalize_weights(w)
         w = self._bound_weights(w)
         self.weights[t] = w
@@ -334,10 +337,8 @@ class AdaptivePNormDistance(PNormDistance):
     def _normalize_weights(self, w):
         if not self.normalize_weights:
             return w
-        mean_weight = np.mean(list(w.values()))
-        for key in w:
-            w[key] /= mean_weight
-        return w
+        vals = np.array(list(w.values()), dtype=np.float64)
+        return dict(zip(w.keys(), (vals / np.mean(vals)).tolist()))
 
     def _bound_weights(self, w):
         if self.max_weight_ratio is None:

@@ -88,7 +88,16 @@ class DeviceMVNFit:
         host = np.concatenate([self.A_host.ravel(),
                                (U * math.sqrt(0.5 * K.LOG2E)).ravel(),
                                np.asarray(mu, dtype=np.float64).ravel()])
-        dev = torch.as_tensor(host, dtype=F64, device=X.device)
+        if pack_stream is not None:
+            # page-locked staging: an asynchronous copy (the buffer is
+            # reused a generation later, after the stream has passed it)
+            pin = _pinned("h2d", host.size)
+            pin[:host.size].numpy()[:] = host
+            dev = torch.empty(host.size, dtype=F64, device=X.device)
+            dev.copy_(pin[:host.size], non_blocking=True)
+            _pinned_used("h2d")
+        else:
+            dev = torch.as_tensor(host, dtype=F64, device=X.device)
         self.A = dev[:d * d].view(d, d)
         Us = dev[d * d:2 * d * d].view(d, d)
         mu_t = dev[2 * d * d:]
@@ -157,6 +166,7 @@ class DeviceMVNFit:
 
 
 _SIDE = {}
+_PINNED = {}
 
 
 def _side_stream():
@@ -164,6 +174,47 @@ def _side_stream():
     if dev not in _SIDE:
         _SIDE[dev] = torch.cuda.Stream(device=dev)
     return _SIDE[dev]
+
+
+def _pinned(key, n):
+    """A cached page-locked host buffer of >= n float64 for asynchronous
+    copies.  Waits for the copy that last used the buffer (its event, see
+    _pinned_used) before handing it out again."""
+    b, ev = _PINNED.get(key, (None, None))
+    if ev is not None:
+        ev.synchronize()
+    if b is None or b.numel() < n:
+        b = torch.empty(max(n, 256), dtype=F64, pin_memory=True)
+    _PINNED[key] = (b, None)
+    return b
+
+
+def _pinned_used(key):
+    """Mark the buffer's pending copy (an event on the current stream)."""
+    b, _ = _PINNED[key]
+    ev = torch.cuda.Event()
+    ev.record()
+    _PINNED[key] = (b, ev)
+
+
+def start_cdf(w):
+    """The resampling CDF of w and its bucket table, launched on the side
+    stream after the launching stream's work so far; returns (cdf, tab,
+    event) for DeviceMVNFit.adopt_cdf (waited at first use)."""
+    main = torch.cuda.current_stream()
+    ev = torch.cuda.Event()
+    ev.record(main)
+    side = _side_stream()
+    with torch.cuda.stream(side):
+        side.wait_event(ev)
+        cdf = K.resample_cdf(w)
+        tab = K.cdf_index(cdf)
+        cdf_ev = torch.cuda.Event()
+        cdf_ev.record(side)
+    # allocated on the side stream, read on the main one
+    cdf.record_stream(main)
+    tab.record_stream(main)
+    return cdf, tab, cdf_ev
 
 
 def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
@@ -178,21 +229,18 @@ def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
     generation's density pass waits for it, its proposals do not).  Every rank holds the whole population and computes
     the same bits (no collective).  Returns (eps, fit)."""
     main = torch.cuda.current_stream()
-    ev = torch.cuda.Event()
-    ev.record(main)
     side = _side_stream()
-    with torch.cuda.stream(side):
-        side.wait_event(ev)
-        cdf = K.resample_cdf(w)
-        tab = K.cdf_index(cdf)
-        cdf_ev = torch.cuda.Event()
-        cdf_ev.record(side)
-    # allocated on the side stream, read on the main one
-    cdf.record_stream(main)
-    tab.record_stream(main)
+    cdf, tab, cdf_ev = start_cdf(w)
     mom = K.weighted_moments(theta, w)
     q = K.weighted_quantile(d, w, alpha, comm=comm)
-    host = torch.cat([mom, q[:1]]).cpu().numpy()            # one host wait
+    nm = mom.numel()
+    pin = _pinned("d2h", nm + 1)
+    pin[:nm].copy_(mom, non_blocking=True)
+    pin[nm:nm + 1].copy_(q[:1], non_blocking=True)
+    done = torch.cuda.Event()
+    done.record(main)
+    done.synchronize()                                       # one host wait
+    host = pin[:nm + 1].numpy().copy()
     # the KDE pack follows the CDF on the side stream (needed only by the
     # next generation's density pass)
     fit = DeviceMVNFit(theta, w, scaling, bandwidth_selector, precision,

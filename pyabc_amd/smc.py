@@ -195,7 +195,7 @@ class ABCSMC:
     def _spec(self, t, kind):
         mp = None
         if t > 0:
-            mp = self.history.get_model_probabilities(t - 1)
+            mp = self.history.model_probabilities_dict(t - 1)
         return BatchSpec(t, kind, self.models, self.parameter_priors,
                          self.transitions, self.distance_function, self.eps,
                          self.acceptor, self.x_0,
@@ -233,9 +233,9 @@ class ABCSMC:
 
     def _create_simulate_function(self, t):
         """Per-proposal closure (smc.py:536-600) with the batch spec."""
-        mp = self.history.get_model_probabilities(t - 1)
-        m = np.array(mp.index)
-        p = np.array(mp.p)
+        mp = self.history.model_probabilities_dict(t - 1)
+        m = np.array(list(mp.keys()))
+        p = np.array(list(mp.values()), dtype=np.float64)
         model_prior = self.model_prior
         priors = self.parameter_priors
         mpk = self.model_perturbation_kernel

@@ -736,17 +736,30 @@ class History:
         return (pd.DataFrame(rows, columns=["p", "m", "t"])
                 .pivot(index="t", columns="m", values="p").fillna(0))
 
+    def model_probabilities_dict(self, t):
+        """{m: p} of generation t, as get_model_probabilities(t)'s rows
+        (the generation loop's fast path: no DataFrame for a population
+        held in memory)."""
+        if self._sql is None or (t >= 0 and self._mem(int(t)) is not None):
+            if t < 0:
+                n = len(self._meta.get("model_names", [0]))
+                return {i: 1.0 / n for i in range(n)}
+            return dict(self._pops[int(t)]["population"]
+                        .get_model_probabilities())
+        df = self.get_model_probabilities(t)
+        return dict(zip(df.index, df.p))
+
     def alive_models(self, t=None):
         t = self._t(t)
         if self._sql is None or self._mem(t) is not None:
-            mp = self.get_model_probabilities(t)
-            return list(mp.index[mp.p > 0])
+            return [m for m, p in self.model_probabilities_dict(t).items()
+                    if p > 0]
         return sorted(r[0] for r in self._q("SELECT mo.m " + self._JOIN,
                                             (self._id, t)))
 
     def nr_of_models_alive(self, t=None):
-        mp = self.get_model_probabilities(self._t(t))
-        return int((mp.p > 0).sum())
+        mp = self.model_probabilities_dict(self._t(t))
+        return int(sum(1 for p in mp.values() if p > 0))
 
     def get_distribution(self, m=0, t=None):
         """history.py:268-313 (device frame for a population of this

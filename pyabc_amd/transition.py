@@ -18,7 +18,8 @@ import torch
 
 from . import kernels as K
 from .distributed import Comm
-from .engine import (DeviceMVNFit, silverman_rule_of_thumb,
+from .engine import (DeviceMVNFit, _side_stream, start_cdf,
+                     silverman_rule_of_thumb,
                      scott_rule_of_thumb)
 from .frames import DeviceFrame, as_device_matrix, as_device_vector
 
@@ -169,8 +170,19 @@ class MultivariateNormalTransition(Transition):
             raise NotEnoughParticles("Fitting not possible.")
         Xd, _ = as_device_matrix(X)
         wd = as_device_vector(w)
-        self._fit = DeviceMVNFit(Xd, wd, self.scaling,
-                                 self.bandwidth_selector, self.kde_precision)
+        if Xd.is_cuda:
+            # the resampling CDF and the KDE pack on the side stream,
+            # overlapping the host's d x d finish (engine.start_cdf)
+            c = start_cdf(wd)
+            self._fit = DeviceMVNFit(Xd, wd, self.scaling,
+                                     self.bandwidth_selector,
+                                     self.kde_precision,
+                                     pack_stream=_side_stream())
+            self._fit.adopt_cdf(*c)
+        else:
+            self._fit = DeviceMVNFit(Xd, wd, self.scaling,
+                                     self.bandwidth_selector,
+                                     self.kde_precision)
         self.cov = self._fit.cov
 
     # device-level API used by the batch sampler

@@ -227,7 +227,7 @@ KNOBS = {
         ("ABC_KDE_MFMA_LDS2", "3"), ("ABC_KDE_MFMA_LDS2", "0"),
         ("ABC_KDE_MFMA_SMAJOR", "1")],
     20: [("ABC_KDE_MFMA_LDS2", "1"), ("ABC_KDE_MFMA_LDS2", "0"),
-         ("ABC_KDE_MFMA_LDS2", "2"), ("ABC_KDE_MFMA_LDS2", "4"),
+         ("ABC_KDE_MFMA_LDS2", "2"),
          ("ABC_KDE_MFMA_IB", "1"), ("ABC_KDE_MFMA_IB", "2"),
          ("ABC_KDE_MFMA_SPLIT", "2"), ("ABC_KDE_MFMA_PIPE", "1"),
          ("ABC_KDE_MFMA_SMAJOR", "1")],

@@ -1360,6 +1360,99 @@ void kde_mfma_lds2g_kernel(
   }
 }
 
+// The refine's passes over a device-counted row list (MODE 0 density, 1
+// max), folded schemes: the unpipelined LDS-DMA form of
+// kde_mfma_lds2g_kernel (A fragments shared by the block's four waves
+// through LDS) with blocks taking (segment, row block) pairs grid-stride.
+// A row's arithmetic is the main pass's (the register list kernel, which
+// streams A per wave from L2, served the round's first measurements: 1.6 ms
+// per launch for ~4000 rows at d = 20, N = 1e6).
+template <int KH, int KL, int IB, int SCH, int MODE>
+__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_list_kernel(
+    const bf16x8* __restrict__ Bfr, const int* __restrict__ count, int64_t ld,
+    const bf16x8* __restrict__ Afr, int64_t npad, int nseg, int jseg,
+    double* __restrict__ partial) {
+  constexpr int KT = KH + KL;
+  constexpr int TPS = lds2g_stage_tiles(KT);
+  constexpr int CH = TPS * KT;
+  constexpr float kInit = MODE == 0 ? 0.0f : -INFINITY;
+  static_assert(kFolded<KL, SCH>, "folded accumulation only");
+  __shared__ bf16x8 As[2][CH][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t M = *count;
+  const int64_t nrb = ceil_div(M, 32 * kWaves * IB);
+  const int s = static_cast<int>(blockIdx.x % nseg);
+  const int64_t stride = gridDim.x / nseg;
+  const int64_t j0 = static_cast<int64_t>(s) * jseg;
+  const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
+  const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
+  auto fill = [&](int buf, int jc, int nt) {
+    const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
+    for (int f = wave; f < nt * KT; f += kWaves)
+      __builtin_amdgcn_global_load_lds(
+          src + f * 64 + lane,
+          (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
+  };
+  auto stage_tiles = [&](int jc) { return min(TPS, (nj - jc) >> 5); };
+  for (int64_t rb = blockIdx.x / nseg; rb < nrb; rb += stride) {
+    const int64_t t0 = (rb * kWaves + wave) * IB;
+    bf16x8 bq[IB][KT];
+#pragma unroll
+    for (int t = 0; t < IB; ++t)
+#pragma unroll
+      for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
+    double S[IB];
+#pragma unroll
+    for (int t = 0; t < IB; ++t) S[t] = kInit;
+    __syncthreads();  // the previous row block's readers are done with As
+    if (nj > 0) fill(0, 0, stage_tiles(0));
+    int buf = 0;
+    f32x16 acc[IB];
+    for (int jc = 0; jc < nj;) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int nt = stage_tiles(jc);
+      const int jn = jc + 32 * nt;
+      if (jn < nj) fill(buf ^ 1, jn, stage_tiles(jn));
+      const bf16x8(*Ab)[64] = As[buf];
+#pragma unroll
+      for (int u0 = 0; u0 < TPS; u0 += 2) {
+        if (u0 < nt) {
+          float sc[IB];
+#pragma unroll
+          for (int t = 0; t < IB; ++t) sc[t] = kInit;
+#pragma unroll
+          for (int u = u0; u < u0 + 2; ++u) {
+            bf16x8 a[2];
+            a[0] = Ab[u * KT][lane];
+            a[1] = Ab[u * KT + 1][lane];
+            lds_chain_f<KT, IB, SCH, false>(Ab, u, lane, bq, acc, acc, sc, a);
+#pragma unroll
+            for (int t = 0; t < IB; ++t) tile_acc<MODE, KL, SCH>(sc[t], acc[t], acc[t]);
+          }
+#pragma unroll
+          for (int t = 0; t < IB; ++t) {
+            if constexpr (MODE == 0)
+              S[t] += static_cast<double>(sc[t]);
+            else
+              S[t] = fmax(S[t], static_cast<double>(sc[t]));
+          }
+        }
+      }
+      buf ^= 1;
+      jc = jn;
+    }
+#pragma unroll
+    for (int t = 0; t < IB; ++t) {
+      const double o = __shfl_xor(S[t], 32, 64);
+      const double tot = MODE == 0 ? S[t] + o : fmax(S[t], o);
+      const int64_t i = (t0 + t) * 32 + lane;
+      if (lane < 32 && i < M) partial[static_cast<int64_t>(s) * ld + i] = tot;
+    }
+  }
+}
+
 template <int D>
 int64_t mpad_rows(int64_t M) {
   constexpr int rows = 32 * kWaves * Mk<D>::PADIB;
@@ -1729,10 +1822,17 @@ template <int D, int MODE>
 void launch_list(const bf16x8* Bbuf, const int* count, int64_t ld,
                  const bf16x8* Afr, int64_t npad, int nseg, int jseg,
                  double* partial, hipStream_t st) {
-  // the register kernel holds IB x KT B fragments and two A tiles: IB = 2
-  // above d = 8 keeps it in registers
-  constexpr int IB = D <= 8 ? Mk<D>::IB : (Mk<D>::IB > 2 ? 2 : Mk<D>::IB);
   const int rbs = kListBlocks / nseg > 0 ? kListBlocks / nseg : 1;
+  if constexpr (kFolded<Mk<D>::KL, Mk<D>::SCH>) {
+    hipLaunchKernelGGL((kde_mfma_lds_list_kernel<Mk<D>::KH, Mk<D>::KL, Mk<D>::IB,
+                                               Mk<D>::SCH, MODE>),
+                       dim3(rbs * nseg), dim3(64 * kWaves), 0, st, Bbuf, count, ld,
+                       Afr, npad, nseg, jseg, partial);
+    return;
+  }
+  // the split schemes: the register kernel (it holds IB x KT B fragments
+  // and two A tiles: IB = 2 above d = 8 keeps it in registers)
+  constexpr int IB = D <= 8 ? Mk<D>::IB : (Mk<D>::IB > 2 ? 2 : Mk<D>::IB);
   hipLaunchKernelGGL((kde_mfma_list_kernel<Mk<D>::KH, Mk<D>::KL, IB, (D <= 8),
                                            Mk<D>::SCH, MODE>),
                      dim3(rbs * nseg), dim3(64 * kWaves), 0, st, Bbuf, count, ld,

@@ -223,30 +223,36 @@ def next_generation_inputs(theta, d, w, alpha, comm=None, scaling=1.0,
     of the new population (``smc.py:942-1061``: epsilon update, then
     ``_fit_transitions``), with the stages that do not depend on each other
     overlapped: the resampling CDF (latency-bound binade walks) runs on a
-    side stream while the main stream computes the weighted moments and the
-    quantile, both read back by ONE host wait; then the host d x d finish,
-    and the KDE pack goes to the side stream after the CDF (the next
-    generation's density pass waits for it, its proposals do not).  Every rank holds the whole population and computes
+    side stream while the main stream computes the weighted moments and then
+    the quantile; the host's d x d finish starts as soon as the moments are
+    back (the quantile's kernels still running), and the KDE pack goes to
+    the side stream after the CDF (the next generation's density pass waits
+    for it, its proposals do not).  Every rank holds the whole population and computes
     the same bits (no collective).  Returns (eps, fit)."""
     main = torch.cuda.current_stream()
     side = _side_stream()
     cdf, tab, cdf_ev = start_cdf(w)
     mom = K.weighted_moments(theta, w)
-    q = K.weighted_quantile(d, w, alpha, comm=comm)
     nm = mom.numel()
     pin = _pinned("d2h", nm + 1)
     pin[:nm].copy_(mom, non_blocking=True)
+    mom_ev = torch.cuda.Event()
+    mom_ev.record(main)
+    q = K.weighted_quantile(d, w, alpha, comm=comm)
     pin[nm:nm + 1].copy_(q[:1], non_blocking=True)
-    done = torch.cuda.Event()
-    done.record(main)
-    done.synchronize()                                       # one host wait
-    host = pin[:nm + 1].numpy().copy()
-    # the KDE pack follows the CDF on the side stream (needed only by the
-    # next generation's density pass)
+    q_ev = torch.cuda.Event()
+    q_ev.record(main)
+    # the host's d x d finish runs while the quantile's kernels do; the
+    # KDE pack follows the CDF on the side stream (needed only by the next
+    # generation's density pass)
+    mom_ev.synchronize()
     fit = DeviceMVNFit(theta, w, scaling, bandwidth_selector, precision,
-                       moments=host[:-1], pack_stream=side)
+                       moments=pin[:nm].numpy().copy(), pack_stream=side)
     fit.adopt_cdf(cdf, tab, cdf_ev)
-    return float(host[-1]), fit
+    q_ev.synchronize()
+    eps = float(pin[nm].item())
+    _PINNED["d2h"] = (pin, None)
+    return eps, fit
 
 
 def selection_plan(nvs, nas, n):

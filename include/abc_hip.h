@@ -32,7 +32,8 @@ extern "C" {
 const char* abc_last_error(void);
 int abc_version(void);
 /* Re-read the launch-shape tuning knobs (ABC_KDE_MFMA_SPLIT / _IB / _PIPE /
- * _LDS2 / _SMAJOR, ABC_KDE_TIER, ABC_LZ_IB / _TPB) from the environment.
+ * _LDS2 / _SMAJOR, ABC_KDE_TIER, ABC_LZ_IB / _TPB, ABC_KNN_ROWS) from the
+ * environment.
  * The library reads them once, at the first launch that consults them; the
  * knobs only change how work maps to the chip, never a result bit
  * (tests/test_gpu_kernels.py knob tests).  No reference counterpart. */

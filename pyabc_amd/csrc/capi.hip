@@ -21,7 +21,7 @@ namespace {
 constexpr const char* kKnobNames[kKnobCount] = {
     "ABC_KDE_MFMA_SPLIT", "ABC_KDE_MFMA_IB",   "ABC_KDE_MFMA_PIPE",
     "ABC_KDE_MFMA_LDS2",  "ABC_KDE_MFMA_SMAJOR", "ABC_KDE_TIER",
-    "ABC_LZ_IB",          "ABC_LZ_TPB"};
+    "ABC_LZ_IB",          "ABC_LZ_TPB",          "ABC_KNN_ROWS"};
 std::atomic<int> g_knobs[kKnobCount];
 std::once_flag g_knobs_once;
 

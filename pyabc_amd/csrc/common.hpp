@@ -39,6 +39,7 @@ enum Knob : int {
   kKnobKdeTier,           // ABC_KDE_TIER
   kKnobLzIb,              // ABC_LZ_IB
   kKnobLzTpb,             // ABC_LZ_TPB
+  kKnobKnnRows,           // ABC_KNN_ROWS
   kKnobCount
 };
 // the knob's integer value, or dflt when the variable is unset

@@ -716,12 +716,20 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
   q += al256(static_cast<size_t>(T) * kTile * 8 * 4);
   SpatialWs v = spatial_ws(q, N);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
-  const unsigned grid = static_cast<unsigned>(ceil_div(nrows, kKnnRows));
+  // rows per wave: kKnnRows, or 16 / 4 (tuning knob ABC_KNN_ROWS; the
+  // neighbour sets, order and distances are the same)
+  const int rpw = tuning_knob(kKnobKnnRows, kKnnRows);
   const int64_t rlo = row0, rhi = row0 + nrows;
+#define KNN_R(DD, H, RR)                                                          \
+  hipLaunchKernelGGL((knn_kernel<DD, H, RR>), dim3(ceil_div(nrows, RR)), dim3(64), \
+                     0, st, X, Xs, v.perm, v.tbox, v.T, amax, k, rows, v.count,   \
+                     rlo, nbr, nbr_d2)
 #define KNN(DD, H)                                                               \
-  hipLaunchKernelGGL((knn_kernel<DD, H, kKnnRows>), dim3(grid), dim3(64), 0, st, \
-                     X, Xs, v.perm, v.tbox, v.T, amax, k, rows, v.count, rlo, nbr, \
-                     nbr_d2)
+  do {                                                                           \
+    if (rpw == 16) KNN_R(DD, H, 16);                                             \
+    else if (rpw == 4) KNN_R(DD, H, 4);                                          \
+    else KNN_R(DD, H, kKnnRows);                                                 \
+  } while (0)
 #define L(DD)                                                                    \
   {                                                                              \
     const int rc = spatial_sort_population<DD>(X, N, v, st);                     \

@@ -6,6 +6,7 @@ covariances / epsilon within 1e-5 relative for the fp32 KDE kernel and
 1e-12 for fp64.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -1175,6 +1176,17 @@ def test_knn_rows_tiled_equal_full(K, d):
         nb, dd = K.knn_rows(dev(X), k, lo, m)
         np.testing.assert_array_equal(host(nb), nbr[lo:lo + m])
         np.testing.assert_array_equal(host(dd), d2[lo:lo + m])
+    # rows per wave (tuning knob ABC_KNN_ROWS): the same sets and distances
+    for rpw in ("4", "16"):
+        os.environ["ABC_KNN_ROWS"] = rpw
+        K.reload_tuning()
+        try:
+            nb, dd = K.knn(dev(X), k)
+        finally:
+            os.environ.pop("ABC_KNN_ROWS", None)
+            K.reload_tuning()
+        np.testing.assert_array_equal(host(nb), nbr, err_msg=rpw)
+        np.testing.assert_array_equal(host(dd), d2, err_msg=rpw)
     rows = rng.choice(n, 200, replace=False)
     diff = X[None, :, :] - X[rows, None, :]
     D2 = np.zeros((len(rows), n))

@@ -854,107 +854,6 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_list_kernel(
                                                jseg, partial);
 }
 
-// MFMA-bound form for d > 8.  Per 32x32 tile a wave runs KT = KH + KL
-// MFMAs; with A streamed per wave from L2 (kde_mfma_kernel) every MFMA needs
-// 1 KiB of A per 32 cycles, i.e. 128 B/clk/CU at IB = 1 and 64 at IB = 2 --
-// the vector L1's whole bandwidth, so the matrix pipe ran at ~50 % (21 ms at
-// N = M = 262144, d = 20).  Here the A fragments of each 64-row chunk are
-// copied ONCE per block into LDS by LDS-DMA (double-buffered, one barrier
-// per chunk), and each fragment read back from LDS (ds_read_b128) feeds IB
-// MFMAs, one per i-tile held in registers: LDS serves 128/IB B/clk/CU, L2
-// only 1/(kWaves*IB) of the A bytes.  A wave holds B (IB*KT fragments), the
-// 2*IB accumulators and one A fragment in flight, so two waves share a SIMD
-// and one wave's exp block runs beside another's MFMA chain.  Per-lane
-// arithmetic and summation order are those of kde_mfma_rows (split hi / lo
-// accumulators, tile 0 then tile 1 of each chunk): the rows are
-// bit-identical to kde_mfma_kernel's.
-template <int KH, int KL, int IB, int SCH>
-__global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds2_kernel(
-    const bf16x8* __restrict__ Bfr, int64_t M, const bf16x8* __restrict__ Afr,
-    int64_t npad, int split, int spb, int jseg, double* __restrict__ partial) {
-  constexpr int KT = KH + KL;
-  constexpr int CH = 2 * KT;  // 1-KiB fragments per 64-row chunk
-  __shared__ bf16x8 As[2][CH][64];
-  const int lane = threadIdx.x & 63;
-  // wave-uniform: the LDS-DMA fill loop and its M0 address stay scalar
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int s;
-  int64_t rb;
-  block_coords(split, s, rb);
-  split = split < 0 ? -split : split;
-  const int64_t t0 = (rb * kWaves + wave) * IB;
-
-  bf16x8 bq[IB][KT];
-#pragma unroll
-  for (int t = 0; t < IB; ++t)
-#pragma unroll
-    for (int c = 0; c < KT; ++c) bq[t][c] = Bfr[((t0 + t) * KT + c) * 64 + lane];
-
-  for (int gi = 0; gi < spb; ++gi) {
-    const int seg = s * spb + gi;
-    const int64_t j0 = static_cast<int64_t>(seg) * jseg;
-    const int nj = static_cast<int>(j0 < npad ? min<int64_t>(jseg, npad - j0) : 0);
-    const bf16x8* __restrict__ Aseg = Afr + (j0 >> 5) * KT * 64;
-    double S[IB];
-#pragma unroll
-    for (int t = 0; t < IB; ++t) S[t] = 0.0;
-    // fragment f of a chunk = contiguous 1 KiB at Aseg + (chunk*2*KT + f)*64
-    auto fill = [&](int buf, int jc) {
-      const bf16x8* __restrict__ src = Aseg + (jc >> 5) * KT * 64;
-      for (int f = wave; f < CH; f += kWaves)
-        __builtin_amdgcn_global_load_lds(
-            src + f * 64 + lane,
-            (__attribute__((address_space(3))) void*)&As[buf][f][0], 16, 0, 0);
-    };
-    __syncthreads();  // the previous segment's readers are done with As
-    if (nj > 0) fill(0, 0);
-    int buf = 0;
-    for (int jc = 0; jc < nj; jc += 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // chunk jc landed (each wave waited for its own pieces) and every wave
-      // is done with chunk jc - 64, whose buffer is refilled now
-      __syncthreads();
-      if (jc + 64 < nj) fill(buf ^ 1, jc + 64);
-      const bf16x8(*Ab)[64] = As[buf];
-      float sacc[IB];
-#pragma unroll
-      for (int t = 0; t < IB; ++t) sacc[t] = 0.0f;
-#pragma unroll
-      for (int tile = 0; tile < 2; ++tile) {
-        f32x16 hi[IB], lo[IB];
-#pragma unroll
-        for (int t = 0; t < IB; ++t) hi[t] = lo[t] = f32x16{};
-#pragma unroll
-        for (int c = 0; c < KT; ++c) {
-          const bf16x8 a = Ab[tile * KT + c][lane];
-#pragma unroll
-          for (int t = 0; t < IB; ++t) {
-            if (c < KH)
-              hi[t] = mfma_op<(SCH != 0)>(a, bq[t][c], hi[t]);
-            else
-              lo[t] = mfma_op<(SCH != 0)>(a, bq[t][c], lo[t]);
-          }
-          // one fragment read ahead of its IB MFMAs, no early hoisting
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, IB, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < IB; ++t)
-          sacc[t] += tile_sum_split<SCH>(hi[t], lo[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < IB; ++t) S[t] += static_cast<double>(sacc[t]);
-      buf ^= 1;  // the next top barrier also ends every read of this buffer
-    }
-#pragma unroll
-    for (int t = 0; t < IB; ++t) {
-      const double tot = S[t] + __shfl_xor(S[t], 32, 64);
-      const int64_t i = (t0 + t) * 32 + lane;
-      if (lane < 32 && i < M) partial[static_cast<int64_t>(seg) * M + i] = tot;
-    }
-  }
-}
-
 // ---- hand-interleaved LDS-DMA passes (d > 8) --------------------------------
 // The VALU of one 32-row tile is cut into slices placed in the gaps of the
 // NEXT tile's MFMA chain, one slice after each MFMA, with sched_barrier
@@ -1069,9 +968,10 @@ __device__ __forceinline__ void lds_chain(const bf16x8 (*Ab)[64], int tile, int 
   }
 }
 
-// The d > 8 default: the split accumulation of kde_mfma_lds2_kernel with
-// the VALU hand-placed in the MFMA gaps; rows bit-identical to it (and to
-// the register kernel).  d = 20, N = M = 262144: 19.3 (lds2) -> 18.0 ms.
+// The split accumulation (d > 24) with A fragments shared through LDS by
+// LDS-DMA (double-buffered, one barrier per 64-row chunk; each fragment
+// read feeds IB MFMAs) and the VALU hand-placed in the MFMA gaps; rows
+// bit-identical to the register kernel's.  d = 20, N = M = 262144: 19.3 (lds2) -> 18.0 ms.
 // (The folded accumulation in the same schedule ran 16.8 ms but its error
 // reached 6.3e-6 at N = M = 1e6 against 1.5e-6 -- DESIGN.md section 4 --
 // and was dropped.)
@@ -1556,18 +1456,13 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
       return;
     }
   } else if constexpr (D > 8) {
-    // 2: hand-interleaved split pass; 1: LDS-DMA A fragments, compiler
-    // schedule (d = 20: 21.5 -> 20.4 ms at N = M = 262144 against the
-    // register kernel); 0: the register kernel.  Rows bit-identical.
+    // the split schemes (d > 24): the hand-interleaved LDS-DMA pass, or the
+    // register kernel (0); rows bit-identical.  (The LDS-DMA pass with the
+    // compiler's schedule, rounds 2-4, is gone: 19.3 vs 17.9 ms at d = 20,
+    // N = M = 262144.)
     const int lds2 = tuning_knob(kKnobKdeMfmaLds2, 2);
-    if (lds2 == 2) {
-      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
-                         dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
-                         p.spb, p.jseg, partial);
-      return;
-    }
     if (lds2 != 0) {
-      hipLaunchKernelGGL((kde_mfma_lds2_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
+      hipLaunchKernelGGL((kde_mfma_lds2i_kernel<Mk<D>::KH, Mk<D>::KL, IB, Mk<D>::SCH>),
                          dim3(grid), block, 0, st, Bfr, M, Afr, npad, split,
                          p.spb, p.jseg, partial);
       return;

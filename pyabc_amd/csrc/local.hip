@@ -25,7 +25,8 @@
 namespace abc {
 
 
-constexpr int kKnnRows = 8;     // rows per wave (one wave per block)
+constexpr int kKnnRows = 4;     // rows per wave (one wave per block; 8 before
+                                // round 5: 7.6 -> 6.1 ms, tools/knn_ab.py)
 constexpr int kMaxK = 192;      // buffer of 256 = k kept + 64 appended
 
 // Separately rounded fp64 ops: hipcc contracts a*b+c into an FMA by default
@@ -716,7 +717,7 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
   q += al256(static_cast<size_t>(T) * kTile * 8 * 4);
   SpatialWs v = spatial_ws(q, N);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
-  // rows per wave: kKnnRows, or 16 / 4 (tuning knob ABC_KNN_ROWS; the
+  // rows per wave: kKnnRows, or 2 / 8 / 16 (tuning knob ABC_KNN_ROWS; the
   // neighbour sets, order and distances are the same)
   const int rpw = tuning_knob(kKnobKnnRows, kKnnRows);
   const int64_t rlo = row0, rhi = row0 + nrows;
@@ -727,7 +728,8 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
 #define KNN(DD, H)                                                               \
   do {                                                                           \
     if (rpw == 16) KNN_R(DD, H, 16);                                             \
-    else if (rpw == 4) KNN_R(DD, H, 4);                                          \
+    else if (rpw == 8) KNN_R(DD, H, 8);                                          \
+    else if (rpw == 2) KNN_R(DD, H, 2);                                          \
     else KNN_R(DD, H, kKnnRows);                                                 \
   } while (0)
 #define L(DD)                                                                    \

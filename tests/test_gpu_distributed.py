@@ -109,6 +109,86 @@ def _rank_main(rank, world, port, n, out):
     torch.distributed.destroy_process_group()
 
 
+def _generations_parents(comm, n, min_batch):
+    """d = 12 (KL >= 4: the MFMA pass evaluates each row relative to its
+    parent's term): two generations, the second on the fit of
+    engine.next_generation_inputs (CDF and KDE pack on the side stream)."""
+    from pyabc_amd import kernels as K
+    from pyabc_amd.batch_models import LinearGaussianModel
+    from pyabc_amd.engine import (GenerationEngine, DeviceMVNFit,
+                                  next_generation_inputs)
+    d, S = 12, 24
+    model = LinearGaussianModel.benchmark(d, S)
+    x0 = torch.as_tensor(model._x0, device="cuda")
+    fw = torch.ones(S, dtype=torch.float64, device="cuda")
+    eng = GenerationEngine(model, np.full(d, -5.0), np.full(d, 10.0),
+                           distance_p=2.0, comm=comm, seed=11,
+                           min_batch=min_batch)
+    eng.max_batch = min_batch
+    r0 = eng.sample_prior(0, n)
+    d0, _, _ = K.pnorm_distance(r0.stats_T, x0, fw, 2.0, math.inf,
+                                with_accept=False)
+    theta = comm.all_gather_rows(r0.theta)
+    dist = comm.all_gather_rows(d0)
+    w = torch.full((theta.shape[0],), 1.0 / theta.shape[0],
+                   dtype=torch.float64, device="cuda")
+    eps = float(K.weighted_quantile(dist, w, 0.5, comm=comm)[0].item())
+    fit = DeviceMVNFit(theta, w)
+    out = {}
+    for t in (1, 2):
+        res = eng.sample_generation(t, n, fit, x0, fw, eps)
+        th, dd, ww, _, _ = eng.gather_population(res)
+        out[f"theta{t}"] = th.cpu().numpy()
+        out[f"parent{t}"] = res.parent.cpu().numpy()
+        out[f"logpd{t}"] = res.logpd.cpu().numpy()
+        out[f"w{t}"] = ww.cpu().numpy()
+        eps, fit = next_generation_inputs(th, dd, ww, 0.5, comm=comm)
+        out[f"eps{t}"] = eps
+    return out
+
+
+def _rank_main_parents(rank, world, port, n, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from pyabc_amd.distributed import Comm
+    comm = Comm.from_env("gloo", device=0)
+    multi = _generations_parents(comm, n, 1 << 11)
+    if rank == 0:
+        out["single"] = _generations_parents(Comm.single(), n, 1 << 12)
+    out[rank] = multi
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_ranks_equal_one_rank_parents_d12():
+    """At d > 8 the accepted rows' parents travel with theta through the
+    all-gather to the row-parallel KDE pass (per-row offsets), and the next
+    fit comes from next_generation_inputs: two ranks reproduce one rank's
+    parents, log-densities, weights and epsilons bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = 3001
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rank_main_parents, args=(2, port, n, out), nprocs=2,
+                 join=True)
+        res = dict(out)
+    one = res["single"]
+    for r in (0, 1):
+        for k, v in one.items():
+            if isinstance(v, float):
+                assert res[r][k] == v, k
+            else:
+                np.testing.assert_array_equal(res[r][k], v, err_msg=k)
+    # the parents index the previous population and are real draws
+    for t in (1, 2):
+        p = one[f"parent{t}"]
+        assert p.min() >= 0 and p.max() < n and len(np.unique(p)) > n // 4
+
+
 @pytest.mark.timeout(240)
 def test_two_ranks_equal_one_rank_bit_for_bit():
     """Global-id sampling (engine.sample_generation): two ranks sharing

@@ -38,6 +38,12 @@ int abc_version(void);
  * knobs only change how work maps to the chip, never a result bit
  * (tests/test_gpu_kernels.py knob tests).  No reference counterpart. */
 void abc_tuning_reload(void);
+/* Load the library's code objects on the current device now (HIP loads each
+ * translation unit's code object at the first launch of one of its kernels,
+ * which otherwise lands inside the first generation that uses it: ~4 ms for
+ * the LocalTransition density pass).  Returns the number of units that did
+ * not resolve (0 on a GPU).  Idempotent.  No reference counterpart. */
+int abc_preload(void);
 
 /* ---------------- (a1) MultivariateNormalTransition.fit ------------------
  * Replaces smart_cov = np.cov(X, aweights=w)        transition/util.py:4-15

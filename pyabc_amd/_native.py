@@ -34,6 +34,7 @@ _SIGS = {
     "abc_last_error": (ctypes.c_char_p, []),
     "abc_version": (c_int, []),
     "abc_tuning_reload": (None, []),
+    "abc_preload": (c_int, []),
     # (a1)
     "abc_moments_workspace_bytes": (c_size, [c_int]),
     "abc_weighted_moments_f64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,

@@ -46,5 +46,12 @@ void abc_tuning_reload(void) {
   abc::load_knobs();
 }
 const char* abc_last_error(void) { return abc::g_err; }
+// Load every unit's code object on the current device up front; returns the
+// number of units that failed to resolve (0 on a GPU).
+int abc_preload(void) {
+  return abc::preload_propose() + abc::preload_kde() + abc::preload_kde_mfma() +
+         abc::preload_distance() + abc::preload_select() + abc::preload_stochastic() +
+         abc::preload_local() + abc::preload_local_pdf32() + abc::preload_local_mfma();
+}
 int abc_version(void) { return 10000; }  // 0.1.0
 }

@@ -85,6 +85,23 @@ inline unsigned stream_grid(int64_t n, int block, int cap = 4096) {
   return static_cast<unsigned>(g);
 }
 
+// Resolve one kernel of a translation unit on the current device, which
+// loads that unit's code object (the per-unit abc::preload_* hooks).
+template <typename F>
+inline int preload_kernel(F* f) {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(f)) == hipSuccess ? 0 : 1;
+}
+int preload_propose();
+int preload_kde();
+int preload_kde_mfma();
+int preload_distance();
+int preload_select();
+int preload_stochastic();
+int preload_local();
+int preload_local_pdf32();
+int preload_local_mfma();
+
 // ---- wave / block reductions (64-lane waves) -------------------------------
 template <typename T>
 __device__ inline T wave_sum(T v) {

@@ -256,3 +256,10 @@ int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_distance() { return preload_kernel(pnorm_kernel<2>); }
+}  // namespace abc

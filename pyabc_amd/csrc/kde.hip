@@ -900,3 +900,10 @@ int abc_kde_logpdf_f64(const double* Ynew, int64_t M, const double* P,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_kde() { return preload_kernel(whiten_kernel<double, 8>); }
+}  // namespace abc

@@ -1970,3 +1970,10 @@ int abc_kde_logpdf_mfma_rows(const void* Bfr, const double* Ynew,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_kde_mfma() { return preload_kernel(ymax_kernel<8>); }
+}  // namespace abc

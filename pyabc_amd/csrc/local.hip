@@ -11,8 +11,8 @@
 // buffer that is re-ranked by EXACT fp64 squared distance (sequential over
 // dimensions, no FMA contraction, as the reference tree computes them) in
 // registers and cut back to k, setting the pruning threshold tau.
-// cov/det/inv: one thread per particle, weighted moments of the k neighbour
-// deltas, LU with partial pivoting for det and inverse (fp64).
+// cov/det/inv: 8 lanes per particle for the weighted moments of the k
+// neighbour deltas, then LU with partial pivoting for det and inverse (fp64).
 // pdf: one thread per evaluation point; the previous population's
 // (X_n, packed symmetric inv_n, log(w_n / norm_n)) stream through the scalar
 // path (wave-uniform), d(d+1)/2 + d FMAs per pair for the quadratic form,
@@ -61,7 +61,7 @@ __device__ inline float knn_filter_bound(double tau, int d, double A) {
   return __double2float_ru(T);
 }
 
-// Tiled prep (spatial.hpp): fp32 centred coordinates in Morton order (one
+// Tiled prep (spatial.hpp): fp32 centred coordinates in Hilbert order (one
 // wave per tile of 64 sorted positions, padding positions at kFar), the
 // tile's bounding box of those fp32 values, and the coordinate bound A.
 constexpr float kFar = 1e30f;  // (kFar - x)^2 overflows to +inf
@@ -69,8 +69,8 @@ constexpr float kFar = 1e30f;  // (kFar - x)^2 overflows to +inf
 template <int D>
 __global__ __launch_bounds__(256) void knn_prep_kernel(
     const double* __restrict__ X, int64_t N, const int32_t* __restrict__ perm,
-    int T, float* __restrict__ Xs, float* __restrict__ tbox,
-    unsigned long long* __restrict__ amax) {
+    int T, float* __restrict__ Xs, double* __restrict__ Xd,
+    float* __restrict__ tbox, unsigned long long* __restrict__ amax) {
   const int lane = threadIdx.x & 63;
   const int t = static_cast<int>((static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) >> 6);
   const int64_t s = static_cast<int64_t>(t) * kTile + lane;
@@ -83,7 +83,9 @@ __global__ __launch_bounds__(256) void knn_prep_kernel(
     const int64_t n = perm[s];
 #pragma unroll
     for (int q = 0; q < D; ++q) {
-      const double v = X[n * D + q] - X[q];
+      const double x = X[n * D + q];
+      Xd[s * D + q] = x;
+      const double v = x - X[q];
       xf[q] = static_cast<float>(v);
       m = fmax(m, fabs(v));
     }
@@ -114,11 +116,12 @@ __device__ inline bool knn_less(double a, int ia, double b, int ib) {
   return a < b || (a == b && ia < ib);
 }
 
-// Bitonic sort of H*64 (d2, idx) pairs held in registers, element
-// i = h*64 + lane: strides < 64 exchange across lanes (shuffles), stride >= 64
-// within a lane.
+// Bitonic sort of H*64 (d2, idx) pairs held in registers (with the
+// candidates' sorted positions as payload), element i = h*64 + lane: strides
+// < 64 exchange across lanes (shuffles), stride >= 64 within a lane.
 template <int H>
-__device__ inline void reg_bitonic(double (&v)[H], int (&ix)[H], int lane) {
+__device__ inline void reg_bitonic(double (&v)[H], int (&ix)[H], int (&ps)[H],
+                                   int lane) {
 #pragma unroll
   for (int size = 2; size <= H * 64; size <<= 1) {
 #pragma unroll
@@ -139,6 +142,9 @@ __device__ inline void reg_bitonic(double (&v)[H], int (&ix)[H], int lane) {
             const int ti = ix[h];
             ix[h] = ix[g];
             ix[g] = ti;
+            const int tp = ps[h];
+            ps[h] = ps[g];
+            ps[g] = tp;
           }
         }
       } else {
@@ -149,12 +155,14 @@ __device__ inline void reg_bitonic(double (&v)[H], int (&ix)[H], int lane) {
           const bool lower = (lane & stride) == 0;
           const double pv = __shfl_xor(v[h], stride, 64);
           const int pi = __shfl_xor(ix[h], stride, 64);
+          const int pp = __shfl_xor(ps[h], stride, 64);
           // the lower element keeps the min when ascending
           const bool p_less = knn_less(pv, pi, v[h], ix[h]);
           const bool take = (lower == up) ? p_less : !p_less;
           if (take) {
             v[h] = pv;
             ix[h] = pi;
+            ps[h] = pp;
           }
         }
       }
@@ -175,30 +183,36 @@ __device__ inline double knn_exact_d2(const double* __restrict__ X, int64_t i,
   return d2;
 }
 
-// Sort one row's candidate buffer (cnt indices) by exact distance; keep the
-// first k (written back), return tau = the k-th exact distance; with out
-// pointers, write the final neighbours instead.
+// Sort one row's candidate buffer (cnt sorted positions) by exact distance
+// and original index; keep the first k (written back), return tau = the k-th
+// exact distance; with out pointers, write the final neighbours (original
+// indices) instead.  The exact distances read the fp64 coordinates in the
+// spatial order (Xd: the same values as X, so the same d2), where a tile's
+// candidates are contiguous.
 template <int D, int H>
-__device__ inline double knn_sort_cut(const double* __restrict__ X,
-                                      int64_t row, int* __restrict__ buf,
+__device__ inline double knn_sort_cut(const double* __restrict__ Xd,
+                                      const int32_t* __restrict__ perm,
+                                      int64_t rs, int* __restrict__ buf,
                                       int cnt, int k, int lane,
                                       int32_t* __restrict__ out_idx,
                                       double* __restrict__ out_d2) {
   double v[H];
-  int ix[H];
+  int ix[H], ps[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     const int i = h * 64 + lane;
     if (i < cnt) {
-      ix[h] = buf[i];
+      ps[h] = buf[i];
+      ix[h] = perm[ps[h]];
       // the row itself passes the filter (d2f = 0); it ranks last
-      v[h] = ix[h] == row ? INFINITY : knn_exact_d2<D>(X, row, ix[h]);
+      v[h] = ps[h] == rs ? INFINITY : knn_exact_d2<D>(Xd, rs, ps[h]);
     } else {
       ix[h] = 0x7fffffff;
+      ps[h] = 0;
       v[h] = INFINITY;
     }
   }
-  reg_bitonic<H>(v, ix, lane);
+  reg_bitonic<H>(v, ix, ps, lane);
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int h = 0; h < H; ++h) {
@@ -208,7 +222,7 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
         out_idx[i] = ix[h];
         if (out_d2) out_d2[i] = v[h];
       } else {
-        buf[i] = ix[h];
+        buf[i] = ps[h];
       }
     }
   }
@@ -222,7 +236,7 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
   return __shfl(tk, lk, 64);
 }
 
-// One wave per R rows (R consecutive rows of the Morton order), no block
+// One wave per R rows (R consecutive rows of the Hilbert order), no block
 // barriers.  Candidates stream tile by tile (64 sorted positions, one per
 // lane; fp32 centred coordinates) against the wave's rows (packed-fp32
 // pairs in VGPRs); lanes passing the fp32 filter append the candidate's
@@ -237,19 +251,28 @@ __device__ inline double knn_sort_cut(const double* __restrict__ X,
 // scan.  The per-step test is ONE compare per row: padding positions carry
 // coordinates whose d2f is +inf, rows past the list a threshold of -inf, and
 // the row itself (d2f = 0) is dropped by the exact ranking (knn_sort_cut).
+// The wave's steps are a dependent chain (each may move the thresholds), so
+// the loop keeps the NEXT streamed tile's coordinates (and the next chunk's
+// boxes) in flight while it computes the current one: without that every
+// step waits one memory latency (C4: knn_kernel 3.2 ms).
+template <int D>
+__device__ inline void knn_load(const float* __restrict__ Xs, int t, int lane,
+                                float (&x)[D]) {
+  const int64_t j = static_cast<int64_t>(t) * kTile + lane;
+#pragma unroll
+  for (int q = 0; q < D; ++q) x[q] = Xs[j * D + q];
+}
+
 template <int D, int H, int R>
-__device__ inline void knn_step(const float* __restrict__ Xs,
+__device__ inline void knn_step(const float (&xj)[D],
                                 const int32_t* __restrict__ perm,
-                                const double* __restrict__ X, int t,
+                                const double* __restrict__ Xd, int t,
                                 const f32x2 (&xrf)[R / 2][D], float (&Tf)[R],
-                                int (&cnt)[R], const int64_t (&row)[R],
+                                int (&cnt)[R], const int64_t (&rs)[R],
                                 int (&buf)[R][H * 64], int k, double A,
                                 int lane) {
   constexpr int CAP = H * 64;
   const int64_t j = static_cast<int64_t>(t) * kTile + lane;
-  float xj[D];
-#pragma unroll
-  for (int q = 0; q < D; ++q) xj[q] = Xs[j * D + q];
   float d2f[R];
 #pragma unroll
   for (int p = 0; p < R / 2; ++p) {
@@ -270,27 +293,26 @@ __device__ inline void knn_step(const float* __restrict__ Xs,
     any |= m[r];
   }
   if (!any) return;
-  const int jo = perm[j];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (!m[r]) continue;
     bool cand = d2f[r] < Tf[r];
     if (cnt[r] + __popcll(m[r]) > CAP) {
-      const double tau = knn_sort_cut<D, H>(X, row[r], buf[r], cnt[r], k, lane,
-                                            nullptr, nullptr);
+      const double tau = knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k,
+                                            lane, nullptr, nullptr);
       cnt[r] = k;
       Tf[r] = knn_filter_bound(tau, D, A);
       cand = cand && d2f[r] < Tf[r];
       m[r] = __ballot(cand);
     }
-    if (cand) buf[r][cnt[r] + __popcll(m[r] & ((1ull << lane) - 1ull))] = jo;
+    if (cand) buf[r][cnt[r] + __popcll(m[r] & ((1ull << lane) - 1ull))] = static_cast<int>(j);
     cnt[r] += __popcll(m[r]);
   }
 }
 
 template <int D, int H, int R>
 __global__ __launch_bounds__(64) void knn_kernel(
-    const double* __restrict__ X, const float* __restrict__ Xs,
+    const double* __restrict__ Xd, const float* __restrict__ Xs,
     const int32_t* __restrict__ perm, const float* __restrict__ tbox, int T,
     const unsigned long long* __restrict__ amax, int k,
     const int32_t* __restrict__ rows, const int* __restrict__ nrows_p,
@@ -306,13 +328,14 @@ __global__ __launch_bounds__(64) void knn_kernel(
 
   f32x2 xrf[R / 2][D];   // rows in pairs for packed fp32 math
   float xr[R][D];
-  int64_t row[R];
+  int64_t row[R], rs[R];
   float Tf[R];
   int cnt[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t li = w0 + r < nrows ? w0 + r : nrows - 1;
     const int64_t sp = rows[li];
+    rs[r] = sp;
     row[r] = perm[sp];
 #pragma unroll
     for (int q = 0; q < D; ++q) xr[r][q] = Xs[sp * D + q];
@@ -327,21 +350,55 @@ __global__ __launch_bounds__(64) void knn_kernel(
   const int home = static_cast<int>(rows[w0] / kTile);
   const int wlo = home > 0 ? home - 1 : 0;
   const int whi = home + 1 < T ? home + 1 : T - 1;
-  for (int t = wlo; t <= whi; ++t)
-    knn_step<D, H, R>(Xs, perm, X, t, xrf, Tf, cnt, row, buf, k, A, lane);
+  float xc[D], xn[D];
+  knn_load<D>(Xs, wlo, lane, xc);
+  for (int t = wlo; t <= whi; ++t) {
+    if (t < whi) knn_load<D>(Xs, t + 1, lane, xn);
+    knn_step<D, H, R>(xc, perm, Xd, t, xrf, Tf, cnt, rs, buf, k, A, lane);
+#pragma unroll
+    for (int q = 0; q < D; ++q) xc[q] = xn[q];
+  }
+  // chunk boxes: lane l holds tile tb + l's box, the next chunk's in flight
+  float blo[D], bhi[D], nlo[D], nhi[D];
+  auto load_box = [&](int tb, float (&lo)[D], float (&hi)[D]) {
+    const int t = tb + lane < T ? tb + lane : T - 1;
+    const float* b = tbox + static_cast<int64_t>(t) * 2 * D;
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      lo[q] = b[q];
+      hi[q] = b[D + q];
+    }
+  };
+  load_box(0, nlo, nhi);
   for (int tb = 0; tb < T; tb += 64) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      blo[q] = nlo[q];
+      bhi[q] = nhi[q];
+    }
+    if (tb + 64 < T) load_box(tb + 64, nlo, nhi);
     const int t = tb + lane;
     bool need = false;
     if (t < T && (t < wlo || t > whi)) {
-      const float* lo = tbox + static_cast<int64_t>(t) * 2 * D;
 #pragma unroll
-      for (int r = 0; r < R; ++r) need = need || box_dist2<D>(xr[r], lo, lo + D) < Tf[r];
+      for (int r = 0; r < R; ++r) need = need || box_dist2<D>(xr[r], blo, bhi) < Tf[r];
     }
     uint64_t mask = __ballot(need);
-    while (mask) {
-      const int tt = tb + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      knn_step<D, H, R>(Xs, perm, X, tt, xrf, Tf, cnt, row, buf, k, A, lane);
+    if (!mask) continue;
+    int tt = tb + __builtin_ctzll(mask);
+    mask &= mask - 1;
+    knn_load<D>(Xs, tt, lane, xc);
+    for (;;) {
+      const int tn = mask ? tb + __builtin_ctzll(mask) : -1;
+      if (mask) {
+        mask &= mask - 1;
+        knn_load<D>(Xs, tn, lane, xn);
+      }
+      knn_step<D, H, R>(xc, perm, Xd, tt, xrf, Tf, cnt, rs, buf, k, A, lane);
+      if (tn < 0) break;
+      tt = tn;
+#pragma unroll
+      for (int q = 0; q < D; ++q) xc[q] = xn[q];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -349,7 +406,8 @@ __global__ __launch_bounds__(64) void knn_kernel(
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (w0 + r < nrows)
-      knn_sort_cut<D, H>(X, row[r], buf[r], cnt[r], k, lane, nbr + (row[r] - rlo) * k,
+      knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k, lane,
+                         nbr + (row[r] - rlo) * k,
                          nbr_d2 ? nbr_d2 + (row[r] - rlo) * k : nullptr);
   }
 }
@@ -438,6 +496,18 @@ __device__ inline double lu_det_inv(double (&a)[D][D], double (&inv)[D][D],
   return det;
 }
 
+// cov/det/inv: kCovLanes lanes per particle share its k neighbour gathers
+// (one thread per particle ran 0.9 ms at C4's N = 2e5, d = 6, k = 50: three
+// dependent gather chains of k steps each at ~3 waves per SIMD).
+constexpr int kCovLanes = 8;
+
+__device__ inline double cov_group_sum(double v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
 template <int D, bool EXACT>
 __global__ __launch_bounds__(128) void local_cov_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
@@ -445,39 +515,49 @@ __global__ __launch_bounds__(128) void local_cov_kernel(
     int64_t rlo, int64_t rhi, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets) {
   const int d = EXACT ? D : d_arg;
-  // particles [rlo, rhi); nbr and the outputs are indexed from rlo
-  const int64_t n = rlo + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (n >= rhi) return;
+  // particles [rlo, rhi), kCovLanes lanes per particle (lane s takes the
+  // neighbours t = s, s + 8, ...; the partial sums meet in a fixed xor
+  // tree, identical on every lane of the group); nbr and the outputs are
+  // indexed from rlo
+  const int sub = threadIdx.x & (kCovLanes - 1);
+  const int64_t n = rlo + (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) /
+                              kCovLanes;
+  if (rlo + (static_cast<int64_t>(blockIdx.x) * blockDim.x) / kCovLanes >= rhi) return;
+  const bool live = n < rhi;
+  const int64_t nn = live ? n : rhi - 1;  // idle groups still join the shuffles
   nbr -= rlo * k;
   covs -= rlo * d * d;
   invs -= rlo * d * d;
   dets -= rlo;
   double xn[D];
 #pragma unroll
-  for (int q = 0; q < d; ++q) xn[q] = X[n * d + q];
+  for (int q = 0; q < d; ++q) xn[q] = X[nn * d + q];
   // local weights lw = w[nbr] / sum
   double sw = 0.0;
-  for (int t = 0; t < k; ++t) sw += w[nbr[n * k + t]];
+  for (int t = sub; t < k; t += kCovLanes) sw += w[nbr[nn * k + t]];
+  sw = cov_group_sum(sw);
   double v1 = 0.0, v2 = 0.0, mu[D];
 #pragma unroll
   for (int q = 0; q < d; ++q) mu[q] = 0.0;
-  for (int t = 0; t < k; ++t) {
-    const int64_t j = nbr[n * k + t];
+  for (int t = sub; t < k; t += kCovLanes) {
+    const int64_t j = nbr[nn * k + t];
     const double lw = w[j] / sw;
     v1 += lw;
     v2 += lw * lw;
 #pragma unroll
     for (int q = 0; q < d; ++q) mu[q] = fma(lw, X[j * d + q] - xn[q], mu[q]);
   }
+  v1 = cov_group_sum(v1);
+  v2 = cov_group_sum(v2);
 #pragma unroll
-  for (int q = 0; q < d; ++q) mu[q] /= v1;
+  for (int q = 0; q < d; ++q) mu[q] = cov_group_sum(mu[q]) / v1;
   double C[D][D];
 #pragma unroll
   for (int a = 0; a < d; ++a)
 #pragma unroll
     for (int b = 0; b < d; ++b) C[a][b] = 0.0;
-  for (int t = 0; t < k; ++t) {
-    const int64_t j = nbr[n * k + t];
+  for (int t = sub; t < k; t += kCovLanes) {
+    const int64_t j = nbr[nn * k + t];
     const double lw = w[j] / sw;
     double dl[D];
 #pragma unroll
@@ -487,6 +567,11 @@ __global__ __launch_bounds__(128) void local_cov_kernel(
 #pragma unroll
       for (int b = a; b < d; ++b) C[a][b] = fma(lw * dl[a], dl[b], C[a][b]);
   }
+#pragma unroll
+  for (int a = 0; a < d; ++a)
+#pragma unroll
+    for (int b = a; b < d; ++b) C[a][b] = cov_group_sum(C[a][b]);
+  if (!live || sub != 0) return;
   double fact = v1 - v2 / v1;
   if (fact <= 0.0) fact = 0.0;
   double csum = 0.0;
@@ -688,10 +773,12 @@ int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
 
 size_t abc_knn_workspace_bytes(int64_t N, int k) {
   (void)k;
-  // amax | rows[N] | fp32 sorted coordinates [T*64][8] | spatial index
+  // amax | rows[N] | fp32 sorted centred coordinates [T*64][8] | fp64
+  // sorted coordinates [T*64][8] | spatial index
   const int64_t T = ceil_div(N > 0 ? N : 1, kTile);
   return 256 + al256(static_cast<size_t>(N > 0 ? N : 1) * 4) +
-         al256(static_cast<size_t>(T) * kTile * 8 * 4) + spatial_ws_bytes(N > 0 ? N : 1);
+         al256(static_cast<size_t>(T) * kTile * 8 * 4) +
+         al256(static_cast<size_t>(T) * kTile * 8 * 8) + spatial_ws_bytes(N > 0 ? N : 1);
 }
 
 int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
@@ -715,21 +802,21 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
   const int64_t T = ceil_div(N, kTile);
   float* Xs = reinterpret_cast<float*>(q);
   q += al256(static_cast<size_t>(T) * kTile * 8 * 4);
+  double* Xd = reinterpret_cast<double*>(q);
+  q += al256(static_cast<size_t>(T) * kTile * 8 * 8);
   SpatialWs v = spatial_ws(q, N);
   ABC_HIP(hipMemsetAsync(amax, 0, 8, st));
-  // rows per wave: kKnnRows, or 2 / 8 / 16 (tuning knob ABC_KNN_ROWS; the
-  // neighbour sets, order and distances are the same)
+  // rows per wave: kKnnRows, or 8 (tuning knob ABC_KNN_ROWS; the neighbour
+  // sets, order and distances are the same; 2 and 16 measured slower)
   const int rpw = tuning_knob(kKnobKnnRows, kKnnRows);
   const int64_t rlo = row0, rhi = row0 + nrows;
 #define KNN_R(DD, H, RR)                                                          \
   hipLaunchKernelGGL((knn_kernel<DD, H, RR>), dim3(ceil_div(nrows, RR)), dim3(64), \
-                     0, st, X, Xs, v.perm, v.tbox, v.T, amax, k, rows, v.count,   \
+                     0, st, Xd, Xs, v.perm, v.tbox, v.T, amax, k, rows, v.count,  \
                      rlo, nbr, nbr_d2)
 #define KNN(DD, H)                                                               \
   do {                                                                           \
-    if (rpw == 16) KNN_R(DD, H, 16);                                             \
-    else if (rpw == 8) KNN_R(DD, H, 8);                                          \
-    else if (rpw == 2) KNN_R(DD, H, 2);                                          \
+    if (rpw == 8) KNN_R(DD, H, 8);                                               \
     else KNN_R(DD, H, kKnnRows);                                                 \
   } while (0)
 #define L(DD)                                                                    \
@@ -737,7 +824,7 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
     const int rc = spatial_sort_population<DD>(X, N, v, st);                     \
     if (rc != kOk) return rc;                                                    \
     hipLaunchKernelGGL((knn_prep_kernel<DD>), dim3(ceil_div(T, 4)), dim3(256), 0, \
-                       st, X, N, v.perm, v.T, Xs, v.tbox, amax);                 \
+                       st, X, N, v.perm, v.T, Xs, Xd, v.tbox, amax);             \
     hipLaunchKernelGGL(sp_rows_in_range_kernel, dim3(ceil_div(N, 256)), dim3(256), \
                        0, st, v.perm, N, rlo, rhi, rows, v.count);               \
     if (k <= 64) KNN(DD, 2); else KNN(DD, 4);                                    \
@@ -771,7 +858,7 @@ int abc_local_cov_rows_f64(const double* X, const double* w, int64_t N, int d,
   ABC_REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= N,
               "local_cov: rows outside [0, N)");
   if (nrows == 0) return kOk;
-  const unsigned g = static_cast<unsigned>(ceil_div(nrows, 128));
+  const unsigned g = static_cast<unsigned>(ceil_div(nrows * kCovLanes, 128));
   const int64_t rlo = row0, rhi = row0 + nrows;
 #define L(DD, EX)                                                                \
   hipLaunchKernelGGL((local_cov_kernel<DD, EX>), dim3(g), dim3(128), 0, st, X, w, \
@@ -936,3 +1023,10 @@ int abc_local_cov_f32(const float* X, const float* w, int64_t N, int d,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_local() { return preload_kernel(local_sumw_part_kernel); }
+}  // namespace abc

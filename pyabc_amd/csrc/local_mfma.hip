@@ -701,3 +701,10 @@ int abc_local_logpdf_mfma(const double* pts, int64_t M, const double* X,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_local_mfma() { return preload_kernel(local_sumw_part_kernel); }
+}  // namespace abc

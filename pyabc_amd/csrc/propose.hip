@@ -1094,3 +1094,10 @@ int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_propose() { return preload_kernel(cdf_tile_sum_kernel); }
+}  // namespace abc

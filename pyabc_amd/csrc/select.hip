@@ -2246,3 +2246,10 @@ int abc_weighted_moments_f32(const float* X, const float* w, int64_t n, int d,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_select() { return preload_kernel(partial_sum_kernel); }
+}  // namespace abc

@@ -1,4 +1,4 @@
-// Key/value radix sort used by the spatial index (spatial.hpp): Morton keys
+// Key/value radix sort used by the spatial index (spatial.hpp): Hilbert keys
 // of the particles (or of the evaluation points) with their indices.  Kept
 // in its own translation unit so that rocPRIM's templates compile once
 // (declared in spatial.hpp).

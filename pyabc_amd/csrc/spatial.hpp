@@ -1,10 +1,13 @@
 // Spatial index of a particle population for the LocalTransition kNN
 // (cKDTree(X).query(X, k + 1), local_transition.py:82-83).
 //
-// The population is put in Morton order (d coordinates quantised to
-// b = min(21, 63 / d) bits each on the population's bounding box, keys
-// radix-sorted with their indices) and cut into tiles of 64 consecutive
-// particles.  A tile carries the bounding box of its fp32 centred
+// The population is put in Hilbert order (d coordinates quantised to
+// b = min(21, 63 / d) bits each on the population's bounding box, Skilling's
+// transpose form of the Hilbert index, keys radix-sorted with their indices)
+// and cut into tiles of 64 consecutive particles.  Hilbert order has no
+// jumps, so a tile's box is tighter than under Morton order: a numpy count at
+// C4's shape (N = 2e5, d = 6, k = 50, 4 rows per wave) needs 238 instead of
+// 377 tiles per wave at the final thresholds.  A tile carries the bounding box of its fp32 centred
 // coordinates (x - X[0], the same rounding the kNN filter computes with).
 // The kNN skips a tile for a query row when the box distance, computed with
 // the filter's own rounded operations (rounding is monotone), is not below
@@ -83,7 +86,9 @@ __global__ __launch_bounds__(256) void sp_extent_kernel(
   }
 }
 
-// Morton key of the points P[n][D] in the frame of X (clamped to the grid).
+// Hilbert key of the points P[n][D] in the frame of X (clamped to the grid):
+// J. Skilling, "Programming the Hilbert curve" (AIP Conf. Proc. 707, 2004),
+// AxesToTranspose, then the transposed index interleaved into one key.
 template <int D>
 __global__ __launch_bounds__(256) void sp_key_kernel(
     const double* __restrict__ P, int64_t n, const double* __restrict__ X,
@@ -102,6 +107,27 @@ __global__ __launch_bounds__(256) void sp_key_kernel(
     v = v > 0.0 ? (v < cells ? v : cells) : 0.0;  // NaN -> 0
     c[q] = static_cast<uint64_t>(v);
   }
+  constexpr uint64_t M = 1ull << (B - 1);
+  for (uint64_t Q = M; Q > 1; Q >>= 1) {  // inverse undo
+    const uint64_t P1 = Q - 1;
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      if (c[q] & Q) {
+        c[0] ^= P1;
+      } else {
+        const uint64_t t = (c[0] ^ c[q]) & P1;
+        c[0] ^= t;
+        c[q] ^= t;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 1; q < D; ++q) c[q] ^= c[q - 1];  // Gray encode
+  uint64_t tg = 0;
+  for (uint64_t Q = M; Q > 1; Q >>= 1)
+    if (c[D - 1] & Q) tg ^= Q - 1;
+#pragma unroll
+  for (int q = 0; q < D; ++q) c[q] ^= tg;
   uint64_t key = 0;
 #pragma unroll
   for (int b = B - 1; b >= 0; --b)
@@ -193,7 +219,7 @@ inline SpatialWs spatial_ws(void* ws, int64_t n) {
   return v;
 }
 
-// Morton order of X (spatial.hpp): ext, keys, sort -> keys_out / perm (the
+// Hilbert order of X (spatial.hpp): ext, keys, sort -> keys_out / perm (the
 // padding positions of the last tile map to particle 0).
 template <int D>
 int spatial_sort_population(const double* X, int64_t N, SpatialWs& v,

@@ -332,3 +332,10 @@ int abc_tempered_sums_f64(const double* pd, const double* w,
 }
 
 }  // extern "C"
+
+namespace abc {
+// Loads this translation unit's code object (HIP loads each one lazily, at
+// the first launch of one of its kernels: ~4 ms for local_mfma's inside
+// C4's first weighted generation); abc_preload calls every unit's hook.
+int preload_stochastic() { return preload_kernel(stochastic_kernel_kernel<0>); }
+}  // namespace abc

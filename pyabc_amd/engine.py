@@ -506,6 +506,9 @@ class GenerationEngine:
         self.timers = {}
         self.kde_events = None   # list -> (start, end, M, N) per KDE launch
         self.max_rounds = None
+        # load the library's code objects now, not inside the first
+        # generation that launches a unit's kernels (abc_preload)
+        K.preload()
 
     # ------------------------------------------------------------------
     def _sid(self, t, kind):

@@ -207,6 +207,23 @@ def reload_tuning():
     nat.lib().abc_tuning_reload()
 
 
+_PRELOADED = set()
+
+
+def preload():
+    """Load every translation unit's code object on the current device
+    (abc_preload; HIP otherwise loads one at its first kernel launch, e.g.
+    ~4 ms for the LocalTransition density pass inside C4's first weighted
+    generation).  Once per device."""
+    dev = torch.cuda.current_device()
+    if dev in _PRELOADED:
+        return
+    rc = nat.lib().abc_preload()
+    if rc:
+        raise RuntimeError(f"abc_preload: {rc} code objects did not load")
+    _PRELOADED.add(dev)
+
+
 def psd_whitening(cov):
     """scipy _PSD semantics on the host (d x d): U, rank, log_pdet."""
     cov = np.asarray(cov, dtype=np.float64)

@@ -22,7 +22,7 @@ def main():
     X *= torch.linspace(0.5, 2.0, d, dtype=torch.float64, device="cuda")
     base = None
     for rnd in range(3):
-        for rpw in ("4", "2", "8"):
+        for rpw in ("4", "8"):
             os.environ["ABC_KNN_ROWS"] = rpw
             K.reload_tuning()
             nbr, d2 = K.knn(X, k)

@@ -251,10 +251,9 @@ __device__ inline double knn_sort_cut(const double* __restrict__ Xd,
 // scan.  The per-step test is ONE compare per row: padding positions carry
 // coordinates whose d2f is +inf, rows past the list a threshold of -inf, and
 // the row itself (d2f = 0) is dropped by the exact ranking (knn_sort_cut).
-// The wave's steps are a dependent chain (each may move the thresholds), so
-// the loop keeps the NEXT streamed tile's coordinates (and the next chunk's
-// boxes) in flight while it computes the current one: without that every
-// step waits one memory latency (C4: knn_kernel 3.2 ms).
+// The kernel is VALU-bound (PMC at C4's shape: VALU busy ~90 % of the
+// cycles, ~4.5e4 VALU per wave, a third of them in the ~5 re-rankings per
+// row); keeping the next tile's coordinates in flight measured no faster.
 template <int D>
 __device__ inline void knn_load(const float* __restrict__ Xs, int t, int lane,
                                 float (&x)[D]) {
@@ -350,55 +349,25 @@ __global__ __launch_bounds__(64) void knn_kernel(
   const int home = static_cast<int>(rows[w0] / kTile);
   const int wlo = home > 0 ? home - 1 : 0;
   const int whi = home + 1 < T ? home + 1 : T - 1;
-  float xc[D], xn[D];
-  knn_load<D>(Xs, wlo, lane, xc);
+  float xj[D];
   for (int t = wlo; t <= whi; ++t) {
-    if (t < whi) knn_load<D>(Xs, t + 1, lane, xn);
-    knn_step<D, H, R>(xc, perm, Xd, t, xrf, Tf, cnt, rs, buf, k, A, lane);
-#pragma unroll
-    for (int q = 0; q < D; ++q) xc[q] = xn[q];
+    knn_load<D>(Xs, t, lane, xj);
+    knn_step<D, H, R>(xj, perm, Xd, t, xrf, Tf, cnt, rs, buf, k, A, lane);
   }
-  // chunk boxes: lane l holds tile tb + l's box, the next chunk's in flight
-  float blo[D], bhi[D], nlo[D], nhi[D];
-  auto load_box = [&](int tb, float (&lo)[D], float (&hi)[D]) {
-    const int t = tb + lane < T ? tb + lane : T - 1;
-    const float* b = tbox + static_cast<int64_t>(t) * 2 * D;
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      lo[q] = b[q];
-      hi[q] = b[D + q];
-    }
-  };
-  load_box(0, nlo, nhi);
   for (int tb = 0; tb < T; tb += 64) {
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-      blo[q] = nlo[q];
-      bhi[q] = nhi[q];
-    }
-    if (tb + 64 < T) load_box(tb + 64, nlo, nhi);
     const int t = tb + lane;
     bool need = false;
     if (t < T && (t < wlo || t > whi)) {
+      const float* lo = tbox + static_cast<int64_t>(t) * 2 * D;
 #pragma unroll
-      for (int r = 0; r < R; ++r) need = need || box_dist2<D>(xr[r], blo, bhi) < Tf[r];
+      for (int r = 0; r < R; ++r) need = need || box_dist2<D>(xr[r], lo, lo + D) < Tf[r];
     }
     uint64_t mask = __ballot(need);
-    if (!mask) continue;
-    int tt = tb + __builtin_ctzll(mask);
-    mask &= mask - 1;
-    knn_load<D>(Xs, tt, lane, xc);
-    for (;;) {
-      const int tn = mask ? tb + __builtin_ctzll(mask) : -1;
-      if (mask) {
-        mask &= mask - 1;
-        knn_load<D>(Xs, tn, lane, xn);
-      }
-      knn_step<D, H, R>(xc, perm, Xd, tt, xrf, Tf, cnt, rs, buf, k, A, lane);
-      if (tn < 0) break;
-      tt = tn;
-#pragma unroll
-      for (int q = 0; q < D; ++q) xc[q] = xn[q];
+    while (mask) {
+      const int tt = tb + __builtin_ctzll(mask);
+      mask &= mask - 1;
+      knn_load<D>(Xs, tt, lane, xj);
+      knn_step<D, H, R>(xj, perm, Xd, tt, xrf, Tf, cnt, rs, buf, k, A, lane);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

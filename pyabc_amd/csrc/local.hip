@@ -27,7 +27,7 @@ namespace abc {
 
 constexpr int kKnnRows = 4;     // rows per wave (one wave per block; 8 before
                                 // round 5: 7.6 -> 6.1 ms, tools/knn_ab.py)
-constexpr int kMaxK = 192;      // buffer of 256 = k kept + 64 appended
+constexpr int kMaxK = 192;      // k > 64: buffer of 256 = k kept + 64 appended
 
 // Separately rounded fp64 ops: hipcc contracts a*b+c into an FMA by default
 // (-ffp-contract=fast, and __dmul_rn/__dadd_rn are plain operators), so the
@@ -236,6 +236,57 @@ __device__ inline double knn_sort_cut(const double* __restrict__ Xd,
   return __shfl(tk, lk, 64);
 }
 
+// k <= 64 (H = 1): the row's best 64 (exact d2, index) pairs stay sorted in
+// registers (element i in lane i) and the passing candidates' sorted
+// positions collect in a 64-slot LDS buffer.  A full buffer is ranked by
+// exact distance (bitonic sort, descending) and merged into the kept set
+// (elementwise min of an ascending and a descending run is bitonic and holds
+// the 64 smallest of both; six merge stages sort it), which sets tau = the
+// k-th kept distance: 27 compare-exchange stages over one register per lane
+// instead of the 28 over two of a full 128-element re-rank, and the kept
+// pairs are never re-read or recomputed.
+__device__ inline void knn_cmpx(double& v, int& ix, int stride, bool up, int lane) {
+  const double pv = __shfl_xor(v, stride, 64);
+  const int pi = __shfl_xor(ix, stride, 64);
+  const bool lower = (lane & stride) == 0;
+  const bool p_less = knn_less(pv, pi, v, ix);
+  if ((lower == up) ? p_less : !p_less) {
+    v = pv;
+    ix = pi;
+  }
+}
+
+template <int D>
+__device__ inline double knn_merge(const double* __restrict__ Xd,
+                                   const int32_t* __restrict__ perm, int64_t rs,
+                                   const int* __restrict__ buf, int cnt, int k,
+                                   int lane, double& kv, int& ki) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  double v = INFINITY;
+  int ix = 0x7fffffff;
+  if (lane < cnt) {
+    const int ps = buf[lane];
+    ix = perm[ps];
+    // the row itself passes the filter (d2f = 0); it ranks last
+    v = ps == rs ? INFINITY : knn_exact_d2<D>(Xd, rs, ps);
+  }
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+      knn_cmpx(v, ix, stride, (lane & size) != 0, lane);  // descending
+  if (knn_less(v, ix, kv, ki)) {
+    kv = v;
+    ki = ix;
+  }
+#pragma unroll
+  for (int stride = 32; stride > 0; stride >>= 1) knn_cmpx(kv, ki, stride, true, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return __shfl(kv, k - 1, 64);
+}
+
 // One wave per R rows (R consecutive rows of the Hilbert order), no block
 // barriers.  Candidates stream tile by tile (64 sorted positions, one per
 // lane; fp32 centred coordinates) against the wave's rows (packed-fp32
@@ -268,8 +319,8 @@ __device__ inline void knn_step(const float (&xj)[D],
                                 const double* __restrict__ Xd, int t,
                                 const f32x2 (&xrf)[R / 2][D], float (&Tf)[R],
                                 int (&cnt)[R], const int64_t (&rs)[R],
-                                int (&buf)[R][H * 64], int k, double A,
-                                int lane) {
+                                int (&buf)[R][H * 64], double (&kv)[R],
+                                int (&ki)[R], int k, double A, int lane) {
   constexpr int CAP = H * 64;
   const int64_t j = static_cast<int64_t>(t) * kTile + lane;
   float d2f[R];
@@ -297,9 +348,15 @@ __device__ inline void knn_step(const float (&xj)[D],
     if (!m[r]) continue;
     bool cand = d2f[r] < Tf[r];
     if (cnt[r] + __popcll(m[r]) > CAP) {
-      const double tau = knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k,
-                                            lane, nullptr, nullptr);
-      cnt[r] = k;
+      double tau;
+      if constexpr (H == 1) {
+        tau = knn_merge<D>(Xd, perm, rs[r], buf[r], cnt[r], k, lane, kv[r], ki[r]);
+        cnt[r] = 0;
+      } else {
+        tau = knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k, lane, nullptr,
+                                 nullptr);
+        cnt[r] = k;
+      }
       Tf[r] = knn_filter_bound(tau, D, A);
       cand = cand && d2f[r] < Tf[r];
       m[r] = __ballot(cand);
@@ -328,6 +385,8 @@ __global__ __launch_bounds__(64) void knn_kernel(
   f32x2 xrf[R / 2][D];   // rows in pairs for packed fp32 math
   float xr[R][D];
   int64_t row[R], rs[R];
+  double kv[R];  // H = 1: the kept set, sorted across lanes
+  int ki[R];
   float Tf[R];
   int cnt[R];
 #pragma unroll
@@ -340,6 +399,8 @@ __global__ __launch_bounds__(64) void knn_kernel(
     for (int q = 0; q < D; ++q) xr[r][q] = Xs[sp * D + q];
     Tf[r] = w0 + r < nrows ? INFINITY : -INFINITY;
     cnt[r] = 0;
+    kv[r] = INFINITY;
+    ki[r] = 0x7fffffff;
   }
 #pragma unroll
   for (int p = 0; p < R / 2; ++p)
@@ -352,7 +413,7 @@ __global__ __launch_bounds__(64) void knn_kernel(
   float xj[D];
   for (int t = wlo; t <= whi; ++t) {
     knn_load<D>(Xs, t, lane, xj);
-    knn_step<D, H, R>(xj, perm, Xd, t, xrf, Tf, cnt, rs, buf, k, A, lane);
+    knn_step<D, H, R>(xj, perm, Xd, t, xrf, Tf, cnt, rs, buf, kv, ki, k, A, lane);
   }
   for (int tb = 0; tb < T; tb += 64) {
     const int t = tb + lane;
@@ -367,17 +428,27 @@ __global__ __launch_bounds__(64) void knn_kernel(
       const int tt = tb + __builtin_ctzll(mask);
       mask &= mask - 1;
       knn_load<D>(Xs, tt, lane, xj);
-      knn_step<D, H, R>(xj, perm, Xd, tt, xrf, Tf, cnt, rs, buf, k, A, lane);
+      knn_step<D, H, R>(xj, perm, Xd, tt, xrf, Tf, cnt, rs, buf, kv, ki, k, A, lane);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    if (w0 + r < nrows)
-      knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k, lane,
-                         nbr + (row[r] - rlo) * k,
-                         nbr_d2 ? nbr_d2 + (row[r] - rlo) * k : nullptr);
+    if constexpr (H == 1) {
+      if (w0 + r < nrows) {
+        if (cnt[r] > 0) knn_merge<D>(Xd, perm, rs[r], buf[r], cnt[r], k, lane, kv[r], ki[r]);
+        if (lane < k) {
+          nbr[(row[r] - rlo) * k + lane] = ki[r];
+          if (nbr_d2) nbr_d2[(row[r] - rlo) * k + lane] = kv[r];
+        }
+      }
+    } else {
+      if (w0 + r < nrows)
+        knn_sort_cut<D, H>(Xd, perm, rs[r], buf[r], cnt[r], k, lane,
+                           nbr + (row[r] - rlo) * k,
+                           nbr_d2 ? nbr_d2 + (row[r] - rlo) * k : nullptr);
+    }
   }
 }
 
@@ -796,7 +867,7 @@ int abc_knn_rows_f64(const double* X, int64_t N, int d, int k, int64_t row0,
                        st, X, N, v.perm, v.T, Xs, Xd, v.tbox, amax);             \
     hipLaunchKernelGGL(sp_rows_in_range_kernel, dim3(ceil_div(N, 256)), dim3(256), \
                        0, st, v.perm, N, rlo, rhi, rows, v.count);               \
-    if (k <= 64) KNN(DD, 2); else KNN(DD, 4);                                    \
+    if (k <= 64) KNN(DD, 1); else KNN(DD, 4);                                    \
   }
   switch (d) {
     case 1: L(1) break;

@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -49,7 +50,11 @@ def main():
     mean = {k: sum(v) / len(v) for k, v in acc.items()}
     per_tile = {k: v / tiles for k, v in mean.items()
                 if k.startswith("SQ_") and k not in ("SQ_WAVES", "SQ_BUSY_CYCLES")}
-    out = {"kernel": kernel, "description": desc, "tiles_per_launch": tiles,
+    # d from the file name (bench.py kde_pmc: rNN_kde_pmc.json is d = 8,
+    # rNN_kde_dDD_pmc.json is d = DD)
+    md = re.search(r"_kde_d(\d+)_pmc\.json$", out_path)
+    out = {"kernel": kernel, "description": desc, "d": int(md.group(1)) if md else 8,
+           "tiles_per_launch": tiles,
            "passes": passes, "per_tile": per_tile,
            "units": "per tile; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in "
                     "quad-cycles per wave, SQ_VALU_MFMA_BUSY_CYCLES in cycles"}

@@ -956,15 +956,18 @@ def test_cdf_scan_sizes(K, n):
                                   ref.resample_cdf(w))
 
 
+@pytest.mark.parametrize("k", [50, 64, 150])
 @pytest.mark.parametrize("case", ["offset", "clustered", "d1", "d8"])
-def test_knn_fp32_filter_exact(K, case):
+def test_knn_fp32_filter_exact(K, case, k):
     """The fp32 candidate filter never drops a true neighbour: sets, order
     and distances equal an fp64 brute force (the reference's sub/mul/add
     sequence) on data far from the origin (large fp32 rounding of the
-    centred coordinates), near-duplicate clusters and d = 1 / 8."""
+    centred coordinates), near-duplicate clusters and d = 1 / 8; k <= 64
+    takes the register-resident merged top-64 (k = 64: tau is its last
+    element), k > 64 the 256-slot re-rank."""
     rng = np.random.default_rng({"offset": 1, "clustered": 2, "d1": 3,
                                  "d8": 4}[case])
-    n, d, k = 3000, 6, 50
+    n, d = 3000, 6
     if case == "offset":
         X = rng.normal(size=(n, d)) * 1e-3 + 1e3
         X[0] -= 5e3                         # x0 far away: large bound A

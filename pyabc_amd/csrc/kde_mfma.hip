@@ -1130,9 +1130,20 @@ constexpr int lds2g_waves(int KT, int IB, bool PIPE) {
 #ifndef ABC_KDE_STAGE_TILES
 #define ABC_KDE_STAGE_TILES 4
 #endif
-// (d > 8 keeps 2: a 4-tile stage of 9 fragments per tile is 72 KB of LDS,
-// two blocks per CU)
-constexpr int lds2g_stage_tiles(int KT) { return KT <= 4 ? ABC_KDE_STAGE_TILES : 2; }
+// d > 8 (KT = 9 / 10 fragments per tile): 4 tiles per stage too since
+// round 5 (72 / 80 KB of LDS per block, still two blocks per CU): at IB = 3,
+// N = M = 1e6, d = 20 the launch ran 199.4 / 201.5-201.9 ms (min / median)
+// against 200.8-200.9 / 203.6 ms with 2-tile stages, rows bit-identical
+// (tools/build_variant.sh + tools/lib_ab.py tools/kde_time.py, gpurun_out/
+// r05y).  Issuing the next stage's LDS-DMA pieces a share before each tile's
+// chain instead of all at the stage start measured slower at both d = 8
+// (116.1 vs 111.5 ms) and d = 20 (206.4 vs 200.9 ms) and was not kept.
+#ifndef ABC_KDE_STAGE_TILES_LARGE
+#define ABC_KDE_STAGE_TILES_LARGE 4
+#endif
+constexpr int lds2g_stage_tiles(int KT) {
+  return KT <= 4 ? ABC_KDE_STAGE_TILES : ABC_KDE_STAGE_TILES_LARGE;
+}
 
 // W: waves per block (4).  Measured and not kept (round 5): 8 waves per
 // block at d = 20, IB = 3 -- every wave's share of the LDS-DMA refill

@@ -870,13 +870,16 @@ def test_local_transition(K, name):
     np.testing.assert_allclose(np.exp(host(lp)), g["pdf"], rtol=1e-11)
 
 
-@pytest.mark.parametrize("d", [1, 4, 5, 7, 9])
-def test_local_cov_all_dims_vs_oracle(K, d):
+@pytest.mark.parametrize("d,k", [(1, 25), (4, 25), (5, 25), (7, 25), (9, 25),
+                                 (3, 1), (1, 3), (6, 9), (6, 64)])
+def test_local_cov_all_dims_vs_oracle(K, d, k):
     """local_cov_kernel's per-d register form (d <= 6) and its runtime-d
     form (d = 7..16) against the oracle's smart_cov / det / inv restatement
-    (local_transition.py:77-101) on dimensions the goldens do not cover."""
-    rng = np.random.default_rng(40 + d)
-    N, k = 700, 25
+    (local_transition.py:77-101) on dimensions the goldens do not cover;
+    k = 1 (smart_cov's diag(|delta|)), k below, near and above the 8 lanes
+    that share a particle's neighbours."""
+    rng = np.random.default_rng(40 + d + 100 * k)
+    N = 700
     X = rng.normal(size=(N, d)) * rng.uniform(0.5, 2.0, d)
     w = rng.uniform(0.5, 1.5, N)
     w /= w.sum()
@@ -985,6 +988,28 @@ def test_knn_fp32_filter_exact(K, case, k):
     diff = X[None, :, :] - X[:, None, :]
     D2 = np.zeros((n, n))
     for q in range(d):                        # sequential, no FMA
+        D2 = D2 + diff[:, :, q] * diff[:, :, q]
+    np.fill_diagonal(D2, np.inf)
+    order = np.lexsort((np.broadcast_to(np.arange(n), (n, n)), D2), axis=1)
+    want = order[:, :k]
+    np.testing.assert_array_equal(nbr, want)
+    np.testing.assert_array_equal(d2, np.take_along_axis(D2, want, axis=1))
+
+
+@pytest.mark.parametrize("n,k", [(2, 1), (11, 10), (65, 64), (65, 30),
+                                 (130, 100)])
+def test_knn_tiny_and_maximal_k(K, n, k):
+    """Edge sizes of the kNN pass: one partial tile, k = N - 1 (every other
+    particle is a neighbour), k at the 64-slot merge boundary and k > 64 on
+    the re-rank path; sets, order and distances equal the fp64 brute force."""
+    rng = np.random.default_rng(n * 1000 + k)
+    d = 3
+    X = rng.normal(size=(n, d))
+    nbr, d2 = K.knn(dev(X), k)
+    nbr, d2 = host(nbr), host(d2)
+    diff = X[None, :, :] - X[:, None, :]
+    D2 = np.zeros((n, n))
+    for q in range(d):
         D2 = D2 + diff[:, :, q] * diff[:, :, q]
     np.fill_diagonal(D2, np.inf)
     order = np.lexsort((np.broadcast_to(np.arange(n), (n, n)), D2), axis=1)

@@ -996,6 +996,18 @@ def test_knn_fp32_filter_exact(K, case, k):
     np.testing.assert_array_equal(d2, np.take_along_axis(D2, want, axis=1))
 
 
+def test_native_stream_follows_torch(K):
+    """The launch stream the C-ABI calls receive is torch's current stream,
+    inside and outside a side-stream context."""
+    from pyabc_amd import _native as nat
+    raw = lambda: nat.stream().value or 0  # NULL (the default stream) -> 0
+    assert raw() == torch.cuda.current_stream().cuda_stream
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        assert raw() == side.cuda_stream != 0
+    assert raw() == torch.cuda.current_stream().cuda_stream
+
+
 @pytest.mark.parametrize("n,k", [(2, 1), (11, 10), (65, 64), (65, 30),
                                  (130, 100)])
 def test_knn_tiny_and_maximal_k(K, n, k):

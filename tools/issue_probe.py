@@ -25,7 +25,9 @@ MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
          14: "mix 13 + 5 ds_read_b128 per step",
          15: "mix 13 + 5 ds_read_b128 per step + barrier every 4 steps",
          16: "mix 13 + 5 ds_read_b128 + barrier + 18-KiB LDS-DMA refill every 4 steps",
-         17: "mix 13 + 4 ds_read_b128 per step"}
+         17: "mix 13 + 4 ds_read_b128 per step",
+         18: "LocalTransition z form d=6 (lz_kernel): 3 MFMA, 2 v_exp_f32, 17 v_add_f32",
+         19: "LocalTransition z form d=6: 3 MFMA, 2 v_exp_f32, 19 v_add_f32"}
 
 
 def parse():

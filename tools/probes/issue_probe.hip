@@ -242,6 +242,11 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 15: ns = time_mem_mix<9, 16, 28, 5, 4, 0, 18>(waves_per_simd, iters, cus, out, src); break;
     case 16: ns = time_mem_mix<9, 16, 28, 5, 4, 1, 18>(waves_per_simd, iters, cus, out, src); break;
     case 17: ns = time_mem_mix<9, 16, 28, 4, 0, 0, 18>(waves_per_simd, iters, cus, out, src); break;
+    // LocalTransition z-form density (lz_kernel, d = 6): per (particle tile,
+    // point tile) product 3 MFMAs, 2 v_exp_f32 and 17 other VALU (12
+    // squares, 2 fma, 2 adds, the flush) -- 19 bounds the flush's share
+    case 18: ns = time_mix<3, 2, 17>(waves_per_simd, iters, cus, out); break;
+    case 19: ns = time_mix<3, 2, 19>(waves_per_simd, iters, cus, out); break;
     default: break;
   }
   (void)hipFree(src);

@@ -85,14 +85,14 @@ def run(name, abc, x0, names, theta_true=None, db=None, **run_kw):
     return out
 
 
-def c1():
+def c1(gens=10):
     np.random.seed(0)
     prior = pa.Distribution(mean=pa.RV("uniform", 0, 5))
     abc = pa.ABCSMC(pa.GaussianMeanModel(), prior, pa.PNormDistance(p=2),
                     population_size=1000, eps=pa.MedianEpsilon(),
                     sampler=pa.GPUBatchSampler(seed=1))
     run("c1_quickstart_N1000", abc, {"data": 2.5}, ["mean"], [2.5],
-        minimum_epsilon=0.1, max_nr_populations=10)
+        minimum_epsilon=0.1, max_nr_populations=gens)
 
 
 def c2(N=100_000, gens=6):

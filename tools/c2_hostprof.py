@@ -28,6 +28,7 @@ def main():
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("cumulative").print_stats(30)
+    st.sort_stats("tottime").print_stats(30)
     out = io.StringIO()
     st2 = pstats.Stats(pr, stream=out)
     st2.sort_stats("tottime").print_callers(

@@ -1522,7 +1522,9 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 // and any row the second pass still cannot resolve, take the exact fp64
 // fixup.  lo: the folded scheme's routing bound: a row
 // without an offset whose sum stays at or above lo keeps the derived bound
-// under 1e-5 / 1.5 -- 2^-24 where KL <= 2 lo MFMAs fold (d <= 4), 2^-12
+// under 1e-5 / 1.5 -- 2^-26 where KL <= 2 lo MFMAs fold (d <= 4: band rows
+// e_max in [-40, -16] bound at 5.2e-6 / 5.4e-6 / 6.2e-6 / 9.1e-6 for 2^-24 /
+// -26 / -28 / -30, tools/route_bound.py; 2^-24 until round 5), 2^-12
 // where KL = 3 (d = 6, 8; 2^-16 measured a 6.76e-6 bound on rows at
 // e = -16, tests/test_gpu_kde_band.py), 2^-4 where KL = 4 ... 8
 // (8 < d <= 24).  The split and bf16 schemes keep the 2^-32 of rounds 1-4.
@@ -1541,7 +1543,7 @@ struct Route {
   static constexpr bool kFold = Mk<D>::SCH == 2;
   static constexpr double lo =
       !kFold ? 0x1p-32
-             : (Mk<D>::KL <= 2 ? 0x1p-24 : (Mk<D>::KL <= 3 ? 0x1p-12 : 0x1p-4));
+             : (Mk<D>::KL <= 2 ? 0x1p-26 : (Mk<D>::KL <= 3 ? 0x1p-12 : 0x1p-4));
 };
 constexpr double kLn2d = 0.6931471805599453;
 constexpr int kListBlocks = 8192;  // (segment, row block) blocks of a list pass

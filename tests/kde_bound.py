@@ -50,14 +50,15 @@ def row_stats(Yp, lw, Y, off, KL, D, g, chunk=128):
     return {k: torch.cat(v).cpu().numpy() for k, v in out.items()}
 
 
-def pass_offsets(log2S, emax, m1, D):
+def pass_offsets(log2S, emax, m1, D, lo=None):
     """The offset each row ends up with in kde_mfma.hip: the pass-1 offset
     m1 while the sum relative to it lies in the routing range (Route for
     rows without an offset, [2^-16, 2^16] for rows with a parent offset),
     otherwise m1 + floor(log2 S') (S' in the normal range) or the max
     pass's m1 + floor(max e')."""
     KL = (5 * D + 4 + 15) // 16
-    lo = 2.0 ** -24 if KL <= 2 else (2.0 ** -12 if KL <= 3 else 2.0 ** -4)
+    if lo is None:  # kde_mfma.hip Route<D>::lo
+        lo = 2.0 ** -26 if KL <= 2 else (2.0 ** -12 if KL <= 3 else 2.0 ** -4)
     lS = log2S - m1
     keep = np.where(m1 == 0, lS >= math.log2(lo), (lS >= -16) & (lS <= 16))
     normal = (lS > -100) & (lS < 100)

@@ -540,9 +540,14 @@ __device__ inline int64_t search_right(const double* __restrict__ cdf, int64_t n
   return lo;
 }
 
-template <int D>
+// EXACT: d == D, so every loop bound and stride is a compile-time constant
+// (the shared factor's rows then load as wide scalar loads instead of one
+// dependent s_load per element).  The perturbation is accumulated row of A
+// by row (k outer), each component's fma chain in ascending k as before:
+// the same bits.
+template <int D, bool EXACT = false>
 __device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
-                                   int d, const double* __restrict__ cdf,
+                                   int d_arg, const double* __restrict__ cdf,
                                    double u, const double (&z)[D],
                                    const double* __restrict__ A,
                                    const double* __restrict__ lo,
@@ -552,17 +557,28 @@ __device__ inline void perturb_one(const double* __restrict__ X, int64_t N,
                                    int64_t a_stride = 0,
                                    const int64_t* __restrict__ tab = nullptr,
                                    int log2k = 0) {
+  const int d = EXACT ? D : d_arg;
   int64_t idx = search_right(cdf, N, u, tab, log2k);
   const int64_t idx_c = idx < N ? idx : N - 1;  // numpy would raise; u<1 always
   A += idx_c * a_stride;  // per-particle factor (LocalTransition) or shared
+  double pl[D];
+#pragma unroll
+  for (int l = 0; l < D; ++l) pl[l] = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    if (k < d) {
+      const double zk = z[k];
+      const double* __restrict__ Ak = A + k * d;
+#pragma unroll
+      for (int l = 0; l < D; ++l)
+        if (l < d) pl[l] = fma(zk, Ak[l], pl[l]);
+    }
+  }
   bool ok = true;
 #pragma unroll
   for (int l = 0; l < D; ++l) {
     if (l < d) {
-      double p = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k)
-        if (k < d) p = fma(z[k], A[k * d + l], p);
+      const double p = pl[l];
       const double th = X[idx_c * d + l] + p;
       theta_row[l] = th;
       if (lo) {
@@ -658,14 +674,21 @@ __global__ __launch_bounds__(256) void philox_fill_kernel(
 // Production proposals: u from stream (2*sid), z from stream (2*sid+1).
 //   u[b]   = philox_uniform(seed, 2*sid,   offset + b)
 //   z[b,k] = philox_normal (seed, 2*sid+1, (offset + b) * d + k)
-template <int D>
+template <int D, bool EXACT>
 __global__ __launch_bounds__(256) void propose_philox_kernel(
-    const double* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ X, int64_t N, int d_arg,
     const double* __restrict__ cdf, const double* __restrict__ A,
     const double* __restrict__ lo, const double* __restrict__ scale,
     uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
     double* __restrict__ theta, int64_t* __restrict__ idx,
     uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
+  const int d = EXACT ? D : d_arg;
+  // the shared factor A through LDS: read directly, the compiler hoists all
+  // d*d uniform elements into SGPRs and spills them to VGPR lanes (5344
+  // v_readlane per thread at d = 20; the waves waited ~95 % of their time)
+  __shared__ double As[D * D];
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) As[i] = A[i];
+  __syncthreads();
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint64_t ui = offset + static_cast<uint64_t>(b);
@@ -673,8 +696,8 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
   const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
   double zz[D];
   philox_normals<D>(seed, 2 * sid + 1, ui * static_cast<uint64_t>(d), d, zz);
-  perturb_one<D>(X, N, d, cdf, u, zz, A, lo, scale, theta + b * d, idx + b,
-                 sup + b, 0, tab, log2k);
+  perturb_one<D, EXACT>(X, N, d, cdf, u, zz, As, lo, scale, theta + b * d, idx + b,
+                        sup + b, 0, tab, log2k);
 }
 
 // bucket table of the CDF: tab[k] = searchsorted(cdf, k / 2^L, 'right')
@@ -975,12 +998,19 @@ int abc_propose_philox_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
               "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
-#define L(DD)                                                              \
-  hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \
-                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta, \
+#define LX(DD, EX)                                                              \
+  hipLaunchKernelGGL((propose_philox_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
                      idx, in_support, nullptr, 0);
+#define L(DD)                     \
+  if ((DD) <= 8 && d == (DD)) {   \
+    LX(DD, (DD) <= 8)             \
+  } else {                        \
+    LX(DD, false)                 \
+  }
   DISPATCH_D(d, L)
 #undef L
+#undef LX
   ABC_LAUNCH_CHECK("propose_philox_kernel");
   return kOk;
 }
@@ -1013,12 +1043,22 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
               "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
-#define L(DD)                                                              \
-  hipLaunchKernelGGL((propose_philox_kernel<DD>), dim3(g), dim3(256), 0, st, \
-                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta, \
+#define LX(DD, EX)                                                              \
+  hipLaunchKernelGGL((propose_philox_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
                      idx, in_support, tab, log2k);
+#define L(DD)                     \
+  if ((DD) <= 8 && d == (DD)) {   \
+    LX(DD, (DD) <= 8)             \
+  } else {                        \
+    LX(DD, false)                 \
+  }
+  // exact instantiations (compile-time d) for d <= 8; above, a
+  // compile-time d lets the scheduler interleave all d/2 Box-Muller pairs
+  // (512 VGPRs and scratch at d >= 16), so d > 8 keeps the runtime-d form
   DISPATCH_D(d, L)
 #undef L
+#undef LX
   ABC_LAUNCH_CHECK("propose_philox_kernel");
   return kOk;
 }

@@ -25,6 +25,12 @@
 namespace abc {
 
 
+// 1: the wave's query rows are held in VGPRs (uniform, the compiler put
+// them in SGPRs and the kernel sat at 100 SGPRs, spilling to VGPR lanes):
+// knn 4.10 -> 3.93 ms at C4's shape, interleaved (gpurun_out/r05ax)
+#ifndef ABC_KNN_XR_VGPR
+#define ABC_KNN_XR_VGPR 1
+#endif
 constexpr int kKnnRows = 4;     // rows per wave (one wave per block; 8 before
                                 // round 5: 7.6 -> 6.1 ms, tools/knn_ab.py)
 constexpr int kMaxK = 192;      // k > 64: buffer of 256 = k kept + 64 appended
@@ -396,7 +402,12 @@ __global__ __launch_bounds__(64) void knn_kernel(
     rs[r] = sp;
     row[r] = perm[sp];
 #pragma unroll
-    for (int q = 0; q < D; ++q) xr[r][q] = Xs[sp * D + q];
+    for (int q = 0; q < D; ++q) {
+      xr[r][q] = Xs[sp * D + q];
+#if ABC_KNN_XR_VGPR
+      asm volatile("" : "+v"(xr[r][q]));  // keep the rows out of the SGPRs
+#endif
+    }
     Tf[r] = w0 + r < nrows ? INFINITY : -INFINITY;
     cnt[r] = 0;
     kv[r] = INFINITY;

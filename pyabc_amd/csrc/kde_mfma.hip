@@ -98,6 +98,10 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
 #define ABC_KDE_SCHEME_LARGE 2
 #endif
 
+#ifndef ABC_KDE_IB_LARGE
+#define ABC_KDE_IB_LARGE 3
+#endif
+
 template <int D>
 struct Mk {
   static constexpr int SCH =
@@ -113,10 +117,10 @@ struct Mk {
   // read feeds three MFMAs instead of two -- the d = 20 probe ladder,
   // profiles/r05_issue_probe.json, prices a ds_read_b128 at ~9 ns per tile
   // step); 1 for the split scheme above d = 24
-  static constexpr int IB = D <= 24 ? 3 : 1;
+  static constexpr int IB = D <= 8 ? 3 : D <= 24 ? ABC_KDE_IB_LARGE : 1;
   // row padding unit in i-tiles per wave: every IB the launch may pick
   // (1, 2, 3) divides it
-  static constexpr int PADIB = D <= 24 ? 6 : IB;
+  static constexpr int PADIB = D <= 24 ? (D > 8 && IB == 4 ? 12 : 6) : IB;
 };
 
 __device__ inline unsigned short bf16_rne(float x) {
@@ -1094,10 +1098,13 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VALU) {
 #define ABC_GAP(TT) \
-  if (t == TT) fold_gap_ops<KT, IB, C * IB + TT>(prev, sacc);
+  if constexpr (TT < IB) if (t == TT) fold_gap_ops<KT, IB, C * IB + TT>(prev, sacc);
         ABC_GAP(0)
         ABC_GAP(1)
         ABC_GAP(2)
+        ABC_GAP(3)
+        ABC_GAP(4)
+        ABC_GAP(5)
 #undef ABC_GAP
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1117,6 +1124,7 @@ __device__ __forceinline__ void lds_chain_f(const bf16x8 (*Ab)[64], int tile, in
 #endif
 constexpr int lds2g_waves(int KT, int IB, bool PIPE) {
   return ABC_KDE_LDS2G_WAVES == 0 ? 1
+         : ABC_KDE_LDS2G_WAVES >= 2 && KT > 4 ? ABC_KDE_LDS2G_WAVES
          : (PIPE ? KT * IB <= 8 : KT * IB <= 12) ? 4
          : (!PIPE && KT * IB <= 18) ? 3 : 1;
 }
@@ -1159,7 +1167,7 @@ void kde_mfma_lds2g_kernel(
   constexpr int TPS = lds2g_stage_tiles(KT);  // 32-row tiles per LDS stage
   constexpr int CH = TPS * KT;
   static_assert(kFolded<KL, SCH>, "folded accumulation only");
-  static_assert(IB <= 3, "the gap ops serve at most 3 i-tiles");
+  static_assert(IB <= 6, "the gap ops serve at most 6 i-tiles");
   static_assert(TPS % 2 == 0, "stages hold whole 64-row chunks");
   __shared__ bf16x8 As[2][CH][64];
   const int lane = threadIdx.x & 63;

@@ -9,7 +9,7 @@ OUT=../../build_var
 UNIT=${3:-kde_mfma}
 mkdir -p $OUT
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function"
-if [ "$UNIT" != local ]; then BASE="$BASE -mllvm -amdgpu-mfma-vgpr-form=1"; fi
+if [ "$UNIT" != local ] && [ -z "$AGPR_FORM" ]; then BASE="$BASE -mllvm -amdgpu-mfma-vgpr-form=1"; fi
 if [ "$UNIT" = kde_mfma ]; then
   BASE="$BASE -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp"
 fi

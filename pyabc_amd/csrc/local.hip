@@ -719,7 +719,10 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
 // The index is the same CDF search as the global kernel (bit-exact for the
 // same u); the Gaussian draw uses the Cholesky factor of C[idx] (numpy uses
 // an SVD factor: same distribution, different map from z to theta).
-template <int D>
+// EXACT (d == D, d <= 8): compile-time loops keep the factor in registers;
+// with the runtime bound the d x d factor lived in scratch (528 B per lane
+// at D = 8, tools/spill_report.py).  Same operations in the same order.
+template <int D, bool EXACT>
 __global__ __launch_bounds__(256) void propose_local_kernel(
     const double* __restrict__ X, int64_t N, int d,
     const double* __restrict__ cdf, const double* __restrict__ covs,
@@ -738,11 +741,16 @@ __global__ __launch_bounds__(256) void propose_local_kernel(
     if (cdf[mid] <= u) lo_i = mid + 1; else hi_i = mid;
   }
   const int64_t idx = lo_i < N ? lo_i : N - 1;
+  const int dd = EXACT ? D : d;
+  constexpr int kUnroll = EXACT ? D : 1;
   double L[D][D];
-  const double* C = covs + idx * d * d;
-  for (int i = 0; i < d; ++i)
+  const double* C = covs + idx * dd * dd;
+#pragma unroll kUnroll
+  for (int i = 0; i < dd; ++i)
+#pragma unroll kUnroll
     for (int j = 0; j <= i; ++j) {
-      double s = C[i * d + j];
+      double s = C[i * dd + j];
+#pragma unroll kUnroll
       for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
       if (i == j)
         L[i][i] = sqrt(s > 0.0 ? s : 0.0);
@@ -750,19 +758,22 @@ __global__ __launch_bounds__(256) void propose_local_kernel(
         L[i][j] = L[j][j] > 0.0 ? s / L[j][j] : 0.0;
     }
   double z[D];
-  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
-  for (int k = 0; k < d; ++k) {
+  const uint64_t zi0 = ui * static_cast<uint64_t>(dd);
+#pragma unroll kUnroll
+  for (int k = 0; k < dd; ++k) {
     const uint64_t zi = zi0 + k;
     double c0, c1;
     box_muller(philox_block(seed, 2 * sid + 1, zi >> 1), c0, c1);
     z[k] = (zi & 1) ? c1 : c0;
   }
   bool ok = true;
-  for (int i = 0; i < d; ++i) {
+#pragma unroll kUnroll
+  for (int i = 0; i < dd; ++i) {
     double s = 0.0;
+#pragma unroll kUnroll
     for (int k = 0; k <= i; ++k) s = fma(L[i][k], z[k], s);
-    const double th = X[idx * d + i] + s;
-    theta[b * d + i] = th;
+    const double th = X[idx * dd + i] + s;
+    theta[b * dd + i] = th;
     if (lo) {
       const double x = (th - lo[i]) / scale[i];
       ok = ok && x >= 0.0 && x <= 1.0;
@@ -806,18 +817,22 @@ int abc_propose_local_philox_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE(N > 0 && B >= 0 && d >= 1 && d <= 16, "propose_local: bad sizes");
   if (B == 0) return kOk;
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
-  if (d <= 4)
-    hipLaunchKernelGGL((propose_local_kernel<4>), dim3(g), dim3(256), 0, st, X,
-                       N, d, cdf, covs, lo, scale, seed, sid, offset, B, theta,
-                       idx, in_support);
-  else if (d <= 8)
-    hipLaunchKernelGGL((propose_local_kernel<8>), dim3(g), dim3(256), 0, st, X,
-                       N, d, cdf, covs, lo, scale, seed, sid, offset, B, theta,
-                       idx, in_support);
-  else
-    hipLaunchKernelGGL((propose_local_kernel<16>), dim3(g), dim3(256), 0, st,
-                       X, N, d, cdf, covs, lo, scale, seed, sid, offset, B,
-                       theta, idx, in_support);
+  switch (d) {
+#define PL(DD, EX)                                                              \
+  hipLaunchKernelGGL((propose_local_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
+                     X, N, d, cdf, covs, lo, scale, seed, sid, offset, B, theta, \
+                     idx, in_support)
+    case 1: PL(1, true); break;
+    case 2: PL(2, true); break;
+    case 3: PL(3, true); break;
+    case 4: PL(4, true); break;
+    case 5: PL(5, true); break;
+    case 6: PL(6, true); break;
+    case 7: PL(7, true); break;
+    case 8: PL(8, true); break;
+    default: PL(16, false); break;
+#undef PL
+  }
   ABC_LAUNCH_CHECK("propose_local_kernel");
   return kOk;
 }

@@ -42,6 +42,10 @@ HOT = [
     # the ceiling guards against the round-5 regression (the row pinned to
     # VGPRs, DESIGN.md section 4 "LocalTransition kNN design")
     ("void abc::knn_kernel<6, 1, 4>", 48, 0, 0),
+] + [
+    # the LocalTransition proposal, one instantiation per d <= 8: the
+    # Cholesky factor in registers (the runtime-d form kept it in scratch)
+    (f"void abc::propose_local_kernel<{d}, true>", 0, 0, 0) for d in range(1, 9)
 ]
 
 

@@ -100,32 +100,64 @@ __global__ __launch_bounds__(256) void pack_prev_kernel(
     T* __restrict__ P, int64_t npad,
     const unsigned long long* __restrict__ max_key,
     double* __restrict__ lw2max_out) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // The block's 256 rows of X and the whitening matrix are staged in LDS
+  // (coalesced row loads instead of one 8 d-byte row per lane; the matrix
+  // read from LDS instead of uniform loads), and the
+  // packed rows leave through LDS as whole contiguous lines.  Each row's
+  // arithmetic is unchanged (same products, same fma order).
+  constexpr int kRowsB = 256;
+  constexpr size_t kBuf = sizeof(double) * kRowsB * D > sizeof(T) * kRowsB * (D + 1)
+                              ? sizeof(double) * kRowsB * D
+                              : sizeof(T) * kRowsB * (D + 1);
+  __shared__ double Ush[D * D];
+  __shared__ double mus[D];
+  __shared__ __attribute__((aligned(16))) unsigned char buf[kBuf];
+  double* Xs = reinterpret_cast<double*>(buf);
+  T* Ps = reinterpret_cast<T*>(buf);
+  const int tid = threadIdx.x;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kRowsB;
+  const int64_t i = r0 + tid;
   const double L = log2(key_f64(*max_key));
   if (i == 0 && lw2max_out) *lw2max_out = L;
-  if (i >= npad) return;
-  T* row = P + i * (D + 1);
-  if (i >= n) {
+  for (int q = tid; q < d * d; q += kRowsB) Ush[(q / d) * D + q % d] = Us[q];
+  for (int q = tid; q < d; q += kRowsB) mus[q] = mu[q];
+  const int nr = r0 < n ? static_cast<int>(min<int64_t>(kRowsB, n - r0)) : 0;
+  for (int q = tid; q < nr * d; q += kRowsB) Xs[q] = X[r0 * d + q];
+  __syncthreads();
+  T row[D + 1];
+  if (i < n) {
+    // row of the matrix by row: each output's fma chain still runs over l
+    // in ascending order (the same bits as the column-wise form)
+    double acc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = 0.0;
+#pragma unroll
+    for (int l = 0; l < D; ++l) {
+      if (l < d) {
+        const double xl = Xs[tid * d + l] - mus[l];
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          if (k < d) acc[k] = fma(xl, Ush[l * D + k], acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) row[k] = static_cast<T>(acc[k]);
+    const double wi = w[i];
+    double lw = wi > 0.0 ? log2(wi) - L : -1.0e300;
+    if (lw < static_cast<double>(kPadLw)) lw = kPadLw;
+    row[D] = static_cast<T>(lw);
+  } else {
 #pragma unroll
     for (int k = 0; k < D; ++k) row[k] = T(0);
     row[D] = static_cast<T>(kPadLw);
-    return;
   }
-  double xc[D];
+  __syncthreads();  // every lane is done reading Xs
 #pragma unroll
-  for (int l = 0; l < D; ++l) xc[l] = l < d ? X[i * d + l] - mu[l] : 0.0;
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    double acc = 0.0;
-#pragma unroll
-    for (int l = 0; l < D; ++l)
-      if (l < d && k < d) acc = fma(xc[l], Us[l * d + k], acc);
-    row[k] = static_cast<T>(acc);
-  }
-  const double wi = w[i];
-  double lw = wi > 0.0 ? log2(wi) - L : -1.0e300;
-  if (lw < static_cast<double>(kPadLw)) lw = kPadLw;
-  row[D] = static_cast<T>(lw);
+  for (int k = 0; k <= D; ++k) Ps[tid * (D + 1) + k] = row[k];
+  __syncthreads();
+  const int64_t nb = r0 < npad ? min<int64_t>(kRowsB, npad - r0) : 0;
+  T* dst = P + r0 * (D + 1);
+  for (int64_t q = tid; q < nb * (D + 1); q += kRowsB) dst[q] = Ps[q];
 }
 
 // ---------------------------------------------------------------------------

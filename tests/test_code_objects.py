@@ -42,6 +42,8 @@ HOT = [
     # the ceiling guards against the round-5 regression (the row pinned to
     # VGPRs, DESIGN.md section 4 "LocalTransition kNN design")
     ("void abc::knn_kernel<6, 1, 4>", 48, 0, 0),
+    # the previous population's pack (rows and matrix staged in LDS)
+    ("void abc::pack_prev_kernel<", 0, 0, 0),
 ] + [
     # the LocalTransition proposal, one instantiation per d <= 8: the
     # Cholesky factor in registers (the runtime-d form kept it in scratch)

@@ -134,6 +134,29 @@ int abc_compact_flags(const uint8_t* flags, int64_t n, int64_t* out_idx,
                       hipStream_t stream);
 int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
                         int64_t n, double* out, hipStream_t stream);
+/* The accepted population's rows, first n by evaluation id
+ *   (sampler/multicore_evaluation_parallel.py:131-132, singlecore.py:19-38):
+ * out[i*out_ld + k] = src[(idx ? idx[i] : i)*src_ld + k], k < width, over
+ * 8-byte words (fp64 values or int64 indices), so several columns and
+ * sampling rounds land in one buffer; idx = NULL is a strided row copy. */
+int abc_gather_words(const void* src, int64_t src_ld, int64_t width,
+                     const int64_t* idx, int64_t n, void* out, int64_t out_ld,
+                     hipStream_t stream);
+/* The same selection on a stat-major [rows][ld] matrix (the accepted sum
+ * stats, sampler/base.py:119-141): out[s*out_ld + i] = src[s*src_ld + idx[i]]
+ * (idx = NULL: a column-block copy) */
+int abc_gather_cols_words(const void* src, int64_t src_ld, int64_t rows,
+                          const int64_t* idx, int64_t n, void* out,
+                          int64_t out_ld, hipStream_t stream);
+/* Stable LSD radix sort of (key, int32 value) pairs by the low end_bit key
+ * bits -- the spatial index's Hilbert-key sort, in place of cKDTree's build
+ *                                                 local_transition.py:82-83
+ * keys / vals are overwritten (ping-pong); the result goes to keys_out /
+ * vals_out. */
+size_t abc_radix_sort_workspace_bytes(int64_t n);
+int abc_radix_sort_pairs_u64(uint64_t* keys, int32_t* vals, int64_t n,
+                             int end_bit, uint64_t* keys_out, int32_t* vals_out,
+                             void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* ---------------- (a3) KDE importance-weight pass ------------------------
  * Replaces MultivariateNormalTransition.pdf / pdf_static

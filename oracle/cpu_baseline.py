@@ -192,25 +192,62 @@ def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
                accepted=acc, evaluations=ev, wall=wall,
                seconds_per_generation=per, cpu_model=cpu_model(),
                host_cpus=os.cpu_count())
-    # t(N) = a N + b N^2 from sub-populations of the last generation
+    # t(N) = a N + b N^2 from sub-populations run
+    # over the SAME generation schedule as the direct measurement (every
+    # timed generation's population prefix, fit and epsilon, harmonic mean
+    # over the generations), so the sizes differ only in N_prev: the fit at
+    # BASELINE's sizes is extrapolated to N, and a second fit that includes
+    # the directly measured N shows how far the extrapolation is off.
     n_full = gens[-1][0].shape[0]
     sizes = [n for n in fit_sizes if n < n_full]
     if len(sizes) >= 2:
+        per_fit = fit_seconds / len(gens)
         fr = _spawn(ctx, q, _worker,
-                    [([(paths[-1], fit_seconds, n) for n in sizes], 2000 + i)
-                     for i in range(workers)])
-        rate_n = [sum(r[k][0] / r[k][2] for r in fr) for k in range(len(sizes))]
+                    [([(pa, per_fit, n) for n in sizes for pa in paths],
+                      2000 + i) for i in range(workers)])
+        G = len(gens)
+        rate_n = []
+        for k in range(len(sizes)):
+            rg = [sum(r[k * G + g][0] / r[k * G + g][2] for r in fr)
+                  for g in range(G)]
+            rate_n.append(G / sum(1.0 / max(x, 1e-12) for x in rg))
         tgen = [n / max(rn, 1e-12) for n, rn in zip(sizes, rate_n)]
         Amat = np.array([[n, n * n] for n in sizes], dtype=np.float64)
         (a, b), *_ = np.linalg.lstsq(Amat, np.array(tgen), rcond=None)
         t_ext = a * n_full + b * n_full ** 2
+        t_meas = n_full / max(sched, 1e-12)
+        A4 = np.vstack([Amat, [n_full, n_full ** 2]])
+        (a4, b4), *_ = np.linalg.lstsq(A4, np.array(tgen + [t_meas]),
+                                       rcond=None)
+        # per accepted particle and per previous-population particle: the
+        # O(N) CDF per proposal + O(N d) KDE per acceptance make this flat
+        # where the sampler is in one memory regime
+        us_per = [1e6 * t / n / n for n, t in zip(sizes + [n_full],
+                                                  tgen + [t_meas])]
         out["tN_fit"] = dict(
             sizes=sizes, rate=rate_n, t_generation_s=tgen, a=float(a),
             b=float(b), n=n_full, t_generation_extrapolated_s=float(t_ext),
             rate_extrapolated=float(n_full / t_ext),
-            rate_measured_last_generation=rates[-1],
+            rate_measured=sched, t_generation_measured_s=t_meas,
+            extrapolated_over_measured_time=float(t_ext / t_meas),
+            fit_with_measured_n=dict(a=float(a4), b=float(b4),
+                                     rate_at_n=float(n_full / (a4 * n_full
+                                                               + b4 * n_full ** 2))),
+            us_per_accepted_per_prev_particle=dict(zip(
+                [str(n) for n in sizes + [n_full]], us_per)),
+            schedule="every size runs the same timed generations (their "
+                     "populations' first n particles, fit and epsilon), "
+                     "harmonic mean over them, as the measured rate",
             label="extrapolated: t(N) = a N + b N^2 fitted at the sizes "
-                  "above with the measured workers")
+                  "above (BASELINE.md section 2) with the measured workers; "
+                  "the cost per accepted particle and per previous-"
+                  "population particle is not constant below N: small "
+                  "populations sit in the cores' caches while the "
+                  "workers share the memory bus at large N, so the "
+                  "quadratic term fitted on the small sizes does not carry "
+                  "to N -- the directly measured rate (value) is the "
+                  "baseline, the extrapolation is reported because "
+                  "BASELINE.md asks for it")
     if kde_dims:
         kd = _spawn(ctx, q, _kde_worker, [(kde_n_prev, tuple(kde_dims), 3)])[0]
         out["kde_pairs_per_s_1core"] = {

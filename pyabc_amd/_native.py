@@ -65,6 +65,13 @@ _SIGS = {
     "abc_compact_flags": (c_int, [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size,
                                   c_ptr]),
     "abc_gather_rows_f64": (c_int, [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr]),
+    "abc_gather_words": (c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr,
+                                 c_i64, c_ptr]),
+    "abc_gather_cols_words": (c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64,
+                                      c_ptr, c_i64, c_ptr]),
+    "abc_radix_sort_workspace_bytes": (c_size, [c_i64]),
+    "abc_radix_sort_pairs_u64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
+                                         c_ptr, c_ptr, c_size, c_ptr]),
     # (a3)
     "abc_kde_padded_dim": (c_int, [c_int]),
     "abc_kde_row_pad": (c_int, []),

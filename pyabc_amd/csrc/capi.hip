@@ -21,7 +21,8 @@ namespace {
 constexpr const char* kKnobNames[kKnobCount] = {
     "ABC_KDE_MFMA_SPLIT", "ABC_KDE_MFMA_IB",   "ABC_KDE_MFMA_PIPE",
     "ABC_KDE_MFMA_LDS2",  "ABC_KDE_MFMA_SMAJOR", "ABC_KDE_TIER",
-    "ABC_LZ_IB",          "ABC_LZ_TPB",          "ABC_KNN_ROWS"};
+    "ABC_LZ_IB",          "ABC_LZ_TPB",          "ABC_KNN_ROWS",
+    "ABC_KDE_PARENT_SHIFT", "ABC_KDE_PARENT_WIN", "ABC_PROPOSE_FORM"};
 std::atomic<int> g_knobs[kKnobCount];
 std::once_flag g_knobs_once;
 
@@ -51,7 +52,8 @@ const char* abc_last_error(void) { return abc::g_err; }
 int abc_preload(void) {
   return abc::preload_propose() + abc::preload_kde() + abc::preload_kde_mfma() +
          abc::preload_distance() + abc::preload_select() + abc::preload_stochastic() +
-         abc::preload_local() + abc::preload_local_pdf32() + abc::preload_local_mfma();
+         abc::preload_local() + abc::preload_local_pdf32() + abc::preload_local_mfma() +
+         abc::preload_sort();
 }
 int abc_version(void) { return 10000; }  // 0.1.0
 }

@@ -27,7 +27,8 @@ enum Status : int {
 void set_error(const char* fmt, ...);
 
 // Launch-shape tuning knobs (environment variables, tools/ sweeps and the
-// knob tests only; none changes a result bit).  The table is read from the
+// knob tests only; none changes a result bit except the two routing
+// experiments marked below).  The table is read from the
 // environment ONCE per process (capi.hip) and again only by
 // abc_tuning_reload(), so no launch path calls getenv.
 enum Knob : int {
@@ -40,6 +41,12 @@ enum Knob : int {
   kKnobLzIb,              // ABC_LZ_IB
   kKnobLzTpb,             // ABC_LZ_TPB
   kKnobKnnRows,           // ABC_KNN_ROWS
+  // routing experiments of the MFMA KDE pass (tools/kde_offsets.py): these
+  // two DO move rows between the folded pass and its refine, i.e. change
+  // bits within the derived bound (kde_mfma.hip, "refine")
+  kKnobKdeParentShift,    // ABC_KDE_PARENT_SHIFT
+  kKnobKdeParentWin,      // ABC_KDE_PARENT_WIN
+  kKnobProposeForm,       // ABC_PROPOSE_FORM (d > 8: 0 round 5, 1 chunked)
   kKnobCount
 };
 // the knob's integer value, or dflt when the variable is unset
@@ -100,6 +107,7 @@ int preload_select();
 int preload_stochastic();
 int preload_local();
 int preload_local_pdf32();
+int preload_sort();
 int preload_local_mfma();
 
 // ---- wave / block reductions (64-lane waves) -------------------------------

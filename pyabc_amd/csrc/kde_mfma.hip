@@ -420,21 +420,67 @@ __device__ inline void whiten_row(const double* __restrict__ X, int64_t i,
   }
 }
 
+// Block-staged whitening (round 6; the pattern of
+// kde.hip's pack_prev_kernel): the block's 256 rows of X arrive in LDS by
+// coalesced loads (one 8d-byte row per lane otherwise), and the whitening
+// matrix is read from LDS instead of being hoisted into SGPRs (114 SGPR
+// spills in pack_prev_frag_kernel at d = 20).  Row r0 + threadIdx.x gets
+// whiten_row's y: the same products, each output's fma chain over l in
+// ascending order -- the same bits.  Every thread of the block calls it.
+template <int D>
+struct WhitenLds {
+  static constexpr int LD = D | 1;  // odd row stride: fewer bank conflicts
+  double Ush[D * D];
+  double mus[D];
+  double Xs[256 * LD];
+};
+
+template <int D>
+__device__ inline void whiten_block(const double* __restrict__ X, int64_t r0,
+                                    int64_t n, int d, const double* __restrict__ mu,
+                                    const double* __restrict__ Us, WhitenLds<D>& s,
+                                    double (&y)[D]) {
+  constexpr int LD = WhitenLds<D>::LD;
+  const int tid = threadIdx.x;
+  for (int q = tid; q < d * d; q += 256) s.Ush[(q / d) * D + q % d] = Us[q];
+  for (int q = tid; q < d; q += 256) s.mus[q] = mu[q];
+  const int nr = r0 < n ? static_cast<int>(n - r0 < 256 ? n - r0 : 256) : 0;
+  for (int q = tid; q < nr * d; q += 256) s.Xs[(q / d) * LD + q % d] = X[r0 * d + q];
+  __syncthreads();
+  double acc[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) acc[k] = 0.0;
+  if (tid < nr) {
+#pragma unroll
+    for (int l = 0; l < D; ++l) {
+      if (l < d) {
+        const double xl = s.Xs[tid * LD + l] - s.mus[l];
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          if (k < d) acc[k] = fma(xl, s.Ush[l * D + k], acc[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) y[k] = acc[k];
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void ymax_kernel(
     const double* __restrict__ X, int64_t n, int d,
     const double* __restrict__ mu, const double* __restrict__ Us,
     unsigned long long* __restrict__ key) {
+  __shared__ WhitenLds<D> s;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * 256;
+  double y[D];
+  whiten_block<D>(X, r0, n, d, mu, Us, s, y);
   double m = 0.0;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    double y[D];
-    whiten_row<D>(X, i, d, mu, Us, y);
+  if (r0 + threadIdx.x < n) {
     if constexpr (Mk<D>::F16) {  // largest norm
       double n2 = 0.0;
 #pragma unroll
       for (int k = 0; k < D; ++k) n2 = fma(y[k], y[k], n2);
-      m = fmax(m, sqrt(n2));
+      m = sqrt(n2);
     } else {
 #pragma unroll
       for (int k = 0; k < D; ++k) m = fmax(m, fabs(y[k]));
@@ -466,19 +512,18 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
     int64_t npad, const double* __restrict__ lw2max,
     const unsigned long long* __restrict__ ykey, double* __restrict__ gscale,
     bf16x8* __restrict__ A) {
+  __shared__ WhitenLds<D> s;
   const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const double g = Mk<D>::F16 ? grid_from_key_f16(ykey) : grid_from_key(ykey);
   if (j == 0) *gscale = g;
-  if (j >= npad) return;
   double y[D];
+  whiten_block<D>(X, static_cast<int64_t>(blockIdx.x) * blockDim.x, n, d, mu, Us,
+                  s, y);  // zeros beyond n
+  if (j >= npad) return;
   double lw = kLwFloor;
   if (j < n) {
-    whiten_row<D>(X, j, d, mu, Us, y);
     const double wj = w[j];
     if (wj > 0.0) lw = fmax(log2(wj) - *lw2max, kLwFloor);
-  } else {
-#pragma unroll
-    for (int k = 0; k < D; ++k) y[k] = 0.0;
   }
   if constexpr (Mk<D>::F16) {
     unsigned short y1[D], r2[D], r3[D], r2h[D], h[2], l[2];
@@ -513,7 +558,8 @@ __global__ __launch_bounds__(256) void pack_prev_frag_kernel(
 // largest weight ("Accuracy of the folded
 // accumulation").  m_i comes from the row's parent (the particle its
 // proposal was resampled from: e_self = lw2_p - |y_i - y_p|^2, floored, at
-// most 64 below the global offset) or from the refine below.
+// most 64 below the global offset, plus kParentShift = 3, the typical log2
+// of the other terms' mass relative to it) or from the refine below.
 constexpr double kRowOffMin = -64.0;
 constexpr double kF16MaxQ = 4.19e6;  // |b'| / G bound (two 11-bit pieces: 4194303)
 
@@ -569,7 +615,7 @@ __device__ inline bool pack_row_new(const double* y, double g, double m,
 // [npad][D + 1] (y_j, lw2_j)
 template <int D>
 __device__ inline double parent_offset(const double* y, const double* __restrict__ P,
-                                       int64_t p) {
+                                       int64_t p, double shift) {
   const double* pp = P + p * (D + 1);
   double e = pp[D];
 #pragma unroll
@@ -577,7 +623,7 @@ __device__ inline double parent_offset(const double* y, const double* __restrict
     const double df = y[k] - pp[k];
     e = fma(-df, df, e);
   }
-  return e == e ? fmin(fmax(floor(e), kRowOffMin), 0.0) : 0.0;
+  return e == e ? fmin(fmax(floor(e), kRowOffMin), 0.0) + shift : 0.0;
 }
 
 template <int D>
@@ -585,16 +631,18 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     const double* __restrict__ theta, int64_t M, int64_t mpad, int d,
     const double* __restrict__ mu, const double* __restrict__ Us,
     const double* __restrict__ gscale, const double* __restrict__ P,
-    int64_t npad, const int64_t* __restrict__ parent,
+    int64_t npad, const int64_t* __restrict__ parent, double pshift,
     double* __restrict__ Ydir, double* __restrict__ row_off,
     bf16x8* __restrict__ B) {
+  __shared__ WhitenLds<D> s;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  double y[D];
+  whiten_block<D>(theta, static_cast<int64_t>(blockIdx.x) * blockDim.x, M, d, mu,
+                  Us, s, y);
   if (i >= mpad) return;
   const double g = *gscale;
-  double y[D];
   double m = 0.0;
   if (i < M) {
-    whiten_row<D>(theta, i, d, mu, Us, y);
 #pragma unroll
     for (int k = 0; k < D; ++k) Ydir[i * D + k] = y[k];
     // parents only where KL >= 4 lo MFMAs fold (d > 8): at d <= 8 the
@@ -605,7 +653,7 @@ __global__ __launch_bounds__(256) void pack_new_frag_kernel(
     // gpurun_out/r05d)
     if (parent && Mk<D>::SCH == 2 && Mk<D>::KL >= 4) {
       const int64_t p = parent[i];
-      if (p >= 0 && p < npad) m = parent_offset<D>(y, P, p);
+      if (p >= 0 && p < npad) m = parent_offset<D>(y, P, p, pshift);
     }
     if (row_off) row_off[i] = m;
   } else {
@@ -1516,11 +1564,11 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 }
 
 // ---- refine: flagged rows re-evaluated with their own offset (round 5) -----
-// Pass 1 evaluates every row relative to its offset m_i (0, or the parent's
-// term).  Rows whose sum S_i falls below lo (offset 0; the sum is then
-// <= N) or leaves [kParentRoute, 1 / kParentRoute] (a parent offset) are
-// refined on the matrix cores
-// instead of going to the fp64 fixup:
+// Pass 1 evaluates every row relative to its offset m_i (0, or its parent's
+// term shifted up by kParentShift).  Rows whose sum S_i falls below lo
+// (offset 0; the sum is then <= N) or leaves [2^-kParentWin, 2^kParentWin]
+// (a parent offset) are refined on the matrix cores instead of going to the
+// fp64 fixup:
 //   * S_i in the normal range: m_i += floor(log2 S_i) (the dominant terms
 //     then sit in [-log2 n_eff - 1, 0]);
 //   * S_i underflowed: one max pass of the same folded e over the row list
@@ -1536,15 +1584,31 @@ void launch_mfma(const MPlan& p, const bf16x8* Bfr, int64_t M,
 // where KL = 3 (d = 6, 8; 2^-16 measured a 6.76e-6 bound on rows at
 // e = -16, tests/test_gpu_kde_band.py), 2^-4 where KL = 4 ... 8
 // (8 < d <= 24).  The split and bf16 schemes keep the 2^-32 of rounds 1-4.
-// Rows with a parent offset (d > 8): the sum relative to the parent's term
-// is >= 1 by construction and its spread comes from the other terms --
-// quantiles 0.1 / 50 / 99 / 99.9 % of log2 S' = 0.03 / 1.9 / 13.8 / 18.9 on
-// C5's rows (N = 1e6, d = 20), against -22 / -17 / -11 / -8.9 under the
-// global offset.  Routing them at 2^4 would refine 29 % of the rows
-// (353 ms instead of ~200); at 2^16 0.4 % are refined.  Their accuracy is
-// measured (tests/test_gpu_fullsize.py, with the derived bound evaluated
-// on sampled rows); rows without a parent keep the guaranteed range below.
-constexpr double kParentRoute = 0x1p-16;
+// Rows with a parent offset (d > 8; round 6): the sum
+// relative to the parent's own term is >= 1 by construction (the parent's
+// term floored into [1, 2)); its spread comes from the other terms --
+// quantiles 0.1 / 50 / 90 / 99 / 99.9 % of log2 S' = 0.03 / 1.97 / 7.7 /
+// 13.9 / 19.1 on C5's rows (N = 1e6, d = 20; tools/kde_route.py, call
+// r06a).  The offset is the parent's floored term + kParentShift = 3 and
+// the row stays on the folded pass while S'' = S' 2^-3 lies in [2^-7, 2^7]:
+// a one-term-dominated row then has its dominant exponent within |e''| < 8
+// (derived bound <= 4.8e-6), and the refine takes the 4.6 % of C5's rows
+// with S' > 2^10 (211.1 ms against ~201 ms unrouted).  Measured with the
+// derived bound evaluated on EVERY row (tools/probes/kde_bound.hip, call
+// r06e): max 6.29e-6 <= 1e-5 / 1.5 on C5's 1e6 rows; window 2^8 left 18
+// rows above the bar, shift 2 refined 6.5 % of the rows.  A wrong parent
+// (S'' far outside the window) is refined like any other flagged row.  The
+// round-5 window [2^-16, 2^16] with no shift left rows at a 1.5e-5 bound.
+constexpr int kParentShift = 3;
+constexpr int kParentWin = 7;
+// routing experiments (tools/kde_route.py; ABC_KDE_PARENT_SHIFT / _WIN
+// override the two above): the parent offset's shift and the parent rows'
+// window [1 / phi, phi]
+inline double parent_shift() { return tuning_knob(kKnobKdeParentShift, kParentShift); }
+inline double parent_window() {
+  const int u = tuning_knob(kKnobKdeParentWin, kParentWin);
+  return ldexp(1.0, u < 1 ? 1 : (u > 60 ? 60 : u));
+}
 
 template <int D>
 struct Route {
@@ -1603,12 +1667,12 @@ size_t mfma_ws_layout(int64_t M, int nseg, char* base, MfmaWs* w) {
 }
 
 // pass-1 finalize: the fixed-order segment sum; rows at or above lo (rows
-// without an offset) or inside [kParentRoute, 1 / kParentRoute] (rows with
-// a parent offset) are final, the rest join the refine list
+// without an offset) or inside [plo, phi] (rows with a parent offset) are
+// final, the rest join the refine list
 __global__ __launch_bounds__(256) void mfma_finalize_kernel(
     const double* __restrict__ partial, int64_t M, int nseg,
     const double* __restrict__ row_off, const double* __restrict__ lw2max,
-    double log_const, double lo, double* __restrict__ out,
+    double log_const, double lo, double plo, double phi, double* __restrict__ out,
     int* __restrict__ cnt, int* __restrict__ rows1, double* __restrict__ s1) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= M) return;
@@ -1616,7 +1680,8 @@ __global__ __launch_bounds__(256) void mfma_finalize_kernel(
   for (int s = 0; s < nseg; ++s) S += partial[static_cast<int64_t>(s) * M + i];
   const double m = row_off ? row_off[i] : 0.0;
   const double off = kLn2d * (*lw2max) + log_const;
-  const bool keep = m == 0.0 ? S >= lo : (S >= kParentRoute && S <= 1.0 / kParentRoute);
+  // m == 0: the global offset (every e <= 0), whatever the row's origin
+  const bool keep = m == 0.0 ? S >= lo : (S >= plo && S <= phi);
   if (keep) {
     out[i] = log(S) + off + kLn2d * m;
   } else {
@@ -1805,12 +1870,16 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
   ABC_LAUNCH_CHECK("kde_mfma_kernel");
   const unsigned gm = static_cast<unsigned>(ceil_div(M, 256));
   const unsigned gl = stream_grid(M, 256, 1024);
-  // without the grid (abc_kde_logpdf_mfma) flagged rows go straight to the
-  // fp64 fixup, at the 2^-32 bound of rounds 1-4
-  const double lo = gscale ? Route<D>::lo : 0x1p-32;
+  // the folded scheme's routing bound with or without the grid: without it
+  // (the legacy abc_kde_logpdf_mfma) the flagged rows go straight to the
+  // fp64 fixup -- the same 1e-5 contract, only the cost differs (round 6,
+  // the 2^-32 of rounds 1-4 left derived bounds of 1.27e-5 at
+  // d = 8 and 2.9e-5 at d = 20 on this entry)
+  const double lo = Route<D>::lo;
+  const double phi = parent_window();
   hipLaunchKernelGGL(mfma_finalize_kernel, dim3(gm), dim3(256), 0, st, w.partial,
-                     M, p.nseg, row_off, lw2max, log_const, lo, out, w.cnt,
-                     w.rows1, w.s1);
+                     M, p.nseg, row_off, lw2max, log_const, lo, 1.0 / phi, phi,
+                     out, w.cnt, w.rows1, w.s1);
   hipLaunchKernelGGL(refine_classify_kernel<D>, dim3(gl), dim3(256), 0, st, w.cnt,
                      w.rows1, w.s1, row_off, Ynew, gscale, w.rows2, w.m2, w.rowsx,
                      w.mxo, w.rows3, w.Bbuf);
@@ -1885,7 +1954,7 @@ int abc_kde_pack_prev_mfma(const double* X, const double* w, int64_t n, int d,
   switch (D) {
 #define CASE(DD)                                                               \
   case DD:                                                                     \
-    hipLaunchKernelGGL((ymax_kernel<DD>), dim3(stream_grid(n, 256, 1024)),     \
+    hipLaunchKernelGGL((ymax_kernel<DD>), dim3(ceil_div(n > 0 ? n : 1, 256)),  \
                        dim3(256), 0, st, X, n, d, mu, Us, ykey);               \
     hipLaunchKernelGGL((pack_prev_frag_kernel<DD>), dim3(gr), dim3(256), 0, st, \
                        X, w, n, d, mu, Us, npad, lw2max, ykey, gscale,         \
@@ -1918,12 +1987,13 @@ int abc_kde_pack_new_mfma_rows(const double* theta, int64_t M, int d,
               "pack_new_mfma: parents need the packed population P");
   const int64_t mp = mpad_for(d, M);
   const unsigned gr = static_cast<unsigned>(ceil_div(mp, 256));
+  const double pshift = parent_shift();
   switch (D) {
 #define CASE(DD)                                                              \
   case DD:                                                                    \
     hipLaunchKernelGGL((pack_new_frag_kernel<DD>), dim3(gr), dim3(256), 0, st, \
                        theta, M, mp, d, mu, Us, gscale, P, npad, parent,     \
-                       Ynew, row_off, static_cast<bf16x8*>(Bfr));            \
+                       pshift, Ynew, row_off, static_cast<bf16x8*>(Bfr));    \
     break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16)
     CASE(20) CASE(24) CASE(32)

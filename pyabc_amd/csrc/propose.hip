@@ -700,6 +700,72 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
                         sup + b, 0, tab, log2k);
 }
 
+// d > 8 (round 6): the same proposals with the
+// Box-Muller pairs consumed as they are drawn.  Pair q of the proposal's
+// normal range feeds components k0 = 2q - odd and k0 + 1 straight into the
+// perturbation's fma chains (k ascending, as perturb_one), so neither the d
+// normals nor a runtime-d loop over them are kept: 2D fewer live fp64
+// registers.  The CDF search is issued first so its dependent loads overlap
+// the draws.  Same u, z, fma order: the same bits as propose_philox_kernel.
+template <int D, bool EXACT>
+__global__ __launch_bounds__(256) void propose_chunk_kernel(
+    const double* __restrict__ X, int64_t N, int d_arg,
+    const double* __restrict__ cdf, const double* __restrict__ A,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
+    double* __restrict__ theta, int64_t* __restrict__ idx,
+    uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
+  const int d = EXACT ? D : d_arg;
+  __shared__ double As[D * D];
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) As[i] = A[i];
+  __syncthreads();
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t ui = offset + static_cast<uint64_t>(b);
+  const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
+  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
+  const int64_t i = search_right(cdf, N, u, tab, log2k);
+  const int64_t ic = i < N ? i : N - 1;
+  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
+  const uint64_t p0 = zi0 >> 1;
+  const int odd = static_cast<int>(zi0 & 1);
+  double pl[D];
+#pragma unroll
+  for (int l = 0; l < D; ++l) pl[l] = 0.0;
+#pragma unroll
+  for (int q = 0; q < D / 2 + 1; ++q) {
+    const int k0 = 2 * q - odd;  // component of the pair's cos branch
+    if (k0 < d) {
+      double c0, c1;
+      box_muller(philox_block(seed, 2 * sid + 1, p0 + q), c0, c1);
+      if (k0 >= 0) {
+#pragma unroll
+        for (int l = 0; l < D; ++l)
+          if (l < d) pl[l] = fma(c0, As[k0 * d + l], pl[l]);
+      }
+      if (k0 + 1 < d) {
+#pragma unroll
+        for (int l = 0; l < D; ++l)
+          if (l < d) pl[l] = fma(c1, As[(k0 + 1) * d + l], pl[l]);
+      }
+    }
+  }
+  bool ok = true;
+#pragma unroll
+  for (int l = 0; l < D; ++l) {
+    if (l < d) {
+      const double th = X[ic * d + l] + pl[l];
+      theta[b * d + l] = th;
+      if (lo) {
+        const double x = (th - lo[l]) / scale[l];
+        ok = ok && (x >= 0.0) && (x <= 1.0);
+      }
+    }
+  }
+  idx[b] = i;
+  sup[b] = ok ? 1 : 0;
+}
+
 // bucket table of the CDF: tab[k] = searchsorted(cdf, k / 2^L, 'right')
 __global__ __launch_bounds__(256) void cdf_index_kernel(
     const double* __restrict__ cdf, int64_t n, int log2k,
@@ -826,6 +892,36 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(
   if (t >= n * width) return;
   const int64_t i = t / width, k = t % width;
   out[t] = src[idx[i] * width + k];
+}
+
+// strided gather of 8-byte words (fp64 or int64 bits; round 6: the accepted
+// rows' selection without torch's index_select / cat):
+//   out[i * out_ld + k] = src[(idx ? idx[i] : i) * src_ld + k],  k < width
+// one thread per word, grid-stride (width is small: d + 1 at most 33)
+__global__ __launch_bounds__(256) void gather_words_kernel(
+    const uint64_t* __restrict__ src, int64_t src_ld, int64_t width,
+    const int64_t* __restrict__ idx, int64_t n, uint64_t* __restrict__ out,
+    int64_t out_ld) {
+  const int64_t total = n * width;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       t < total; t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t i = t / width, k = t - i * width;
+    const int64_t r = idx ? idx[i] : i;
+    out[i * out_ld + k] = src[r * src_ld + k];
+  }
+}
+
+// column gather of a stat-major matrix: out[s * out_ld + i] =
+// src[s * src_ld + idx[i]], s < rows (the accepted statistics, [S][B]);
+// idx = NULL: a column-block copy
+__global__ __launch_bounds__(256) void gather_cols_kernel(
+    const uint64_t* __restrict__ src, int64_t src_ld, int64_t rows,
+    const int64_t* __restrict__ idx, int64_t n, uint64_t* __restrict__ out,
+    int64_t out_ld) {
+  const int64_t s = blockIdx.y;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    out[s * out_ld + i] = src[s * src_ld + (idx ? idx[i] : i)];
 }
 
 // ---------------------------------------------------------------------------
@@ -1043,6 +1139,20 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
               "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+  const int form = tuning_knob(kKnobProposeForm, 1);
+  if (d > 8 && form != 0) {  // the chunked d > 8 form (same bits)
+#define LC(DD, EX)                                                              \
+  hipLaunchKernelGGL((propose_chunk_kernel<DD, EX>), dim3(g), dim3(256), 0, st,  \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
+                     idx, in_support, tab, log2k);
+    if (d == 20 && form == 1) { LC(20, true) }
+    else if (d <= 16) { LC(16, false) }
+    else if (d <= 24) { LC(24, false) }
+    else { LC(32, false) }
+#undef LC
+    ABC_LAUNCH_CHECK("propose_chunk_kernel");
+    return kOk;
+  }
 #define LX(DD, EX)                                                              \
   hipLaunchKernelGGL((propose_philox_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
                      X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
@@ -1130,6 +1240,47 @@ int abc_gather_rows_f64(const double* src, int64_t width, const int64_t* idx,
   hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(n * width, 256)),
                      dim3(256), 0, st, src, width, idx, n, out);
   ABC_LAUNCH_CHECK("gather_rows_kernel");
+  return kOk;
+}
+
+// Accepted-row selection (round 6; replaces torch index_select / cat on the
+// hot path).  The first-n-by-id population of the reference's samplers
+// (sampler/multicore_evaluation_parallel.py:131-132, singlecore.py:19-38):
+// rows src[idx[i]] (8-byte words: fp64 parameters, distances, weights, int64
+// parent indices) written at out + i * out_ld, so several columns and
+// several sampling rounds land in one preallocated buffer.  idx = NULL:
+// the identity (a strided row copy).
+int abc_gather_words(const void* src, int64_t src_ld, int64_t width,
+                     const int64_t* idx, int64_t n, void* out, int64_t out_ld,
+                     hipStream_t st) {
+  ABC_REQUIRE(width > 0 && n >= 0 && src_ld >= width && out_ld >= width,
+              "gather_words: bad sizes (width %lld, ld %lld / %lld)",
+              static_cast<long long>(width), static_cast<long long>(src_ld),
+              static_cast<long long>(out_ld));
+  if (n == 0) return kOk;
+  ABC_REQUIRE(src && out, "gather_words: null pointer");
+  hipLaunchKernelGGL(gather_words_kernel, dim3(stream_grid(n * width, 256, 4096)),
+                     dim3(256), 0, st, static_cast<const uint64_t*>(src), src_ld,
+                     width, idx, n, static_cast<uint64_t*>(out), out_ld);
+  ABC_LAUNCH_CHECK("gather_words_kernel");
+  return kOk;
+}
+
+// Column selection of a stat-major [rows][*] matrix (the accepted
+// statistics kept for adaptive distances, sampler/base.py:119-141):
+// out[s * out_ld + i] = src[s * src_ld + idx[i]] (idx = NULL: idx[i] = i).
+int abc_gather_cols_words(const void* src, int64_t src_ld, int64_t rows,
+                          const int64_t* idx, int64_t n, void* out,
+                          int64_t out_ld, hipStream_t st) {
+  ABC_REQUIRE(rows >= 0 && n >= 0 && out_ld >= n && rows < 65536,
+              "gather_cols_words: bad sizes");
+  if (n == 0 || rows == 0) return kOk;
+  ABC_REQUIRE(src && out, "gather_cols_words: null pointer");
+  hipLaunchKernelGGL(gather_cols_kernel,
+                     dim3(stream_grid(n, 256, 64), static_cast<unsigned>(rows)),
+                     dim3(256), 0, st, static_cast<const uint64_t*>(src), src_ld,
+                     rows, idx, n, static_cast<uint64_t*>(out), out_ld);
+  ABC_LAUNCH_CHECK("gather_cols_kernel");
   return kOk;
 }
 

@@ -25,9 +25,11 @@ namespace abc {
 constexpr int kTile = 64;  // particles per tile (one per lane)
 
 size_t sort_pairs_temp_bytes(int64_t n);
-hipError_t sort_pairs(void* temp, size_t temp_bytes, const uint64_t* keys_in,
-                      uint64_t* keys_out, const int32_t* vals_in,
-                      int32_t* vals_out, int64_t n, int end_bit, hipStream_t st);
+// this repo's stable LSD radix sort (sort.hip); keys_in / vals_in are
+// overwritten (ping-pong buffers)
+hipError_t sort_pairs(void* temp, size_t temp_bytes, uint64_t* keys_in,
+                      uint64_t* keys_out, int32_t* vals_in, int32_t* vals_out,
+                      int64_t n, int end_bit, hipStream_t st);
 
 __host__ __device__ inline int morton_bits(int d) {
   const int b = 63 / d;

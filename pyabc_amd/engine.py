@@ -115,7 +115,7 @@ class DeviceMVNFit:
             with torch.cuda.stream(pack_stream):
                 pack_stream.wait_event(ev)
                 pp = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
-                                        precision)
+                                        precision, ws_tag="pack_side")
                 self._pack_ev = torch.cuda.Event()
                 self._pack_ev.record(pack_stream)
             for t in (pp.P, pp.lw2max, getattr(pp, "A", None),
@@ -207,7 +207,9 @@ def start_cdf(w):
     side = _side_stream()
     with torch.cuda.stream(side):
         side.wait_event(ev)
-        cdf = K.resample_cdf(w)
+        # its own scratch: a main-stream CDF (LocalTransition.fit) may run
+        # at the same time
+        cdf = K.resample_cdf(w, ws_tag="cdf_side")
         tab = K.cdf_index(cdf)
         cdf_ev = torch.cuda.Event()
         cdf_ev.record(side)
@@ -284,13 +286,48 @@ def selection_plan(nvs, nas, n):
     return takes, closing
 
 
-def gather_segments(comm, pieces, row_shape, counts, device):
+def copy_rows(dst, src):
+    """dst[:] = src (same shape, rows of 8-byte words): the library's strided
+    word copy on the device (no torch kernel), a plain copy for the host
+    tensors of the gloo rehearsals."""
+    if src.shape[0] == 0:
+        return dst
+    if dst.is_cuda:
+        if src.dim() == 1:
+            return K.gather_words(src, None, src.shape[0], dst)
+        return K.gather_words(src.reshape(src.shape[0], -1), None,
+                              src.shape[0], dst.view(dst.shape[0], -1))
+    dst.copy_(src)
+    return dst
+
+
+def cat_rows(pieces, row_shape, device, dtype=F64):
+    """torch.cat of row pieces through :func:`copy_rows` (a single piece is
+    returned as is)."""
+    if len(pieces) == 1:
+        return pieces[0]
+    n = sum(int(p.shape[0]) for p in pieces)
+    out = torch.empty((n,) + tuple(row_shape), dtype=dtype, device=device)
+    r = 0
+    for p in pieces:
+        copy_rows(out[r:r + p.shape[0]], p)
+        r += p.shape[0]
+    return out
+
+
+def gather_segments(comm, pieces, row_shape, counts, device, dtype=F64):
     """Global row order from per-rank pieces: ``pieces`` are this rank's
-    non-empty segments in round order, ``counts[s][k]`` the rows rank s holds
-    from round k.  Returns the rows ordered round-major, then by rank -- the
-    global id order -- on every rank (one all-gather)."""
-    local = torch.cat(pieces) if pieces else torch.empty(
-        (0,) + tuple(row_shape), dtype=F64, device=device)
+    non-empty segments in round order (a list, or one tensor holding them
+    back to back), ``counts[s][k]`` the rows rank s holds from round k.
+    Returns the rows ordered round-major, then by rank -- the global id
+    order -- on every rank (one all-gather; the reorder is a block copy, and
+    none at all when one round produced every row)."""
+    if torch.is_tensor(pieces):
+        local = pieces
+    elif pieces:
+        local = cat_rows(pieces, row_shape, device, pieces[0].dtype)
+    else:
+        local = torch.empty((0,) + tuple(row_shape), dtype=dtype, device=device)
     R = comm.world
     if not comm.active:
         return local
@@ -298,14 +335,25 @@ def gather_segments(comm, pieces, row_shape, counts, device):
     starts = [0]
     for s in range(R):
         starts.append(starts[-1] + sum(counts[s]))
-    out = []
+    blocks = []
     for k in range(len(counts[0])):
         for s in range(R):
             c = counts[s][k]
             if c:
-                off = starts[s] + sum(counts[s][:k])
-                out.append(allr[off:off + c])
-    return torch.cat(out) if out else allr[:0]
+                blocks.append((starts[s] + sum(counts[s][:k]), c))
+    pos = 0
+    for off, c in blocks:     # already in global order (one round): no copy
+        if off != pos:
+            break
+        pos += c
+    else:
+        return allr
+    out = torch.empty_like(allr)
+    pos = 0
+    for off, c in blocks:
+        copy_rows(out[pos:pos + c], allr[off:off + c])
+        pos += c
+    return out
 
 
 def mirrors_simulate(model):
@@ -368,16 +416,24 @@ def redecide_guard_band(stats, B, d, acc, guard, x0_host, fw_host, p, eps,
     return n
 
 
-def _read_counts(acount, gcount, apos, nv, need):
-    """[accepted, guard band, apos[need - 1]] in one host read; the last
-    is the position of the round's need-th acceptance (valid only when
-    accepted >= need) -- the selection's closing position without a read of
-    its own."""
-    parts = [acount.view(1), gcount.view(1)]
+def _count_slots(dev):
+    """int64[3] device slots: accepted count, guard-band count, closing
+    position (filled by the compactions / a word copy, read in one go)."""
+    return torch.empty(3, dtype=torch.int64, device=dev)
+
+
+def _read_counts(cbuf, apos, nv, need):
+    """[accepted, guard band, apos[need - 1]] in one host read of ``cbuf``
+    (the first two slots written by the compactions); the last is the
+    position of the round's need-th acceptance (valid only when accepted >=
+    need) -- the selection's closing position without a read of its own."""
+    k = 2
     if need is not None and nv:
-        parts.append(apos[min(need, nv) - 1:min(need, nv)])
-    vals = torch.cat(parts).cpu().tolist()
-    last = vals[2] if len(vals) > 2 and vals[0] >= need else None
+        p = min(need, nv) - 1
+        K.gather_words(apos[p:p + 1], None, 1, cbuf[2:3])
+        k = 3
+    vals = cbuf[:k].cpu().tolist()
+    last = vals[2] if k == 3 and vals[0] >= need else None
     return int(vals[0]), int(vals[1]), last
 
 
@@ -391,10 +447,13 @@ def decide(acceptance, stats, nv, seed, stream, eval_off, need=None):
         return acceptance.decide(stats, nv, seed, stream, eval_off,
                                  need=need)
     d, acc, guard, accw = acceptance(stats, nv, seed, stream, eval_off)
-    apos, acount = K.compact(acc)
-    g = guard[:nv].sum(dtype=torch.int64).view(1) if guard is not None \
-        else torch.zeros(1, dtype=torch.int64, device=acount.device)
-    n_acc, n_guard, last = _read_counts(acount, g, apos, nv, need)
+    cbuf = _count_slots(acc.device)
+    apos, _ = K.compact(acc, count=cbuf[0:1])
+    if guard is not None:
+        K.compact(guard[:nv], count=cbuf[1:2])
+    else:
+        K.compact(acc[:0], count=cbuf[1:2])    # writes a zero count
+    n_acc, n_guard, last = _read_counts(cbuf, apos, nv, need)
     return d, acc, guard, accw, apos, n_acc, n_guard, last
 
 
@@ -436,9 +495,10 @@ class PNormAcceptance:
                                              self.eps, B=nv)
         else:
             d, acc, guard, simulate = fused
-        gpos, gcount = K.compact(guard[:nv])
-        apos, acount = K.compact(acc)
-        n_acc, n_guard, last = _read_counts(acount, gcount, apos, nv, need)
+        cbuf = _count_slots(acc.device)
+        gpos, _ = K.compact(guard[:nv], count=cbuf[1:2])
+        apos, _ = K.compact(acc, count=cbuf[0:1])
+        n_acc, n_guard, last = _read_counts(cbuf, apos, nv, need)
         if n_guard:
             if stats is None:
                 stats = simulate()
@@ -625,7 +685,9 @@ class GenerationEngine:
                 nvs = comm.all_gather_ints(vcount)                  # sync 1
                 nv = nvs[r]
                 theta = K.gather_rows(theta_all, vpos, nv) if nv else None
-                pid = K.gather_rows(idx.to(F64), vpos, nv) \
+                # the in-support proposals' resample indices (int64)
+                pid = K.gather_words(idx, vpos, nv, torch.empty(
+                    nv, dtype=torch.int64, device=self.dev)) \
                     if nv and use_parent else None
             nv = nvs[r]
             my_eval = eval_off + sum(nvs[:r])
@@ -697,11 +759,23 @@ class GenerationEngine:
         takes, closing = selection_plan([rd["nvs"] for rd in rounds],
                                         [rd["nas"] for rd in rounds], n)
         lasts = []
-        th_loc, d_loc, st_loc, rec_loc = [], [], [], []
-        aw_loc, rth_loc, rd_loc, ra_loc, rp_loc = [], [], [], [], []
+        rec_loc = []
+        rth_loc, rd_loc, ra_loc, rp_loc = [], [], [], []
         stochastic = isinstance(acceptance, StochasticAcceptance)
         n_guard = 0
         n_eval_loc = 0
+        # this rank's accepted rows of every round land in one buffer per
+        # quantity (the library's word gathers; parents as an int64 column
+        # beside theta, so one all-gather carries both)
+        k_loc = sum(tk[r] for tk in takes)
+        wth = self.d + int(use_parent)
+        th_buf = torch.empty((k_loc, wth), dtype=F64, device=self.dev)
+        d_buf = torch.empty(k_loc, dtype=F64, device=self.dev)
+        aw_buf = torch.empty(k_loc, dtype=F64, device=self.dev) \
+            if stochastic else None
+        st_buf = torch.empty((self.model.n_stats, k_loc), dtype=F64,
+                             device=self.dev) if keep_stats else None
+        row = 0
         for rd, take, cl in zip(rounds, takes, closing):
             k = take[r]
             if cl[r] == 1:          # this rank holds the n-th acceptance
@@ -716,17 +790,17 @@ class GenerationEngine:
             lasts.append(last)
             n_eval_loc += last
             if k:
-                sel = rd["apos"][:k]
-                th = rd["theta"].index_select(0, sel)
-                if use_parent:   # parent index as an extra column
-                    th = torch.cat([th, rd["pid"].index_select(0, sel)[:, None]],
-                                   1)
-                th_loc.append(th)
-                d_loc.append(rd["d"].index_select(0, sel))
+                sel = rd["apos"]
+                rows_ = slice(row, row + k)
+                K.gather_words(rd["theta"], sel, k, th_buf[rows_, :self.d])
+                if use_parent:
+                    K.gather_words(rd["pid"], sel, k, th_buf[rows_, self.d:])
+                K.gather_words(rd["d"], sel, k, d_buf[rows_])
                 if stochastic:
-                    aw_loc.append(rd["accw"].index_select(0, sel))
+                    K.gather_words(rd["accw"], sel, k, aw_buf[rows_])
                 if keep_stats:
-                    st_loc.append(rd["stats"].index_select(1, sel))
+                    K.gather_cols(rd["stats"], sel, k, st_buf[:, rows_])
+                row += k
             if last:
                 if record:
                     rec_loc.append(rd["stats"][:, :last])
@@ -748,17 +822,21 @@ class GenerationEngine:
             self.timers = tm
             return GenerationResult(ok=False, n_eval=int(cap))
         take_counts = [[tk[s] for tk in takes] for s in range(R)]
-        theta_acc = self._gather(th_loc, (self.d + int(use_parent),),
-                                 take_counts)
+        theta_acc = self._gather(th_buf, (wth,), take_counts)
         parent_acc = None
         if use_parent:
-            parent_acc = theta_acc[:, self.d].to(torch.int64)
-            theta_acc = theta_acc[:, :self.d].contiguous()
-        d_acc = self._gather(d_loc, (), take_counts)
+            T = theta_acc.shape[0]
+            parent_acc = K.gather_words(
+                theta_acc[:, self.d:], None, T,
+                torch.empty((T, 1), dtype=torch.int64, device=self.dev)).view(-1)
+            theta_acc = K.gather_words(
+                theta_acc[:, :self.d], None, T,
+                torch.empty((T, self.d), dtype=F64, device=self.dev))
+        d_acc = self._gather(d_buf, (), take_counts)
         stats_acc = None
         if keep_stats:
-            stats_acc = self._gather_cols(st_loc, take_counts)
-        accw_acc = self._gather(aw_loc, (), take_counts) if stochastic \
+            stats_acc = self._gather_cols([st_buf], take_counts)
+        accw_acc = self._gather(aw_buf, (), take_counts) if stochastic \
             else None
         rec = None
         last_counts = None
@@ -770,8 +848,8 @@ class GenerationEngine:
         if record_particles:
             rec_theta = self._gather(rth_loc, (self.d,), last_counts)
             if use_parent:
-                rec_parent = self._gather(rp_loc, (), last_counts).to(
-                    torch.int64)
+                rec_parent = self._gather(rp_loc, (), last_counts,
+                                          dtype=torch.int64)
             rec_d = self._gather(rd_loc, (), last_counts)
             rec_acc = self._gather(ra_loc, (), last_counts)
         # host time (the device work of the selection overlaps the KDE pass)
@@ -815,8 +893,9 @@ class GenerationEngine:
             accw=accw_acc, rec_theta=rec_theta, rec_d=rec_d, rec_acc=rec_acc,
             rec_parent=rec_parent)
 
-    def _gather(self, pieces, row_shape, counts):
-        return gather_segments(self.comm, pieces, row_shape, counts, self.dev)
+    def _gather(self, pieces, row_shape, counts, dtype=F64):
+        return gather_segments(self.comm, pieces, row_shape, counts, self.dev,
+                               dtype)
 
     def _gather_cols(self, pieces, counts):
         """Stat-major [S, cols] version of :meth:`_gather`.  Row-contiguous
@@ -830,9 +909,18 @@ class GenerationEngine:
                 # one round: the column slice itself (row stride = the
                 # round's batch; the kernels take (pointer, ld), no copy)
                 return pieces[0]
-            return torch.cat(pieces, 1) if pieces else torch.empty(
-                (S, 0), dtype=F64, device=self.dev)
-        rows = self._gather([x.t() for x in pieces], (S,), counts)
+            n = sum(int(x.shape[1]) for x in pieces)
+            out = torch.empty((S, n), dtype=F64, device=self.dev)
+            c = 0
+            for x in pieces:   # column blocks through the library's copy
+                K.gather_cols(x, None, x.shape[1], out[:, c:c + x.shape[1]])
+                c += x.shape[1]
+            return out
+        # several ranks: the row all-gather takes [cols, S] rows (a
+        # transpose; the recorded statistics of multi-rank runs only)
+        local = torch.cat([x.t() for x in pieces]) if pieces else torch.empty(
+            (0, S), dtype=F64, device=self.dev)
+        rows = self._gather(local, (S,), counts)
         return rows.t().contiguous()
 
     # ------------------------------------------------------------------

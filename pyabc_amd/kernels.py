@@ -78,11 +78,13 @@ def philox_normal(seed, sid, offset, n):
     return out
 
 
-def resample_cdf(w):
+def resample_cdf(w, ws_tag="cdf"):
+    """The resampling CDF of w; ``ws_tag`` names the scratch buffer (callers
+    on another stream pass their own, engine.start_cdf: "cdf_side")."""
     w = _contig(w, F64)
     cdf = torch.empty_like(w)
     wsb = nat.lib().abc_resample_cdf_workspace_bytes(w.numel())
-    ws = WS.get(wsb, "cdf")
+    ws = WS.get(wsb, ws_tag)
     call("abc_resample_cdf_f64", ptr(w), w.numel(), ptr(cdf), ptr(ws), wsb,
          nat.stream())
     return cdf
@@ -144,12 +146,15 @@ def prior_uniform(lo, scale, seed, sid, offset, B):
     return theta
 
 
-def compact(flags, out_idx=None):
-    """Order-preserving positions of nonzero u8 flags; returns (idx, count_dev)."""
+def compact(flags, out_idx=None, count=None):
+    """Order-preserving positions of nonzero u8 flags; returns (idx,
+    count_dev).  ``count``: an int64 device slot to write the count into
+    (several counts in one buffer come back in one host read)."""
     n = flags.numel()
     if out_idx is None:
         out_idx = torch.empty(max(n, 1), dtype=torch.int64, device=_dev())
-    count = torch.empty(1, dtype=torch.int64, device=_dev())
+    if count is None:
+        count = torch.empty(1, dtype=torch.int64, device=_dev())
     wsb = nat.lib().abc_compact_workspace_bytes(n)
     ws = WS.get(wsb, "compact")
     call("abc_compact_flags", ptr(flags), n, ptr(out_idx), ptr(count), ptr(ws),
@@ -165,6 +170,72 @@ def gather_rows(src, idx, n=None):
     call("abc_gather_rows_f64", ptr(src), width, ptr(idx), n, ptr(out),
          nat.stream())
     return out if src.dim() == 2 else out.view(-1)
+
+
+def radix_sort_pairs(keys, vals, end_bit=64):
+    """Stable sort of (uint64 key as int64 bits, int32 value) pairs by the
+    low ``end_bit`` key bits (abc_radix_sort_pairs_u64, the spatial index's
+    sort); returns (keys_sorted, vals_sorted).  The inputs are copied."""
+    n = keys.numel()
+    kin = keys.clone() if keys.dtype == torch.int64 else None
+    if kin is None or vals.dtype != torch.int32:
+        raise TypeError("keys int64 (uint64 bits), vals int32")
+    vin = vals.clone()
+    ko = torch.empty_like(kin)
+    vo = torch.empty_like(vin)
+    wsb = nat.lib().abc_radix_sort_workspace_bytes(n)
+    ws = WS.get(wsb, "sort")
+    call("abc_radix_sort_pairs_u64", ptr(kin), ptr(vin), n, end_bit, ptr(ko),
+         ptr(vo), ptr(ws), wsb, nat.stream())
+    return ko, vo
+
+
+def _words(t):
+    """(tensor, row stride, width) of an 8-byte-element 1-D / 2-D view with
+    unit column stride (a column block of a wider buffer is fine)."""
+    if t.element_size() != 8:
+        raise TypeError(f"8-byte elements expected, got {t.dtype}")
+    if t.dim() == 1:
+        if t.numel() > 1 and t.stride(0) != 1:
+            raise ValueError("1-D view must be contiguous")
+        return 1, 1
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1):
+        raise ValueError("2-D view with unit column stride expected")
+    return max(t.stride(0), t.shape[1]), t.shape[1]
+
+
+def gather_words(src, idx, n, out):
+    """out[i, :] = src[idx[i], :] for i < n (idx None: src[i, :]) over
+    8-byte words -- fp64 values or int64 indices, bit copies
+    (abc_gather_words).  ``out`` may be a row / column block of a larger
+    buffer: the accepted rows of several rounds and columns land in place.
+    Returns ``out``."""
+    src_ld, w = _words(src)
+    out_ld, wo = _words(out)
+    if w != wo or out.shape[0] < n:
+        raise ValueError(f"gather_words: widths {w} / {wo}, rows {out.shape[0]} < {n}")
+    if n:
+        call("abc_gather_words", ptr(src), src_ld, w,
+             ptr(idx) if idx is not None else None, n, ptr(out), out_ld,
+             nat.stream())
+    return out
+
+
+def gather_cols(src, idx, n, out):
+    """out[s, i] = src[s, idx[i]] for i < n (idx None: src[s, i]) over
+    8-byte words of a stat-major [S, *] matrix (abc_gather_cols_words);
+    ``out`` may be a column block of a wider [S, *] buffer."""
+    if src.element_size() != 8 or out.element_size() != 8:
+        raise TypeError("8-byte elements expected")
+    S = src.shape[0]
+    if out.shape[0] != S or out.shape[1] < n or src.stride(1) != 1 \
+            or (out.shape[1] > 1 and out.stride(1) != 1):
+        raise ValueError("gather_cols: shapes")
+    if n and S:
+        call("abc_gather_cols_words", ptr(src), src.stride(0), S,
+             ptr(idx) if idx is not None else None, n, ptr(out),
+             out.stride(0), nat.stream())
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -253,7 +324,8 @@ class PackedPopulation:
     kde_mfma.hip), "f32" (direct fp32 VALU pass) or "f64" (fp64 VALU pass).
     """
 
-    def __init__(self, X, w, mu, Us, rank, log_pdet, precision="mfma"):
+    def __init__(self, X, w, mu, Us, rank, log_pdet, precision="mfma",
+                 ws_tag="pack"):
         X = _contig(X, F64)
         n, d = X.shape
         self.n, self.d = n, d
@@ -270,7 +342,7 @@ class PackedPopulation:
         self.mu = mu
         self.Us = Us
         self.log_const = -0.5 * (rank * LOG_2PI + log_pdet)
-        ws = WS.get(256, "pack")
+        ws = WS.get(256, ws_tag)   # "pack_side" on the engine's side stream
         w = _contig(w, F64)
         if precision == "mfma":
             nb = nat.lib().abc_kde_mfma_prev_bytes(self.npad, d)
@@ -294,7 +366,8 @@ class PackedPopulation:
         theta = _contig(theta, F64)
         M = theta.shape[0]
         if self.precision == "mfma":
-            Y = torch.zeros((M, self.D), dtype=F64, device=_dev())
+            # every column written by the pack (zeros beyond d)
+            Y = torch.empty((M, self.D), dtype=F64, device=_dev())
             nb = nat.lib().abc_kde_mfma_new_bytes(M, self.d)
             B = torch.empty(max(nb, 16), dtype=torch.uint8, device=_dev())
             off = torch.empty(max(M, 1), dtype=F64, device=_dev())

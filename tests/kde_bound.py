@@ -3,10 +3,14 @@
 tests/test_gpu_kde_band.py and tests/test_gpu_fullsize.py.  Not a test
 module (no test functions): torch on the GPU evaluates every pair's fp64
 exponent of the rows it is given."""
+import ctypes
 import math
+import os
 
 import numpy as np
 import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def ulp32(x):
@@ -50,17 +54,57 @@ def row_stats(Yp, lw, Y, off, KL, D, g, chunk=128):
     return {k: torch.cat(v).cpu().numpy() for k, v in out.items()}
 
 
-def pass_offsets(log2S, emax, m1, D, lo=None):
+PARENT_WIN = 7   # kde_mfma.hip kParentWin (log2 of the parent rows' window)
+
+
+def pass_offsets(log2S, emax, m1, D, lo=None, win=PARENT_WIN):
     """The offset each row ends up with in kde_mfma.hip: the pass-1 offset
     m1 while the sum relative to it lies in the routing range (Route for
-    rows without an offset, [2^-16, 2^16] for rows with a parent offset),
+    rows without an offset, [2^-win, 2^win] for rows with a parent offset),
     otherwise m1 + floor(log2 S') (S' in the normal range) or the max
     pass's m1 + floor(max e')."""
     KL = (5 * D + 4 + 15) // 16
     if lo is None:  # kde_mfma.hip Route<D>::lo
         lo = 2.0 ** -26 if KL <= 2 else (2.0 ** -12 if KL <= 3 else 2.0 ** -4)
     lS = log2S - m1
-    keep = np.where(m1 == 0, lS >= math.log2(lo), (lS >= -16) & (lS <= 16))
+    keep = np.where(m1 == 0, lS >= math.log2(lo), (lS >= -win) & (lS <= win))
     normal = (lS > -100) & (lS < 100)
     m2 = np.where(normal, m1 + np.floor(lS), m1 + np.floor(emax - m1))
     return np.where(keep, m1, m2), ~keep
+
+
+_PROBE = {}
+
+
+def _probe():
+    if "lib" not in _PROBE:
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probes",
+                                       "libabc_probe.so"))
+        f = lib.abc_probe_kde_bound
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                      ctypes.c_double, ctypes.c_int, ctypes.c_void_p,
+                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _PROBE["lib"] = lib
+    return _PROBE["lib"]
+
+
+def row_stats_all(packed, Y, off, KL):
+    """:func:`row_stats` on EVERY row, in fp64 on the GPU
+    (tools/probes/kde_bound.hip): ``packed`` the MFMA PackedPopulation,
+    ``Y`` the whitened rows [M][D] (WhitenedRows.Y), ``off`` their offsets.
+    Returns numpy arrays bound, log2S_rel (the sum relative to the row's
+    offset) and H."""
+    M, D = Y.shape
+    n = int(packed.n)
+    g = float(packed.gscale.item())
+    out = torch.empty((3, M), dtype=torch.float64, device=Y.device)
+    off = off.contiguous()
+    rc = _probe().abc_probe_kde_bound(
+        packed.P.data_ptr(), n, D, Y.contiguous().data_ptr(), off.data_ptr(),
+        M, g, KL, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+        torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    o = out.cpu().numpy()
+    return {"bound": o[0], "log2S_rel": o[1], "H": o[2]}

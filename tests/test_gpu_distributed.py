@@ -162,22 +162,23 @@ def _rank_main_parents(rank, world, port, n, out):
 
 
 @pytest.mark.timeout(240)
-def test_two_ranks_equal_one_rank_parents_d12():
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_ranks_equal_one_rank_parents_d12(world):
     """At d > 8 the accepted rows' parents travel with theta through the
     all-gather to the row-parallel KDE pass (per-row offsets), and the next
-    fit comes from next_generation_inputs: two ranks reproduce one rank's
-    parents, log-densities, weights and epsilons bit for bit."""
+    fit comes from next_generation_inputs: two (four) ranks reproduce one
+    rank's parents, log-densities, weights and epsilons bit for bit."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 3001
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_rank_main_parents, args=(2, port, n, out), nprocs=2,
-                 join=True)
+        mp.spawn(_rank_main_parents, args=(world, port, n, out),
+                 nprocs=world, join=True)
         res = dict(out)
     one = res["single"]
-    for r in (0, 1):
+    for r in range(world):
         for k, v in one.items():
             if isinstance(v, float):
                 assert res[r][k] == v, k
@@ -190,9 +191,10 @@ def test_two_ranks_equal_one_rank_parents_d12():
 
 
 @pytest.mark.timeout(240)
-def test_two_ranks_equal_one_rank_bit_for_bit():
-    """Global-id sampling (engine.sample_generation): two ranks sharing
-    cuda:0 over gloo produce exactly the population, distances, weights,
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_ranks_equal_one_rank_bit_for_bit(world):
+    """Global-id sampling (engine.sample_generation): two (and four) ranks
+    sharing cuda:0 over gloo produce exactly the population, distances, weights,
     evaluation count, recorded statistics, next epsilon and next fit that
     one rank produces -- with different sampling-round sizes too; and the
     same for a stochastic-acceptance generation (acceptance weights and
@@ -203,10 +205,11 @@ def test_two_ranks_equal_one_rank_bit_for_bit():
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_rank_main, args=(2, port, n, out), nprocs=2, join=True)
+        mp.spawn(_rank_main, args=(world, port, n, out), nprocs=world,
+                 join=True)
         res = dict(out)
     one = res["single"]
-    for r in (0, 1):
+    for r in range(world):
         got = res[r]
         for k in ("theta0", "d0", "theta", "d", "w", "logpd", "stats", "rec",
                   "cov1", "eps_ties", "s_theta", "s_d", "s_w", "s_accw", "s_rec_theta",

@@ -157,3 +157,51 @@ def test_kde_folded_band_rows(K, d):
     assert err_ref.max() <= BAR, stats
     assert np.all(err <= st["bound"]), stats
     assert st["bound"].max() <= BAR, stats
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("d", [8, 20])
+def test_kde_legacy_entry_band_rows(K, d):
+    """abc_kde_logpdf_mfma (no grid pointer, no row offsets; the entry the
+    INTEGRATION.md example binds) on band rows: it routes at the folded
+    scheme's own bound (Route<D>::lo) and, lacking the grid, hands every
+    flagged row to the exact fp64 fixup -- the 1e-5 contract holds on the
+    rows where rounds 1-4's 2^-32 threshold reached derived bounds of
+    1.27e-5 (d = 8) and 2.9e-5 (d = 20)."""
+    from pyabc_amd import _native as nat
+    rng = np.random.default_rng(900 + d)
+    N, n_rows = 32768, 4000
+    X = rng.normal(size=(N, d)) * rng.uniform(0.5, 2.0, d)
+    w = rng.uniform(0.5, 1.5, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    U, rank, log_pdet = K.psd_whitening(cov)
+    Us = U * math.sqrt(0.5 * K.LOG2E)
+    mu = (X * w[:, None]).sum(0) / w.sum()
+    dv = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    pp = K.PackedPopulation(dv(X), dv(w), dv(mu), dv(Us), rank, log_pdet,
+                            "mfma")
+    pp64 = K.PackedPopulation(dv(X), dv(w), dv(mu), dv(Us), rank, log_pdet,
+                              "f64")
+    D = pp.D
+    Yp = pp.P[:N, :D].contiguous()
+    lw = pp.P[:N, D].contiguous()
+    Yc = _band_rows(Yp, lw, n_rows, rng, d)
+    th = dv(mu + Yc[:, :d] @ np.linalg.pinv(Us))
+    Wr = pp.whiten(th)
+    M = th.shape[0]
+    out = torch.empty(M, dtype=torch.float64, device="cuda")
+    wsb = nat.lib().abc_kde_workspace_bytes(M, pp.npad, d)
+    ws = K.WS.get(wsb, "kde")
+    nat.call("abc_kde_logpdf_mfma", nat.ptr(Wr.frags), nat.ptr(Wr.Y), M,
+             nat.ptr(pp.A), nat.ptr(pp.P), pp.npad, d, nat.ptr(pp.lw2max),
+             pp.log_const, nat.ptr(out), nat.ptr(ws), wsb, nat.stream())
+    lp = out.cpu().numpy()
+    n_fix = int(ws[nat.lib().abc_kde_segments(pp.npad) * M * 8:][:4]
+                .view(torch.int32).item())
+    lp64 = pp64.logpdf(th).cpu().numpy()
+    err = np.abs(np.expm1(lp - lp64))
+    print(json.dumps(dict(d=d, rows=M, fixup_rows=n_fix,
+                          max_rel_err_vs_f64=float(err.max()))))
+    assert err.max() <= BAR, err.max()
+    assert n_fix > 0

@@ -383,3 +383,69 @@ def test_stochastic_acceptor_log_file(K):
     assert isinstance(list(pnorms.keys())[0], int)
     assert isinstance(pnorms[0], float)
     os.remove(pnorm_file)
+
+
+def test_device_records_parents_d12(K, monkeypatch):
+    """get_all_records at d > 8: the records' transition
+    log-densities come from the MFMA pass WITH parents -- the previous
+    population's resample index, and cumsum(acc) - 1 in the new population
+    (smc.py _device_records).  Every record's density must match the fp64
+    pass on the same fit within 1e-5 (multivariatenormal.py:102-125), and
+    so must the pass with wrong (shuffled, out-of-range) parents: a wrong
+    parent only moves the row's offset, which the routing window catches."""
+    import pyabc_amd as pa
+    from pyabc_amd import smc as smc_mod
+    rng = np.random.default_rng(12)
+    d, S = 12, 40
+    A = rng.normal(size=(S, d)) / np.sqrt(d)
+    th0 = np.linspace(-1, 1, d)
+    var = 0.5
+    x0v = A @ th0 + np.sqrt(var) * rng.normal(size=S)
+    keys = [f"y{k:02d}" for k in range(S)]
+    names = [f"p{k:02d}" for k in range(d)]
+    seen = []
+    orig = smc_mod.ABCSMC._device_records
+
+    def spy(self, t, sample, prev_transitions):
+        rec = orig(self, t, sample, prev_transitions)
+        theta = sample.rec_particles[0]
+        m = rec.distance.numel()
+        fits = (prev_transitions[0].device_fit if t > 1 else None,
+                self.transitions[0].device_fit)
+        par = sample.rec_particles[3] if len(sample.rec_particles) > 3 \
+            else None
+        seen.append((t, theta[:m].clone(), rec.log_transition_pd_prev.clone(),
+                     rec.log_transition_pd.clone(), fits,
+                     None if par is None else par[:m].clone()))
+        return rec
+
+    monkeypatch.setattr(smc_mod.ABCSMC, "_device_records", spy)
+    model = pa.LinearGaussianModel(A, sigma=0.0, keys=keys)
+    prior = pa.Distribution(**{n: pa.RV("uniform", -5, 10) for n in names})
+    sampler = pa.GPUBatchSampler(seed=77)
+    abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=var * np.ones(S)),
+                    population_size=3000, eps=pa.Temperature(),
+                    acceptor=pa.StochasticAcceptor(), sampler=sampler)
+    abc.new(pa.create_sqlite_db_id(), dict(zip(keys, x0v)))
+    abc.run(max_nr_populations=4)
+    assert sampler.fallback_reason is None
+    checked = 0
+    for t, theta, lp_prev, lp_cur, fits, par in seen:
+        for fit, lp in zip(fits, (lp_prev, lp_cur)):
+            if fit is None:
+                continue
+            pp64 = K.PackedPopulation(fit.X, fit.w, fit.packed.mu,
+                                      fit.packed.Us, fit.rank, fit.log_pdet,
+                                      "f64")
+            ref64 = pp64.logpdf(theta).cpu().numpy()
+            err = np.abs(np.expm1(lp.cpu().numpy() - ref64))
+            assert err.max() < 1e-5, (t, err.max())
+            # wrong parents: shuffled and out of range
+            n = fit.n
+            bad = torch.as_tensor(rng.integers(-5, n + 5, theta.shape[0]),
+                                  device="cuda")
+            lpb = fit.logpdf(theta, bad).cpu().numpy()
+            errb = np.abs(np.expm1(lpb - ref64))
+            assert errb.max() < 1e-5, (t, errb.max())
+            checked += 1
+    assert checked >= 3, checked

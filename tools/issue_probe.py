@@ -27,7 +27,11 @@ MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
          16: "mix 13 + 5 ds_read_b128 + barrier + 18-KiB LDS-DMA refill every 4 steps",
          17: "mix 13 + 4 ds_read_b128 per step",
          18: "LocalTransition z form d=6 (lz_kernel): 3 MFMA, 2 v_exp_f32, 17 v_add_f32",
-         19: "LocalTransition z form d=6: 3 MFMA, 2 v_exp_f32, 19 v_add_f32"}
+         19: "LocalTransition z form d=6: 3 MFMA, 2 v_exp_f32, 19 v_add_f32",
+         20: "mix 13 as 16x16x32 f16: 4 tiles x (1 hi + 4 lo) = 20 MFMA, "
+             "16 v_exp_f32, 28 v_add_f32 per 1024 pairs",
+         21: "mix 12 as 16x16x32 f16: 4 tiles x (1 hi + 2 lo) = 12 MFMA, "
+             "16 v_exp_f32, 22 v_add_f32 per 1024 pairs"}
 
 
 def parse():
@@ -45,6 +49,8 @@ def load():
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "probes", "libabc_probe.so"))
     lib.abc_probe_kde_mix.restype = ctypes.c_double
     lib.abc_probe_kde_mix.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.abc_probe_last_clock_ghz.restype = ctypes.c_double
+    lib.abc_probe_last_clock_ghz.argtypes = []
     return lib
 
 
@@ -58,8 +64,10 @@ def main():
         desc = MIXES[v]
         for wps in waves:
             ns = lib.abc_probe_kde_mix(v, wps, 100000)
+            ghz = lib.abc_probe_last_clock_ghz()
             out.append(dict(variant=v, mix=desc, waves_per_simd=wps,
-                            ns_per_step_per_simd=ns))
+                            ns_per_step_per_simd=ns,
+                            clock_ghz=ghz if ghz > 0 else None))
             print(json.dumps(out[-1]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 

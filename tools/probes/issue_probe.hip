@@ -50,7 +50,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define ABC_ADD(a, s) asm volatile("v_add_f32 %0, %0, %1" : "+v"(a) : "v"(s));
 
 template <int NM, int NE, int NA>
-__global__ __launch_bounds__(256) void mix_kernel(float* out, int iters) {
+__global__ __launch_bounds__(256) void mix_kernel(float* out, int iters,
+                                                  unsigned long long* cyc) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
   // random-looking bf16 operands (all-zero operands raise the clock)
   uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
   bf16x8 a, b;
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(256) void mix_kernel(float* out, int iters) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) t += v[k] + acc[k];
   out[blockIdx.x * 256 + threadIdx.x] = t;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = __builtin_amdgcn_s_memtime() - c0;
 }
 
 // The same mix with the headline kernel's memory path added step by step
@@ -170,9 +173,102 @@ double time_mem_mix(int waves_per_simd, int iters, int cus, float* out,
   return best * 1e6 / (static_cast<double>(waves_per_simd) * iters);
 }
 
+// mean over blocks of the shader-clock cycles a wave ran (s_memtime), per
+// launch millisecond: the clock the chip held under the mix (GHz)
+double g_clock_ghz = 0.0;
+
+double mean_clock_ghz(const unsigned long long* cyc, int blocks, float ms) {
+  unsigned long long* h = new unsigned long long[blocks];
+  double c = 0.0;
+  if (hipMemcpy(h, cyc, static_cast<size_t>(blocks) * 8, hipMemcpyDeviceToHost) ==
+      hipSuccess) {
+    for (int b = 0; b < blocks; ++b) c += static_cast<double>(h[b]);
+    c /= blocks;
+  }
+  delete[] h;
+  return ms > 0.0f ? c / (ms * 1e6) : 0.0;
+}
+
+// The same work in the v_mfma_f32_16x16x32_f16 shape (variants 20-21, VERDICT
+// r05 item 2): a 32 x 32 tile step becomes four 16 x 16 tiles, each one hi
+// and (NM / 4 - 1) lo MFMAs chained on its own accumulator (the hi and lo
+// products may not share a K = 32 chunk), the four
+// chains interleaved so no MFMA waits on its predecessor's result.  A lane
+// owns one new row and 4 j's of each 16 x 16 tile: 16 exps and the same
+// adds per 1024 pairs as the 32 x 32 mix.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int NM, int NE, int NA>
+__global__ __launch_bounds__(256) void mix16_kernel(float* out, int iters,
+                                                    unsigned long long* cyc) {
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  uint32_t h = (blockIdx.x * 256u + threadIdx.x) * 2654435761u;
+  f16x8 a, b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h ^= h >> 13; h *= 0x5bd1e995u;
+    a[e] = static_cast<_Float16>(1.0f + (h & 0x7F) * (1.0f / 128));
+    b[e] = static_cast<_Float16>(-1.0f - ((h >> 8) & 0x7F) * (1.0f / 128));
+  }
+  f32x4 acc[4] = {};
+  float v[16];
+  const float s = 1e-7f * (threadIdx.x & 7);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = -1e-3f * (threadIdx.x + k);
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      acc[m & 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[m & 3], 0, 0, 0);
+#pragma unroll
+      for (int k = m * NE / NM; k < (m + 1) * NE / NM; ++k) ABC_EXP(v[k & 15])
+#pragma unroll
+      for (int k = m * NA / NM; k < (m + 1) * NA / NM; ++k)
+        ABC_ADD(v[(k + 5) & 15], s)
+    }
+  }
+  float t = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += v[k];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+  out[blockIdx.x * 256 + threadIdx.x] = t;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = __builtin_amdgcn_s_memtime() - c0;
+}
+
+template <int NM, int NE, int NA>
+double time_mix16(int waves_per_simd, int iters, int cus, float* out) {
+  const int blocks = cus * waves_per_simd;
+  unsigned long long* cyc = nullptr;
+  (void)hipMalloc(&cyc, static_cast<size_t>(blocks) * 8);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((mix16_kernel<NM, NE, NA>), dim3(blocks), dim3(256), 0, 0,
+                       out, iters, cyc);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep > 0 && ms < best) {
+      best = ms;
+      g_clock_ghz = mean_clock_ghz(cyc, blocks, ms);
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(cyc);
+  return best * 1e6 / (static_cast<double>(waves_per_simd) * iters);
+}
+
 template <int NM, int NE, int NA>
 double time_mix(int waves_per_simd, int iters, int cus, float* out) {
-  const int blocks = cus * waves_per_simd;  // 4 waves per block, 1 per SIMD
+  const int blocks = cus * waves_per_simd;
+  unsigned long long* cyc = nullptr;
+  (void)hipMalloc(&cyc, static_cast<size_t>(blocks) * 8);  // 4 waves per block, 1 per SIMD
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -180,15 +276,19 @@ double time_mix(int waves_per_simd, int iters, int cus, float* out) {
   for (int rep = 0; rep < 4; ++rep) {  // rep 0 warms the clock
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL((mix_kernel<NM, NE, NA>), dim3(blocks), dim3(256), 0, 0,
-                       out, iters);
+                       out, iters, cyc);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    if (rep > 0 && ms < best) best = ms;
+    if (rep > 0 && ms < best) {
+      best = ms;
+      g_clock_ghz = mean_clock_ghz(cyc, blocks, ms);
+    }
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  (void)hipFree(cyc);
   // every SIMD runs waves_per_simd waves of iters steps
   return best * 1e6 / (static_cast<double>(waves_per_simd) * iters);
 }
@@ -196,6 +296,10 @@ double time_mix(int waves_per_simd, int iters, int cus, float* out) {
 }  // namespace
 
 extern "C" {
+
+// the clock (GHz, s_memtime cycles / launch time) of the last mix timed by
+// abc_probe_kde_mix (variants 0-4, 12, 13, 18-21; 0 for the memory mixes)
+double abc_probe_last_clock_ghz() { return g_clock_ghz; }
 
 // ns per step per SIMD of mix `variant` at `waves_per_simd` waves per SIMD
 // (< 0 on error).  Blocks: one per CU per wave slot.
@@ -219,6 +323,7 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
   }
   (void)hipMemset(src, 0x3C, src_bytes);
   double ns = -1.0;
+  g_clock_ghz = 0.0;
   switch (variant) {
     case 0: ns = time_mix<5, 16, 23>(waves_per_simd, iters, cus, out); break;
     case 1: ns = time_mix<11, 16, 40>(waves_per_simd, iters, cus, out); break;
@@ -247,6 +352,11 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     // squares, 2 fma, 2 adds, the flush) -- 19 bounds the flush's share
     case 18: ns = time_mix<3, 2, 17>(waves_per_simd, iters, cus, out); break;
     case 19: ns = time_mix<3, 2, 19>(waves_per_simd, iters, cus, out); break;
+    // mix 13's work (d = 20, f16 folded) in the 16x16x32 shape: 4 tiles x
+    // (1 hi + 4 lo) = 20 MFMAs per 1024 pairs, 16 exps, 28 other VALU
+    case 20: ns = time_mix16<20, 16, 28>(waves_per_simd, iters, cus, out); break;
+    // the d = 8 mix 12 in that shape: 4 x (1 hi + 2 lo) = 12 MFMAs
+    case 21: ns = time_mix16<12, 16, 22>(waves_per_simd, iters, cus, out); break;
     default: break;
   }
   (void)hipFree(src);

@@ -100,8 +100,13 @@ def kde_pmc(d):
 # tools/probes/issue_probe.hip variants holding the kernel's PMC-counted
 # per-tile mix (MFMA, v_exp_f32, other VALU); a non-integer VALU count is
 # the mean of two variants
-PROBE_MIX = {8: (3, 12),   # 4 MFMA, 16 exp, 21 / 22 other (PMC 21.5)
-             20: (13,)}    # 9 MFMA, 16 exp, 28 other (PMC 28.2)
+# (round 6: SQ_INSTS_VALU counts the MFMAs too -- the issue probe's own mix
+# under --pmc, 4 MFMA + 16 exp + 22 adds per step, reads 42.0 VALU -- so
+# the kernel's other VALU per tile is VALU - TRANS - MFMA: 17.5 at d = 8,
+# 18.0 at d = 20; rounds 2-5 priced 21.5 / 28 and over-stated the probe's
+# ceiling)
+PROBE_MIX = {8: (22, 23),  # 4 MFMA, 16 exp, 17 / 18 other (PMC 17.5)
+             20: (24,)}    # 9 MFMA, 16 exp, 18 other (PMC 18.0)
 PROBE_WAVES = {8: 4, 20: 2}  # the KDE kernel's occupancy (waves per SIMD)
 
 # MI355X_MICROARCH.md per-instruction constants (cycles per wave64
@@ -173,8 +178,10 @@ def kde_roofline(d, achieved_tf, traffic, traffic_src, avg_launch_s,
     KH, KL = (D + 4 + 15) // 16, (5 * D + 4 + 15) // 16
     if pmc is not None:
         pt = pmc["per_tile"]
-        V, T, F = (pt["SQ_INSTS_VALU"], pt.get("SQ_INSTS_VALU_TRANS_F32", 0.0),
-                   pt["SQ_INSTS_MFMA"])
+        # SQ_INSTS_VALU includes the MFMAs (measured on the issue probe):
+        # V below is the VALU excluding them
+        F = pt["SQ_INSTS_MFMA"]
+        V, T = (pt["SQ_INSTS_VALU"] - F, pt.get("SQ_INSTS_VALU_TRANS_F32", 0.0))
         src = f"{os.path.relpath(pmc_path, ROOT)} (rocprofv3 --pmc, per-tile)"
     else:   # static count of the kernel's per-tile code
         F = KH + KL

@@ -148,6 +148,12 @@ int abc_gather_words(const void* src, int64_t src_ld, int64_t width,
 int abc_gather_cols_words(const void* src, int64_t src_ld, int64_t rows,
                           const int64_t* idx, int64_t n, void* out,
                           int64_t out_ld, hipStream_t stream);
+/* Constant fills and an index ramp for the calibration / prior
+ * generations (smc.py:486-534: every proposal accepted, distance inf, weight
+ * 1): x[i] = bits (8-byte words), x[i] = v (bytes), x[i] = start + i. */
+int abc_fill_words(void* x, int64_t n, uint64_t bits, hipStream_t stream);
+int abc_fill_u8(uint8_t* x, int64_t n, int v, hipStream_t stream);
+int abc_iota_i64(int64_t* x, int64_t n, int64_t start, hipStream_t stream);
 /* Stable LSD radix sort of (key, int32 value) pairs by the low end_bit key
  * bits -- the spatial index's Hilbert-key sort, in place of cKDTree's build
  *                                                 local_transition.py:82-83

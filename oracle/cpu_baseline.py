@@ -206,11 +206,16 @@ def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
                     [([(pa, per_fit, n) for n in sizes for pa in paths],
                       2000 + i) for i in range(workers)])
         G = len(gens)
-        rate_n = []
+        rate_n, acc_n, evps = [], [], []
         for k in range(len(sizes)):
             rg = [sum(r[k * G + g][0] / r[k * G + g][2] for r in fr)
                   for g in range(G)]
             rate_n.append(G / sum(1.0 / max(x, 1e-12) for x in rg))
+            a_k = sum(r[k * G + g][0] for r in fr for g in range(G))
+            e_k = sum(r[k * G + g][1] for r in fr for g in range(G))
+            s_k = sum(r[k * G + g][2] for r in fr for g in range(G))
+            acc_n.append(a_k / max(e_k, 1))
+            evps.append(e_k / max(s_k, 1e-12))   # evaluations per worker-s
         tgen = [n / max(rn, 1e-12) for n, rn in zip(sizes, rate_n)]
         Amat = np.array([[n, n * n] for n in sizes], dtype=np.float64)
         (a, b), *_ = np.linalg.lstsq(Amat, np.array(tgen), rcond=None)
@@ -233,6 +238,11 @@ def run(gens, A_model, x0, lo, sc, sigma, p=2.0, workers=None, seconds=8.0,
             fit_with_measured_n=dict(a=float(a4), b=float(b4),
                                      rate_at_n=float(n_full / (a4 * n_full
                                                                + b4 * n_full ** 2))),
+            acceptance_rate=dict(zip([str(n) for n in sizes + [n_full]],
+                                     acc_n + [sum(acc) / max(sum(ev), 1)])),
+            evaluations_per_worker_s=dict(zip(
+                [str(n) for n in sizes + [n_full]],
+                evps + [sum(ev) / max(workers * seconds, 1e-12)])),
             us_per_accepted_per_prev_particle=dict(zip(
                 [str(n) for n in sizes + [n_full]], us_per)),
             schedule="every size runs the same timed generations (their "

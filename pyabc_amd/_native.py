@@ -69,6 +69,9 @@ _SIGS = {
                                  c_i64, c_ptr]),
     "abc_gather_cols_words": (c_int, [c_ptr, c_i64, c_i64, c_ptr, c_i64,
                                       c_ptr, c_i64, c_ptr]),
+    "abc_fill_words": (c_int, [c_ptr, c_i64, c_u64, c_ptr]),
+    "abc_fill_u8": (c_int, [c_ptr, c_i64, c_int, c_ptr]),
+    "abc_iota_i64": (c_int, [c_ptr, c_i64, c_i64, c_ptr]),
     "abc_radix_sort_workspace_bytes": (c_size, [c_i64]),
     "abc_radix_sort_pairs_u64": (c_int, [c_ptr, c_ptr, c_i64, c_int, c_ptr,
                                          c_ptr, c_ptr, c_size, c_ptr]),

@@ -46,7 +46,6 @@ enum Knob : int {
   // bits within the derived bound (kde_mfma.hip, "refine")
   kKnobKdeParentShift,    // ABC_KDE_PARENT_SHIFT
   kKnobKdeParentWin,      // ABC_KDE_PARENT_WIN
-  kKnobProposeForm,       // ABC_PROPOSE_FORM (d > 8: 0 round 5, 1 chunked)
   kKnobCount
 };
 // the knob's integer value, or dflt when the variable is unset

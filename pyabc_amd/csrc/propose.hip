@@ -700,72 +700,6 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
                         sup + b, 0, tab, log2k);
 }
 
-// d > 8 (round 6): the same proposals with the
-// Box-Muller pairs consumed as they are drawn.  Pair q of the proposal's
-// normal range feeds components k0 = 2q - odd and k0 + 1 straight into the
-// perturbation's fma chains (k ascending, as perturb_one), so neither the d
-// normals nor a runtime-d loop over them are kept: 2D fewer live fp64
-// registers.  The CDF search is issued first so its dependent loads overlap
-// the draws.  Same u, z, fma order: the same bits as propose_philox_kernel.
-template <int D, bool EXACT>
-__global__ __launch_bounds__(256) void propose_chunk_kernel(
-    const double* __restrict__ X, int64_t N, int d_arg,
-    const double* __restrict__ cdf, const double* __restrict__ A,
-    const double* __restrict__ lo, const double* __restrict__ scale,
-    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
-    double* __restrict__ theta, int64_t* __restrict__ idx,
-    uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
-  const int d = EXACT ? D : d_arg;
-  __shared__ double As[D * D];
-  for (int i = threadIdx.x; i < d * d; i += blockDim.x) As[i] = A[i];
-  __syncthreads();
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const uint64_t ui = offset + static_cast<uint64_t>(b);
-  const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
-  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
-  const int64_t i = search_right(cdf, N, u, tab, log2k);
-  const int64_t ic = i < N ? i : N - 1;
-  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
-  const uint64_t p0 = zi0 >> 1;
-  const int odd = static_cast<int>(zi0 & 1);
-  double pl[D];
-#pragma unroll
-  for (int l = 0; l < D; ++l) pl[l] = 0.0;
-#pragma unroll
-  for (int q = 0; q < D / 2 + 1; ++q) {
-    const int k0 = 2 * q - odd;  // component of the pair's cos branch
-    if (k0 < d) {
-      double c0, c1;
-      box_muller(philox_block(seed, 2 * sid + 1, p0 + q), c0, c1);
-      if (k0 >= 0) {
-#pragma unroll
-        for (int l = 0; l < D; ++l)
-          if (l < d) pl[l] = fma(c0, As[k0 * d + l], pl[l]);
-      }
-      if (k0 + 1 < d) {
-#pragma unroll
-        for (int l = 0; l < D; ++l)
-          if (l < d) pl[l] = fma(c1, As[(k0 + 1) * d + l], pl[l]);
-      }
-    }
-  }
-  bool ok = true;
-#pragma unroll
-  for (int l = 0; l < D; ++l) {
-    if (l < d) {
-      const double th = X[ic * d + l] + pl[l];
-      theta[b * d + l] = th;
-      if (lo) {
-        const double x = (th - lo[l]) / scale[l];
-        ok = ok && (x >= 0.0) && (x <= 1.0);
-      }
-    }
-  }
-  idx[b] = i;
-  sup[b] = ok ? 1 : 0;
-}
-
 // bucket table of the CDF: tab[k] = searchsorted(cdf, k / 2^L, 'right')
 __global__ __launch_bounds__(256) void cdf_index_kernel(
     const double* __restrict__ cdf, int64_t n, int log2k,
@@ -922,6 +856,28 @@ __global__ __launch_bounds__(256) void gather_cols_kernel(
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
        i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
     out[s * out_ld + i] = src[s * src_ld + (idx ? idx[i] : i)];
+}
+
+// constant fills and an index ramp (round 6: the calibration / prior
+// generations' distances, flags, positions and unit weights without torch
+// fill kernels)
+__global__ __launch_bounds__(256) void fill_words_kernel(uint64_t* __restrict__ x,
+                                                         int64_t n, uint64_t bits) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    x[i] = bits;
+}
+__global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t* __restrict__ x,
+                                                      int64_t n, uint8_t v) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    x[i] = v;
+}
+__global__ __launch_bounds__(256) void iota_kernel(int64_t* __restrict__ x, int64_t n,
+                                                   int64_t start) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n; i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    x[i] = start + i;
 }
 
 // ---------------------------------------------------------------------------
@@ -1139,20 +1095,6 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
               "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
-  const int form = tuning_knob(kKnobProposeForm, 1);
-  if (d > 8 && form != 0) {  // the chunked d > 8 form (same bits)
-#define LC(DD, EX)                                                              \
-  hipLaunchKernelGGL((propose_chunk_kernel<DD, EX>), dim3(g), dim3(256), 0, st,  \
-                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
-                     idx, in_support, tab, log2k);
-    if (d == 20 && form == 1) { LC(20, true) }
-    else if (d <= 16) { LC(16, false) }
-    else if (d <= 24) { LC(24, false) }
-    else { LC(32, false) }
-#undef LC
-    ABC_LAUNCH_CHECK("propose_chunk_kernel");
-    return kOk;
-  }
 #define LX(DD, EX)                                                              \
   hipLaunchKernelGGL((propose_philox_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
                      X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \
@@ -1263,6 +1205,37 @@ int abc_gather_words(const void* src, int64_t src_ld, int64_t width,
                      dim3(256), 0, st, static_cast<const uint64_t*>(src), src_ld,
                      width, idx, n, static_cast<uint64_t*>(out), out_ld);
   ABC_LAUNCH_CHECK("gather_words_kernel");
+  return kOk;
+}
+
+// x[i] = bits (8-byte words: an fp64 or int64 constant), i < n
+int abc_fill_words(void* x, int64_t n, uint64_t bits, hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "fill_words: n < 0");
+  if (n == 0) return kOk;
+  ABC_REQUIRE(x, "fill_words: null pointer");
+  hipLaunchKernelGGL(fill_words_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256),
+                     0, st, static_cast<uint64_t*>(x), n, bits);
+  ABC_LAUNCH_CHECK("fill_words_kernel");
+  return kOk;
+}
+// x[i] = v (flags), i < n
+int abc_fill_u8(uint8_t* x, int64_t n, int v, hipStream_t st) {
+  ABC_REQUIRE(n >= 0 && v >= 0 && v < 256, "fill_u8: bad arguments");
+  if (n == 0) return kOk;
+  ABC_REQUIRE(x, "fill_u8: null pointer");
+  hipLaunchKernelGGL(fill_u8_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0,
+                     st, x, n, static_cast<uint8_t>(v));
+  ABC_LAUNCH_CHECK("fill_u8_kernel");
+  return kOk;
+}
+// x[i] = start + i, i < n (positions of an all-accepted round)
+int abc_iota_i64(int64_t* x, int64_t n, int64_t start, hipStream_t st) {
+  ABC_REQUIRE(n >= 0, "iota: n < 0");
+  if (n == 0) return kOk;
+  ABC_REQUIRE(x, "iota: null pointer");
+  hipLaunchKernelGGL(iota_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, st,
+                     x, n, start);
+  ABC_LAUNCH_CHECK("iota_kernel");
   return kOk;
 }
 

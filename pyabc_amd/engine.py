@@ -710,9 +710,9 @@ class GenerationEngine:
             if acceptance is None:
                 # calibration sample: everything accepted, distances later
                 # (smc.py:486-514: accepted_distances = [inf])
-                d = torch.full((nv,), math.inf, dtype=F64, device=self.dev)
-                guard = torch.zeros(nv, dtype=torch.uint8, device=self.dev)
-                apos = torch.arange(nv, dtype=torch.int64, device=self.dev)
+                d = K.full(nv, math.inf)
+                guard = K.full(nv, 0, torch.uint8)
+                apos = K.arange(nv)
                 nas = list(nvs)
             elif fuse:
                 a = acceptance
@@ -858,8 +858,8 @@ class GenerationEngine:
         if fit is None:
             logpd = None
             # t = 0: weight = 1 * prod(acceptance weights) (smc.py:762-770)
-            w = accw_acc.clone() if stochastic else torch.ones(
-                theta_acc.shape[0], dtype=F64, device=self.dev)
+            w = accw_acc.clone() if stochastic else K.full(
+                theta_acc.shape[0], 1.0)
         else:
             # row-parallel weight pass: rank r weights rows row_range(n)
             lo, hi = self.row_range(theta_acc.shape[0])

@@ -172,6 +172,30 @@ def gather_rows(src, idx, n=None):
     return out if src.dim() == 2 else out.view(-1)
 
 
+def full(n, value, dtype=F64):
+    """A device vector of n copies of ``value`` (fp64 / int64: abc_fill_words;
+    uint8: abc_fill_u8) -- torch.full without torch's fill kernel."""
+    out = torch.empty(n, dtype=dtype, device=_dev())
+    if dtype == torch.uint8:
+        call("abc_fill_u8", ptr(out), n, int(value), nat.stream())
+        return out
+    if dtype == F64:
+        bits = int(np.array(value, dtype=np.float64).view(np.uint64))
+    elif dtype == torch.int64:
+        bits = int(np.array(value, dtype=np.int64).view(np.uint64))
+    else:
+        raise TypeError(f"full: unsupported dtype {dtype}")
+    call("abc_fill_words", ptr(out), n, bits, nat.stream())
+    return out
+
+
+def arange(n, start=0):
+    """int64 start .. start + n - 1 on the device (abc_iota_i64)."""
+    out = torch.empty(n, dtype=torch.int64, device=_dev())
+    call("abc_iota_i64", ptr(out), n, int(start), nat.stream())
+    return out
+
+
 def radix_sort_pairs(keys, vals, end_bit=64):
     """Stable sort of (uint64 key as int64 bits, int32 value) pairs by the
     low ``end_bit`` key bits (abc_radix_sort_pairs_u64, the spatial index's

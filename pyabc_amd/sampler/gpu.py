@@ -23,6 +23,7 @@ from ..distributed import Comm
 from ..engine import GenerationEngine, StochasticAcceptance
 from ..population import ColumnarPopulation
 from ..batch_models import BatchModel
+from .. import kernels as K
 
 
 class BatchSpec:
@@ -184,7 +185,7 @@ class GPUBatchSampler(Sampler):
             if not res.ok:
                 return self._not_ok(res, record)
             # calibration distances are computed later (smc.py:516-534)
-            res.d = torch.full_like(res.w, np.inf)
+            res.d = K.full(res.w.numel(), np.inf)
         else:
             fit = spec.transitions[0].device_fit if spec.t > 0 and \
                 spec.transitions[0].device_fit is not None else None

@@ -106,14 +106,12 @@ def test_radix_sort_stable(n, end_bit, kind):
 
 
 @pytest.mark.parametrize("d", [9, 12, 17, 20, 23, 31])
-def test_propose_chunk_forms_bit_identical(d):
-    """The d > 8 proposal kernel that consumes each Box-Muller pair as it is
-    drawn (ABC_PROPOSE_FORM 1 / 2, default 1) against the round-5 kernel
-    (form 0) and the unindexed entry: theta, resample indices and support
+def test_propose_indexed_equals_unindexed_d_gt_8(d):
+    """d > 8 proposals (the runtime-d kernel) with the CDF bucket table
+    against the plain binary search: theta, resample indices and support
     flags bit for bit (multivariatenormal.py:87-95 restated in-kernel)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    import os
     from pyabc_amd import kernels as K
     rng = np.random.default_rng(d)
     N, B = 5000, 70_001
@@ -121,25 +119,11 @@ def test_propose_chunk_forms_bit_identical(d):
     w = rng.pareto(1.5, size=N) + 0.01
     cdf = K.resample_cdf(_dev(w / w.sum()))
     tab = K.cdf_index(cdf)
-    Am = rng.normal(size=(d, d)) * 0.3
-    A = _dev(Am)
+    A = _dev(rng.normal(size=(d, d)) * 0.3)
     lo = _dev(np.full(d, -2.5))
     sc = _dev(np.full(d, 5.0))
     ref = K.propose_philox(X, cdf, A, lo, sc, 11, 3, 12345, B)
-    old = os.environ.get("ABC_PROPOSE_FORM")
-    try:
-        for form in ("0", "1", "2"):
-            os.environ["ABC_PROPOSE_FORM"] = form
-            K.reload_tuning()
-            got = K.propose_philox(X, cdf, A, lo, sc, 11, 3, 12345, B,
-                                   tab=tab)
-            for a, b in zip(got, ref):
-                np.testing.assert_array_equal(a.cpu().numpy(),
-                                              b.cpu().numpy(), err_msg=form)
-    finally:
-        if old is None:
-            os.environ.pop("ABC_PROPOSE_FORM", None)
-        else:
-            os.environ["ABC_PROPOSE_FORM"] = old
-        K.reload_tuning()
+    got = K.propose_philox(X, cdf, A, lo, sc, 11, 3, 12345, B, tab=tab)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     assert 0.001 < float(ref[2].float().mean()) < 0.999

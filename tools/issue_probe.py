@@ -31,7 +31,12 @@ MIXES = {0: "d<=8 folded: 5 MFMA, 16 v_exp_f32, 23 v_add_f32",
          20: "mix 13 as 16x16x32 f16: 4 tiles x (1 hi + 4 lo) = 20 MFMA, "
              "16 v_exp_f32, 28 v_add_f32 per 1024 pairs",
          21: "mix 12 as 16x16x32 f16: 4 tiles x (1 hi + 2 lo) = 12 MFMA, "
-             "16 v_exp_f32, 22 v_add_f32 per 1024 pairs"}
+             "16 v_exp_f32, 22 v_add_f32 per 1024 pairs",
+         22: "d<=8 folded f16, PMC mix without the MFMAs in VALU: 4 MFMA, "
+             "16 v_exp_f32, 17 v_add_f32",
+         23: "d<=8 folded f16: 4 MFMA, 16 v_exp_f32, 18 v_add_f32",
+         24: "d=20 folded f16, PMC mix without the MFMAs in VALU: 9 MFMA, "
+             "16 v_exp_f32, 18 v_add_f32"}
 
 
 def parse():

@@ -357,6 +357,13 @@ double abc_probe_kde_mix(int variant, int waves_per_simd, int iters) {
     case 20: ns = time_mix16<20, 16, 28>(waves_per_simd, iters, cus, out); break;
     // the d = 8 mix 12 in that shape: 4 x (1 hi + 2 lo) = 12 MFMAs
     case 21: ns = time_mix16<12, 16, 22>(waves_per_simd, iters, cus, out); break;
+    // round 6: the kernels' PMC mixes with SQ_INSTS_VALU's MFMAs taken out
+    // (the counter includes them: this probe's mix 12 reads 42.0 VALU per
+    // step = 4 MFMA + 16 exp + 22 adds): d = 8 4 MFMA, 16 exp, 17.5 other
+    // (22 / 23 average it), d = 20 9 MFMA, 16 exp, 18 other (24)
+    case 22: ns = time_mix<4, 16, 17>(waves_per_simd, iters, cus, out); break;
+    case 23: ns = time_mix<4, 16, 18>(waves_per_simd, iters, cus, out); break;
+    case 24: ns = time_mix<9, 16, 18>(waves_per_simd, iters, cus, out); break;
     default: break;
   }
   (void)hipFree(src);

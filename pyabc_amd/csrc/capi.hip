@@ -22,7 +22,7 @@ constexpr const char* kKnobNames[kKnobCount] = {
     "ABC_KDE_MFMA_SPLIT", "ABC_KDE_MFMA_IB",   "ABC_KDE_MFMA_PIPE",
     "ABC_KDE_MFMA_LDS2",  "ABC_KDE_MFMA_SMAJOR", "ABC_KDE_TIER",
     "ABC_LZ_IB",          "ABC_LZ_TPB",          "ABC_KNN_ROWS",
-    "ABC_KDE_PARENT_SHIFT", "ABC_KDE_PARENT_WIN"};
+    "ABC_KDE_PARENT_SHIFT", "ABC_KDE_PARENT_WIN", "ABC_PROPOSE_GROUP"};
 std::atomic<int> g_knobs[kKnobCount];
 std::once_flag g_knobs_once;
 

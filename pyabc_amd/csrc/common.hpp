@@ -46,6 +46,7 @@ enum Knob : int {
   // bits within the derived bound (kde_mfma.hip, "refine")
   kKnobKdeParentShift,    // ABC_KDE_PARENT_SHIFT
   kKnobKdeParentWin,      // ABC_KDE_PARENT_WIN
+  kKnobProposeGroup,      // ABC_PROPOSE_GROUP (1 four lanes per proposal, 0 one)
   kKnobCount
 };
 // the knob's integer value, or dflt when the variable is unset

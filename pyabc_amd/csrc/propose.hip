@@ -700,6 +700,92 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
                         sup + b, 0, tab, log2k);
 }
 
+// Round 6: four lanes per proposal.  One lane
+// per proposal (propose_philox_kernel) keeps d normals and d outputs live
+// (108 VGPRs at d = 20: four waves per SIMD) and every load instruction of
+// the CDF search and the X row touches 64 unrelated lines; its waves spend
+// ~75 % of their life waiting on those loads (PMC, profiles/r06_propose_pmc
+// .json).  Here lane q of a proposal's group of four draws Box-Muller pairs
+// q, q + 4, ... of the proposal's normal range and owns outputs l = q,
+// q + 4, ...; z_k reaches the other lanes by a group shuffle, k ascending,
+// so every output's fma chain is perturb_one's (k ascending from 0.0) and
+// u, z and theta are the same bits.  The group's four lanes search the same
+// CDF addresses (one line request instead of four) and read / write the X
+// and theta rows as contiguous 32-byte runs.  OUT = outputs per lane, PR =
+// pairs per lane.
+template <int OUT, int PR>
+__global__ __launch_bounds__(256) void propose_group_kernel(
+    const double* __restrict__ X, int64_t N, int d,
+    const double* __restrict__ cdf, const double* __restrict__ A,
+    const double* __restrict__ lo, const double* __restrict__ scale,
+    uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
+    double* __restrict__ theta, int64_t* __restrict__ idx,
+    uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
+  extern __shared__ double As[];  // d * d
+  for (int i = threadIdx.x; i < d * d; i += blockDim.x) As[i] = A[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;
+  const int gbase = lane & ~3;
+  const int64_t b = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2;
+  const bool live = b < B;
+  const int64_t bb = live ? b : B - 1;  // padding lanes redo the last proposal
+  const uint64_t ui = offset + static_cast<uint64_t>(bb);
+  const u32x4 ub = philox_block(seed, 2 * sid, ui >> 1);
+  const double u = (ui & 1) ? u53(ub.z, ub.w) : u53(ub.x, ub.y);
+  const int64_t i = search_right(cdf, N, u, tab, log2k);
+  const int64_t ic = i < N ? i : N - 1;
+  const uint64_t zi0 = ui * static_cast<uint64_t>(d);
+  const uint64_t p0 = zi0 >> 1;
+  const int odd = static_cast<int>(zi0 & 1);
+  const int np = (d + odd + 1) >> 1;  // pairs touching components 0 .. d-1
+  double zc[PR], zs[PR];
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    zc[r] = zs[r] = 0.0;
+    const int pr = q + 4 * r;
+    if (pr < np) box_muller(philox_block(seed, 2 * sid + 1, p0 + pr), zc[r], zs[r]);
+  }
+  double pl[OUT];
+#pragma unroll
+  for (int m = 0; m < OUT; ++m) pl[m] = 0.0;
+  // component k = 2 pr + br - odd: pair pr = (k + odd) >> 1, branch
+  // (k + odd) & 1, owned by lane pr & 3 of the group, register pr >> 2
+  for (int k = 0; k < d; ++k) {
+    const int kk = k + odd;
+    const int pr = kk >> 1, br = kk & 1, rr = pr >> 2;
+    double c = 0.0;
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+      if (r == rr) c = br ? zs[r] : zc[r];
+    const double z = __shfl(c, gbase + (pr & 3), 64);
+    const double* __restrict__ Ak = As + k * d;
+#pragma unroll
+    for (int m = 0; m < OUT; ++m) {
+      const int l = q + 4 * m;
+      if (l < d) pl[m] = fma(z, Ak[l], pl[m]);
+    }
+  }
+  bool ok = true;
+#pragma unroll
+  for (int m = 0; m < OUT; ++m) {
+    const int l = q + 4 * m;
+    if (l < d) {
+      const double th = X[ic * d + l] + pl[m];
+      if (live) theta[bb * d + l] = th;
+      if (lo) {
+        const double x = (th - lo[l]) / scale[l];
+        ok = ok && (x >= 0.0) && (x <= 1.0);
+      }
+    }
+  }
+  const uint64_t bad = __ballot(!ok);
+  if (live && q == 0) {
+    idx[bb] = i;
+    sup[bb] = ((bad >> gbase) & 0xFull) ? 0 : 1;
+  }
+}
+
 // bucket table of the CDF: tab[k] = searchsorted(cdf, k / 2^L, 'right')
 __global__ __launch_bounds__(256) void cdf_index_kernel(
     const double* __restrict__ cdf, int64_t n, int log2k,
@@ -1095,6 +1181,26 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
   ABC_REQUIRE((lo == nullptr) == (scale == nullptr),
               "propose: lo and scale must both be given or NULL");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
+  if (tuning_knob(kKnobProposeGroup, 1) != 0) {
+    // four lanes per proposal (same bits as propose_philox_kernel; N = 1e6,
+    // 4.2e6 proposals, tools/propose_group.py, call r06k: d = 4 0.398 ->
+    // 0.227 ms, d = 6 0.657 -> 0.265, d = 8 0.350 -> 0.283, d = 20 1.690 ->
+    // 0.755)
+    const unsigned gg = static_cast<unsigned>(ceil_div(B * 4, 256));
+    const size_t lds = static_cast<size_t>(d) * d * sizeof(double);
+#define LG(O, P)                                                                  \
+  hipLaunchKernelGGL((propose_group_kernel<O, P>), dim3(gg), dim3(256), lds, st,   \
+                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,      \
+                     idx, in_support, tab, log2k);
+    if (d <= 4) { LG(1, 1) }
+    else if (d <= 8) { LG(2, 2) }
+    else if (d <= 16) { LG(4, 3) }
+    else if (d <= 24) { LG(6, 4) }
+    else { LG(8, 5) }
+#undef LG
+    ABC_LAUNCH_CHECK("propose_group_kernel");
+    return kOk;
+  }
 #define LX(DD, EX)                                                              \
   hipLaunchKernelGGL((propose_philox_kernel<DD, EX>), dim3(g), dim3(256), 0, st, \
                      X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,    \

@@ -106,8 +106,22 @@ def resample_perturb(X, cdf, u, z, A, lo=None, scale=None):
 CDF_INDEX_LOG2 = 16
 
 
-def cdf_index(cdf, log2k=CDF_INDEX_LOG2):
-    """Bucket table tab[k] = searchsorted(cdf, k / 2^log2k, 'right')."""
+def cdf_index_log2(n):
+    """Bucket-table size for an n-particle CDF: about four buckets per
+    particle (2^22 at n = 1e6), so the proposal's search is the two table
+    reads plus ~1 CDF read.  Round 6 (tools/propose_tab.py, N = 1e6, 4.2e6
+    proposals): 2^16 -> 2^22 buckets cut the proposal kernel 0.451 -> 0.359
+    ms at d = 8 and 1.85 -> 1.69 ms at d = 20 (indices identical); the table
+    costs 8 B per bucket and one search per bucket, on the side stream."""
+    L = max(int(n) - 1, 1).bit_length() + 2
+    return min(22, max(CDF_INDEX_LOG2, L))
+
+
+def cdf_index(cdf, log2k=None):
+    """Bucket table tab[k] = searchsorted(cdf, k / 2^log2k, 'right')
+    (log2k None: :func:`cdf_index_log2` of the CDF's length)."""
+    if log2k is None:
+        log2k = cdf_index_log2(cdf.numel())
     tab = torch.empty((1 << log2k) + 1, dtype=torch.int64, device=_dev())
     call("abc_cdf_index_f64", ptr(_contig(cdf, F64)), cdf.numel(), log2k,
          ptr(tab), nat.stream())

@@ -36,14 +36,22 @@ HOT = [
     ("void abc::kde_mfma_lds2g_kernel<1, 3, 3, 2, false, 4>", 0, 2, 12),
     # LocalTransition density (z form) at every dimension and shape
     ("void abc::lz_kernel<", 0, 0, 0),
-    # the MVN proposal (A staged in LDS since round 5: no SGPR spills)
+    # the MVN proposal (A staged in LDS since round 5: no SGPR spills), and
+    # the four-lanes-per-proposal default of round 6 (44-59 VGPRs: eight
+    # waves per SIMD)
     ("void abc::propose_philox_kernel<", 0, 0, 0),
+    ("void abc::propose_group_kernel<", 0, 0, 0),
     # the kNN default (4 rows per wave): spills outside the tile loop only;
     # the ceiling guards against the round-5 regression (the row pinned to
     # VGPRs, DESIGN.md section 4 "LocalTransition kNN design")
     ("void abc::knn_kernel<6, 1, 4>", 48, 0, 0),
     # the previous population's pack (rows and matrix staged in LDS)
     ("void abc::pack_prev_kernel<", 0, 0, 0),
+    # the spatial index's radix sort (round 6, replaces rocPRIM)
+    ("abc::rs_", 0, 0, 0),
+    # the accepted-row word gathers
+    ("abc::gather_words_kernel", 0, 0, 0),
+    ("abc::gather_cols_kernel", 0, 0, 0),
 ] + [
     # the LocalTransition proposal, one instantiation per d <= 8: the
     # Cholesky factor in registers (the runtime-d form kept it in scratch)

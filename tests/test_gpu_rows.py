@@ -105,11 +105,13 @@ def test_radix_sort_stable(n, end_bit, kind):
     np.testing.assert_array_equal(got_k, keys[order])
 
 
-@pytest.mark.parametrize("d", [9, 12, 17, 20, 23, 31])
-def test_propose_indexed_equals_unindexed_d_gt_8(d):
-    """d > 8 proposals (the runtime-d kernel) with the CDF bucket table
-    against the plain binary search: theta, resample indices and support
-    flags bit for bit (multivariatenormal.py:87-95 restated in-kernel)."""
+@pytest.mark.parametrize("d", [1, 2, 3, 5, 8, 9, 12, 17, 20, 23, 31, 32])
+def test_propose_group_equals_single_lane(d):
+    """The indexed entry's proposal kernel (four lanes per proposal, CDF
+    bucket table) against the unindexed entry's one-lane kernel and plain
+    binary search: theta, resample indices and support flags bit for bit
+    (multivariatenormal.py:87-95 restated in-kernel), an odd B so the last
+    group is partial."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from pyabc_amd import kernels as K

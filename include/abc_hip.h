@@ -448,6 +448,16 @@ int abc_sim_linear_gaussian_pnorm_f64(const double* theta, int64_t B, int d,
                                       const double* fw, double p, double eps,
                                       double* d_out, uint8_t* accept,
                                       uint8_t* guard, hipStream_t stream);
+/* The same pass for rounds whose statistics ARE kept (stored population,
+ * recorded evaluations, adaptive distances): the columns are also written
+ * to out_T (stat-major [S][ld], ld >= B) as abc_sim_linear_gaussian_f64
+ * writes them, so the distance pass does not read them back. */
+int abc_sim_linear_gaussian_pnorm_stats_f64(
+    const double* theta, int64_t B, int d, const double* A, const double* c,
+    int S, double sigma, uint64_t seed, uint64_t sid, uint64_t offset,
+    const double* x0, const double* fw, double p, double eps, double* d_out,
+    uint8_t* accept, uint8_t* guard, double* out_T, int64_t ld,
+    hipStream_t stream);
 int abc_sim_gaussian_mean_f64(const double* theta, int64_t B, double sigma,
                               uint64_t seed, uint64_t sid, uint64_t offset,
                               double* out, hipStream_t stream);

@@ -216,6 +216,10 @@ _SIGS = {
                                                   c_u64, c_u64, c_ptr, c_ptr,
                                                   c_dbl, c_dbl, c_ptr, c_ptr,
                                                   c_ptr, c_ptr]),
+    "abc_sim_linear_gaussian_pnorm_stats_f64": (
+        c_int, [c_ptr, c_i64, c_int, c_ptr, c_ptr, c_int, c_dbl, c_u64, c_u64,
+                c_u64, c_ptr, c_ptr, c_dbl, c_dbl, c_ptr, c_ptr, c_ptr, c_ptr,
+                c_i64, c_ptr]),
     "abc_sim_gaussian_mean_f64": (c_int, [c_ptr, c_i64, c_dbl, c_u64, c_u64,
                                           c_u64, c_ptr, c_ptr]),
 }

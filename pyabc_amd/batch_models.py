@@ -65,13 +65,17 @@ class LinearGaussianModel(BatchModel):
         return K.sim_linear_gaussian(theta, A, c, self.sigma, seed, sid,
                                      offset)
 
-    def simulate_distance(self, theta, seed, sid, offset, x0, fw, p, eps):
-        """simulate + p-norm distance + d <= eps in one pass, statistics not
-        stored (their rows in the model's key order): (d, accept, guard),
-        bit-identical to simulate() followed by the distance kernel."""
+    def simulate_distance(self, theta, seed, sid, offset, x0, fw, p, eps,
+                          keep_stats=False):
+        """simulate + p-norm distance + d <= eps in one pass (x0 / fw rows
+        in the model's key order): (d, accept, guard), bit-identical to
+        simulate() followed by the distance kernel; ``keep_stats``: the
+        statistics simulate() returns as a fourth item, written by the same
+        pass."""
         A, c = self._tensors()
         return K.sim_linear_gaussian_pnorm(theta, A, c, self.sigma, seed, sid,
-                                           offset, x0, fw, p, eps)
+                                           offset, x0, fw, p, eps,
+                                           keep_stats=keep_stats)
 
     def simulate_host(self, theta, rng):
         """numpy reference of the same model (for CPU baselines)."""

@@ -101,20 +101,35 @@ __global__ __launch_bounds__(256) void sim_linear_gaussian_kernel(
 // straight into pnorm_kernel's key-ordered chain, so distances, accept and
 // guard flags are bit-identical to the two-kernel path while the 8 S bytes
 // per evaluation are neither written nor read back (test_sim_pnorm_fused).
-template <int PMODE>
+// Round 6: DMAX-sized theta rows (the 32-entry array held 64 VGPRs at any
+// d) and, when they fit (LDS_A), the model matrix A and c staged in LDS
+// once per block -- read as broadcast LDS loads instead of one scalar load
+// per element and statistic.  Same products, same order: the same bits.
+template <int PMODE, int DMAX, bool LDS_A>
 __global__ __launch_bounds__(256) void sim_lg_pnorm_kernel(
     const double* __restrict__ theta, int64_t B, int d,
-    const double* __restrict__ A, const double* __restrict__ c, int S,
+    const double* __restrict__ Ag, const double* __restrict__ cg, int S,
     double sigma, uint64_t seed, uint64_t sid, uint64_t offset,
     const double* __restrict__ x0, const double* __restrict__ fw, double p,
     double eps, double* __restrict__ d_out, uint8_t* __restrict__ accept,
-    uint8_t* __restrict__ guard) {
+    uint8_t* __restrict__ guard, double* __restrict__ out_T, int64_t ld) {
 #pragma clang fp contract(off)  // as pnorm_kernel; the fmas are explicit
+  extern __shared__ double smem[];
+  const double* __restrict__ A = Ag;
+  const double* __restrict__ c = cg;
+  if constexpr (LDS_A) {
+    for (int i = threadIdx.x; i < S * d; i += blockDim.x) smem[i] = Ag[i];
+    if (cg)
+      for (int i = threadIdx.x; i < S; i += blockDim.x) smem[S * d + i] = cg[i];
+    __syncthreads();
+    A = smem;
+    c = cg ? smem + S * d : nullptr;
+  }
   const int64_t b = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  double th[32];
+  double th[DMAX];
 #pragma unroll
-  for (int k = 0; k < 32; ++k) th[k] = k < d ? theta[b * d + k] : 0.0;
+  for (int k = 0; k < DMAX; ++k) th[k] = k < d ? theta[b * d + k] : 0.0;
   const uint64_t base = (offset + static_cast<uint64_t>(b)) * static_cast<uint64_t>(S);
   float z4[4] = {0.f, 0.f, 0.f, 0.f};
   uint64_t have = ~0ull;
@@ -122,7 +137,7 @@ __global__ __launch_bounds__(256) void sim_lg_pnorm_kernel(
   for (int s = 0; s < S; ++s) {
     double acc = c ? c[s] : 0.0;
 #pragma unroll
-    for (int k = 0; k < 32; ++k)
+    for (int k = 0; k < DMAX; ++k)
       if (k < d) acc = fma(A[s * d + k], th[k], acc);
     const uint64_t zi = base + s;
     if ((zi >> 2) != have) {
@@ -130,6 +145,7 @@ __global__ __launch_bounds__(256) void sim_lg_pnorm_kernel(
       have = zi >> 2;
     }
     const double y = fma(sigma, static_cast<double>(z4[zi & 3]), acc);
+    if (out_T) out_T[static_cast<int64_t>(s) * ld + b] = y;  // kept statistics
     const double t = fabs(fw[s] * (y - x0[s]));
     if (PMODE == 1)
       acc2 += t;
@@ -213,6 +229,12 @@ int abc_sim_linear_gaussian_f64(const double* theta, int64_t B, int d,
   return kOk;
 }
 
+int abc_sim_linear_gaussian_pnorm_stats_f64(
+    const double* theta, int64_t B, int d, const double* A, const double* c, int S,
+    double sigma, uint64_t seed, uint64_t sid, uint64_t offset, const double* x0,
+    const double* fw, double p, double eps, double* d_out, uint8_t* accept,
+    uint8_t* guard, double* out_T, int64_t ld, hipStream_t st);
+
 int abc_sim_linear_gaussian_pnorm_f64(const double* theta, int64_t B, int d,
                                       const double* A, const double* c, int S,
                                       double sigma, uint64_t seed, uint64_t sid,
@@ -220,26 +242,62 @@ int abc_sim_linear_gaussian_pnorm_f64(const double* theta, int64_t B, int d,
                                       const double* fw, double p, double eps,
                                       double* d_out, uint8_t* accept,
                                       uint8_t* guard, hipStream_t st) {
+  return abc_sim_linear_gaussian_pnorm_stats_f64(theta, B, d, A, c, S, sigma, seed,
+                                                 sid, offset, x0, fw, p, eps, d_out,
+                                                 accept, guard, nullptr, 0, st);
+}
+
+// The same pass writing the statistics too (stat-major [S][ld], the columns
+// sim_linear_gaussian_kernel writes): the kept-statistics rounds of the
+// sampler (History, adaptive distances) no longer read them back for the
+// distance (round 6)
+int abc_sim_linear_gaussian_pnorm_stats_f64(
+    const double* theta, int64_t B, int d, const double* A, const double* c, int S,
+    double sigma, uint64_t seed, uint64_t sid, uint64_t offset, const double* x0,
+    const double* fw, double p, double eps, double* d_out, uint8_t* accept,
+    uint8_t* guard, double* out_T, int64_t ld, hipStream_t st) {
   ABC_REQUIRE(d >= 1 && d <= 32 && S >= 1 && B >= 0,
               "sim_linear_gaussian_pnorm: bad sizes (d <= 32)");
+  ABC_REQUIRE(!out_T || ld >= B, "sim_linear_gaussian_pnorm: ld < B");
   ABC_REQUIRE(p >= 1.0, "sim_linear_gaussian_pnorm: It must be p >= 1");
   if (B == 0) return kOk;
   ABC_REQUIRE(theta && A && x0 && fw && d_out,
               "sim_linear_gaussian_pnorm: null pointer");
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
-#define L(PM)                                                                    \
-  hipLaunchKernelGGL(sim_lg_pnorm_kernel<PM>, dim3(g), dim3(256), 0, st, theta, B, \
-                     d, A, c, S, sigma, seed, sid, offset, x0, fw, p, eps, d_out, \
-                     accept, guard)
-  if (std::isinf(p))
-    L(3);
-  else if (p == 1.0)
-    L(1);
-  else if (p == 2.0)
-    L(2);
-  else
-    L(0);
+  const size_t lds = static_cast<size_t>(S) * (d + 1) * sizeof(double);
+  const bool in_lds = lds <= 48 * 1024;
+#define LK(PM, DM, LA)                                                             \
+  hipLaunchKernelGGL((sim_lg_pnorm_kernel<PM, DM, LA>), dim3(g), dim3(256),         \
+                     LA ? lds : 0, st, theta, B, d, A, c, S, sigma, seed, sid,      \
+                     offset, x0, fw, p, eps, d_out, accept, guard, out_T, ld)
+#define LD(PM, DM) \
+  if (in_lds) {    \
+    LK(PM, DM, true);  \
+  } else {         \
+    LK(PM, DM, false); \
+  }
+#define L(PM)                  \
+  if (d <= 8) {                \
+    LD(PM, 8)                  \
+  } else if (d <= 16) {        \
+    LD(PM, 16)                 \
+  } else if (d <= 24) {        \
+    LD(PM, 24)                 \
+  } else {                     \
+    LD(PM, 32)                 \
+  }
+  if (std::isinf(p)) {
+    L(3)
+  } else if (p == 1.0) {
+    L(1)
+  } else if (p == 2.0) {
+    L(2)
+  } else {
+    L(0)
+  }
 #undef L
+#undef LD
+#undef LK
   ABC_LAUNCH_CHECK("sim_lg_pnorm_kernel");
   return kOk;
 }

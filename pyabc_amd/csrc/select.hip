@@ -1636,42 +1636,6 @@ __global__ __launch_bounds__(256) void col_std_kernel(const double* __restrict__
 // sw - sw2/sw as np.cov(aweights) does)
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void moments1_kernel(const T* __restrict__ X,
-                                                       const T* __restrict__ w,
-                                                       int64_t n, int d,
-                                                       double* __restrict__ part) {
-  __shared__ double red[4];
-  const int nv = 2 + d;
-  for (int v = 0; v < nv; ++v) {
-    double s = 0.0;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
-         i += static_cast<int64_t>(gridDim.x) * 256) {
-      const double wi = static_cast<double>(w[i]);
-      s += v == 0 ? wi
-                  : (v == 1 ? wi * wi
-                            : wi * static_cast<double>(X[i * d + (v - 2)]));
-    }
-    s = block_sum<double, 256>(s, red);
-    if (threadIdx.x == 0) part[blockIdx.x * nv + v] = s;
-  }
-}
-
-__global__ __launch_bounds__(256) void moments1_final_kernel(const double* __restrict__ part,
-                                                             int np, int d,
-                                                             double* __restrict__ out) {
-  __shared__ double red[4];
-  const int nv = 2 + d;
-  for (int v = 0; v < nv; ++v) {
-    double s = 0.0;
-    for (int b = threadIdx.x; b < np; b += 256) s += part[b * nv + v];
-    s = block_sum<double, 256>(s, red);
-    if (threadIdx.x == 0) out[v] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < d) out[2 + threadIdx.x] = out[2 + threadIdx.x] / out[0];
-}
-
-template <typename T>
 __global__ __launch_bounds__(256) void moments2_kernel(const T* __restrict__ X,
                                                        const T* __restrict__ w,
                                                        int64_t n, int d,
@@ -1717,24 +1681,6 @@ __global__ __launch_bounds__(256) void moments2_kernel(const T* __restrict__ X,
   }
   for (int q = 0; q < 3; ++q)
     if (threadIdx.x + q * 256 < np) part[blockIdx.x * np + threadIdx.x + q * 256] = acc[q];
-}
-
-__global__ __launch_bounds__(256) void moments2_final_kernel(const double* __restrict__ part,
-                                                             int nb, int d,
-                                                             double* __restrict__ out) {
-  const int np = d * (d + 1) / 2;
-  for (int p = threadIdx.x; p < np; p += 256) {
-    double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += part[b * np + p];
-    int k = 0, q = p;
-    while (q >= d - k) {
-      q -= d - k;
-      ++k;
-    }
-    const int l = k + q;
-    out[2 + d + k * d + l] = s;
-    out[2 + d + l * d + k] = s;
-  }
 }
 
 // Single-pass register forms for d <= 8 (the benchmark dimensions): every
@@ -1837,6 +1783,43 @@ __global__ __launch_bounds__(64) void moments_final_wave_kernel(
   }
 }
 
+// d > 8 (round 6): pass 1 in one read of (X, w) with the 2 + d sums in
+// registers (runtime d <= DMAX; the column form above made 2 + d strided
+// passes: 0.38 ms at N = 1e6, d = 20), pass 2 the 64-row LDS tiles of
+// moments2_kernel on kMom2Grid blocks (eight per CU instead of one: the
+// tile loads' latency overlaps), both finished by the wave-per-value sum.
+constexpr int kMom2Grid = 2048;
+
+template <typename T, int DMAX>
+__global__ __launch_bounds__(256) void moments1_wide_kernel(
+    const T* __restrict__ X, const T* __restrict__ w, int64_t n, int d,
+    double* __restrict__ part) {
+  constexpr int NV = 2 + DMAX;
+  __shared__ double lds[4][NV];
+  double v[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const double wi = static_cast<double>(w[i]);
+    v[0] += wi;
+    v[1] = fma(wi, wi, v[1]);
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k)
+      if (k < d) v[2 + k] = fma(wi, static_cast<double>(X[i * d + k]), v[2 + k]);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const double r = wave_sum(v[q]);
+    if (lane == 0) lds[wid][q] = r;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 2 + d; q += blockDim.x)
+    part[static_cast<int64_t>(blockIdx.x) * (2 + d) + q] =
+        ((lds[0][q] + lds[1][q]) + lds[2][q]) + lds[3][q];
+}
+
 __global__ void moments_mu_kernel(double* __restrict__ out, int d) {
   if (threadIdx.x < d) out[2 + threadIdx.x] = out[2 + threadIdx.x] / out[0];
 }
@@ -1862,7 +1845,7 @@ __global__ __launch_bounds__(256) void scale_kernel(double* __restrict__ x, int6
 
 size_t moments_ws_bytes(int d) {
   const int np = d * (d + 1) / 2;
-  const int grid = kMomGrid > kRedGrid ? kMomGrid : kRedGrid;
+  const int grid = kMom2Grid;
   return static_cast<size_t>(grid) * 8 * ((2 + d) > np ? (2 + d) : np) + 256;
 }
 
@@ -1898,14 +1881,19 @@ int moments_impl(const T* X, const T* w, int64_t n, int d, double* out,
     ABC_LAUNCH_CHECK("moments kernels");
     return kOk;
   }
-  hipLaunchKernelGGL(moments1_kernel<T>, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
-                     d, part);
-  hipLaunchKernelGGL(moments1_final_kernel, dim3(1), dim3(256), 0, st, part,
-                     kRedGrid, d, out);
-  hipLaunchKernelGGL(moments2_kernel<T>, dim3(kRedGrid), dim3(256), 0, st, X, w, n,
+  if (d <= 16)
+    hipLaunchKernelGGL((moments1_wide_kernel<T, 16>), dim3(kMomGrid), dim3(256), 0, st,
+                       X, w, n, d, part);
+  else
+    hipLaunchKernelGGL((moments1_wide_kernel<T, 32>), dim3(kMomGrid), dim3(256), 0, st,
+                       X, w, n, d, part);
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(2 + d), dim3(64), 0, st, part,
+                     kMomGrid, 2 + d, d, 1, out);
+  hipLaunchKernelGGL(moments_mu_kernel, dim3(1), dim3(64), 0, st, out, d);
+  hipLaunchKernelGGL(moments2_kernel<T>, dim3(kMom2Grid), dim3(256), 0, st, X, w, n,
                      d, out, part);
-  hipLaunchKernelGGL(moments2_final_kernel, dim3(1), dim3(256), 0, st, part,
-                     kRedGrid, d, out);
+  hipLaunchKernelGGL(moments_final_wave_kernel, dim3(d * (d + 1) / 2), dim3(64), 0,
+                     st, part, kMom2Grid, d * (d + 1) / 2, d, 2, out);
   ABC_LAUNCH_CHECK("moments kernels");
   return kOk;
 }

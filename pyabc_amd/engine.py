@@ -373,6 +373,18 @@ def mirrors_simulate(model):
     return o is not None and o is owner("simulate")
 
 
+def fused_keeps_stats(model):
+    """True when the model's ``simulate_distance`` can also return the
+    statistics it simulates (a ``keep_stats`` parameter): rounds that keep
+    them then run one pass instead of simulate() + the distance kernel."""
+    import inspect
+    try:
+        return "keep_stats" in inspect.signature(
+            model.simulate_distance).parameters
+    except (TypeError, ValueError):
+        return False
+
+
 def pnorm_host(x, x0, fw, p):
     """One particle's distance exactly as the reference evaluates it
     (distance/distance.py:88-100): Python floats, libm ``pow`` for every
@@ -693,10 +705,13 @@ class GenerationEngine:
             my_eval = eval_off + sum(nvs[:r])
             sim_sid = self._stream(t, stream_base + 1)
             # statistics nobody keeps: simulation and distance in one pass
-            fuse = (nv and not keep_stats and not record
-                    and self.fuse_sim_distance
+            # (kept statistics: the same pass writes them, when the model's
+            # fused method can -- round 6)
+            keep_any = bool(keep_stats or record)
+            fuse = (nv and self.fuse_sim_distance
                     and isinstance(acceptance, PNormAcceptance)
-                    and mirrors_simulate(self.model))
+                    and mirrors_simulate(self.model)
+                    and (not keep_any or fused_keeps_stats(self.model)))
             if nv and not fuse:
                 stats = self.model.simulate(theta, self.seed, sim_sid,
                                             my_eval)
@@ -714,6 +729,16 @@ class GenerationEngine:
                 guard = K.full(nv, 0, torch.uint8)
                 apos = K.arange(nv)
                 nas = list(nvs)
+            elif fuse and keep_any:
+                a = acceptance
+                fd = self.model.simulate_distance(
+                    theta, self.seed, sim_sid, my_eval, a.x0, a.fw, a.p, a.eps,
+                    keep_stats=True)
+                stats = fd[3]
+                d, acc, guard, accw, apos, acount, gcount, alast = a.decide(
+                    stats, nv, self.seed, self._stream(t, stream_base + 4),
+                    my_eval, fused=fd[:3] + (None,), need=need1)    # sync 2
+                nas = comm.all_gather_ints(acount)
             elif fuse:
                 a = acceptance
                 fd = self.model.simulate_distance(

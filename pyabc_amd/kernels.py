@@ -711,16 +711,25 @@ def sim_linear_gaussian(theta, A, c, sigma, seed, sid, offset, out_T=None,
 
 
 def sim_linear_gaussian_pnorm(theta, A, c, sigma, seed, sid, offset, x0, fw,
-                              p, eps=math.inf, B=None):
-    """Fused simulation + p-norm distance + acceptance (no statistics
-    stored): (d, accept, guard), bit-identical to sim_linear_gaussian
-    followed by pnorm_distance."""
+                              p, eps=math.inf, B=None, keep_stats=False):
+    """Fused simulation + p-norm distance + acceptance: (d, accept, guard),
+    bit-identical to sim_linear_gaussian followed by pnorm_distance; with
+    ``keep_stats`` the statistics are written too (stat-major [S, B]) and
+    returned as a fourth item."""
     theta = _contig(theta, F64)
     B = theta.shape[0] if B is None else B
     S, d = A.shape
     dist = torch.empty(B, dtype=F64, device=_dev())
     acc = torch.empty(B, dtype=torch.uint8, device=_dev())
     guard = torch.empty(B, dtype=torch.uint8, device=_dev())
+    if keep_stats:
+        out_T = torch.empty((S, max(B, 1)), dtype=F64, device=_dev())
+        call("abc_sim_linear_gaussian_pnorm_stats_f64", ptr(theta), B, d,
+             ptr(A), ptr(c), S, float(sigma), seed, sid, offset,
+             ptr(_contig(x0, F64)), ptr(_contig(fw, F64)), float(p),
+             float(eps), ptr(dist), ptr(acc), ptr(guard), ptr(out_T),
+             out_T.shape[1], nat.stream())
+        return dist, acc, guard, out_T
     call("abc_sim_linear_gaussian_pnorm_f64", ptr(theta), B, d, ptr(A), ptr(c),
          S, float(sigma), seed, sid, offset, ptr(_contig(x0, F64)),
          ptr(_contig(fw, F64)), float(p), float(eps), ptr(dist), ptr(acc),

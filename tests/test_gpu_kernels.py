@@ -457,11 +457,18 @@ def test_sim_pnorm_fused(K, p):
     followed by abc_pnorm_distance_f64, bit for bit, with and without the
     constant term c."""
     rng = np.random.default_rng(31)
-    B, d, S = 20000, 8, 100
+    # d = 8 / 20 (the DMAX 8 / 24 forms with the model in LDS), S = 700 at
+    # d = 20: A no longer fits the LDS stage (the global-A form)
+    for B, d, S, c in ((20000, 8, 100, None), (20000, 8, 100, 1),
+                       (9001, 20, 100, 1), (3001, 20, 700, 1)):
+        _sim_pnorm_case(K, p, rng, B, d, S, c)
+
+
+def _sim_pnorm_case(K, p, rng, B, d, S, c):
     theta = dev(rng.uniform(-2, 2, size=(B, d)))
-    A = dev(rng.normal(size=(S, d)))
+    A = dev(rng.normal(size=(S, d)) / np.sqrt(d))
     x0, fw = dev(rng.normal(size=S)), dev(rng.uniform(0.5, 2, size=S))
-    for c in (None, dev(rng.normal(size=S))):
+    for c in ((None,) if c is None else (dev(rng.normal(size=S)),)):
         stats = K.sim_linear_gaussian(theta, A, c, 0.5, 7, 13, 12345)
         d1, a1, g1 = K.pnorm_distance(stats, x0, fw, p, 30.0)
         eps = float(np.median(host(d1)))
@@ -471,6 +478,13 @@ def test_sim_pnorm_fused(K, p):
         np.testing.assert_array_equal(host(d1), host(d2))
         np.testing.assert_array_equal(host(a1), host(a2))
         np.testing.assert_array_equal(host(g1), host(g2))
+        # the same pass writing the statistics too (round 6)
+        d3, a3, g3, st3 = K.sim_linear_gaussian_pnorm(
+            theta, A, c, 0.5, 7, 13, 12345, x0, fw, p, eps, keep_stats=True)
+        np.testing.assert_array_equal(host(st3), host(stats))
+        np.testing.assert_array_equal(host(d3), host(d1))
+        np.testing.assert_array_equal(host(a3), host(a1))
+        np.testing.assert_array_equal(host(g3), host(g1))
 
 
 def test_engine_fused_round_equals_unfused(K):
@@ -483,7 +497,8 @@ def test_engine_fused_round_equals_unfused(K):
     x0 = dev(model._x0)
     fw = dev(np.ones(30))
     out = []
-    for fuse in (False, True):
+    for fuse, keep in ((False, False), (True, False), (False, True),
+                       (True, True)):
         eng = GenerationEngine(model, np.full(4, -5.0), np.full(4, 10.0),
                                seed=99)
         eng.fuse_sim_distance = fuse
@@ -491,13 +506,20 @@ def test_engine_fused_round_equals_unfused(K):
         d0, _, _ = K.pnorm_distance(r0.stats_T, x0, fw, 2.0)
         w0 = torch.full((8000,), 1 / 8000, dtype=torch.float64, device="cuda")
         eps = float(np.quantile(host(d0), 0.3))
+        # keep: the kept-statistics rounds (stored population, recorded
+        # evaluations) through the stats-writing fused pass
         res = eng.sample_generation(1, 8000, DeviceMVNFit(r0.theta, w0), x0, fw,
-                                    eps)
+                                    eps, keep_stats=keep, record=keep)
         out.append(res)
-    a, b = out
-    for f in ("theta", "d", "w", "logpd"):
-        np.testing.assert_array_equal(host(getattr(a, f)), host(getattr(b, f)))
-    assert a.n_eval == b.n_eval
+    a = out[0]
+    for b in out[1:]:
+        for f in ("theta", "d", "w", "logpd"):
+            np.testing.assert_array_equal(host(getattr(a, f)),
+                                          host(getattr(b, f)))
+        assert a.n_eval == b.n_eval
+    for f in ("stats_T", "rec_stats_T"):
+        np.testing.assert_array_equal(host(getattr(out[2], f)),
+                                      host(getattr(out[3], f)))
 
 
 def test_pnorm_decide_one_read(K):

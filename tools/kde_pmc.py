@@ -15,8 +15,10 @@ per-tile counts (the issue ceiling):
 with the MI355X_MICROARCH.md per-instruction SIMD issue costs (plain or
 packed fp32 VALU 4 cycles per wave64 instruction -- the round-1 probe's
 2.41 for v_fma_f32 timed SLP-packed pairs --, transcendental 8, an MFMA holding vector
-issue for 8 of its 32 matrix-pipe cycles), SQ_INSTS_VALU counting the
-non-MFMA VALU instructions (TRANS included) and SQ_INSTS_MFMA the MFMAs.
+issue for 8 of its 32 matrix-pipe cycles).  SQ_INSTS_VALU counts the MFMAs
+too (round 6: the issue probe's own mix of 4 MFMA + 16 exp + 22 adds per
+step reads 42.0 under --pmc), so VALU_plain = VALU - TRANS - MFMA; rounds
+2-5 took VALU - TRANS and charged every MFMA twice.
 """
 import collections
 import csv
@@ -64,7 +66,7 @@ def main(prof_dir, tag, N=1_000_000, M=1_000_000, d=8):
     valu = per_tile["SQ_INSTS_VALU"]
     trans = per_tile.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
     mfma = per_tile["SQ_INSTS_MFMA"]
-    issue = 4 * (valu - trans) + 8 * trans + 8 * mfma
+    issue = 4 * (valu - trans - mfma) + 8 * trans + 8 * mfma
     cyc = max(issue, 32 * mfma)
     out = {
         "source": f"rocprofv3 --pmc passes over bench.py ({prof_dir}), "
@@ -77,7 +79,10 @@ def main(prof_dir, tag, N=1_000_000, M=1_000_000, d=8):
         "mfma_pipe_cycles_per_tile": 32 * mfma,
         "ceiling_cycles_per_tile": cyc,
         "cost_model": "plain VALU 4, TRANS 8, MFMA issue 8 / pipe 32 SIMD "
-                      "cycles per wave64 instruction (MI355X_MICROARCH.md)",
+                      "cycles per wave64 instruction (MI355X_MICROARCH.md); "
+                      "plain VALU = SQ_INSTS_VALU - TRANS - MFMA (the "
+                      "counter includes the MFMAs)",
+        "other_valu_per_tile": valu - trans - mfma,
     }
     if "GRBM_GUI_ACTIVE" in avg and "_ns" in avg:
         # GRBM_GUI_ACTIVE is summed over the 8 XCDs

@@ -707,13 +707,25 @@ __global__ __launch_bounds__(256) void propose_philox_kernel(
 // ~75 % of their life waiting on those loads (PMC, profiles/r06_propose_pmc
 // .json).  Here lane q of a proposal's group of four draws Box-Muller pairs
 // q, q + 4, ... of the proposal's normal range and owns outputs l = q,
-// q + 4, ...; z_k reaches the other lanes by a group shuffle, k ascending,
-// so every output's fma chain is perturb_one's (k ascending from 0.0) and
-// u, z and theta are the same bits.  The group's four lanes search the same
-// CDF addresses (one line request instead of four) and read / write the X
-// and theta rows as contiguous 32-byte runs.  OUT = outputs per lane, PR =
-// pairs per lane.
-template <int OUT, int PR>
+// q + 4, ...; every output's fma chain is perturb_one's (k ascending from
+// 0.0), so u, z and theta are the same bits.  The group's four lanes search
+// the same CDF addresses (one line request instead of four) and read / write
+// the X and theta rows as contiguous 32-byte runs.  OUT = outputs per lane
+// (ceil(d / 4)), PR = pairs per lane.
+//
+// LDS: the factor as At[k][q][m] = A[k][q + 4 m] (zero where q + 4 m >= d),
+// so lane q reads its OUT factors of row k as one contiguous run and the
+// fma chain runs unmasked (a zero term leaves an unused accumulator at
+// +0.0); the group's normals as zb[group][2 pr + br] (component k at
+// k + odd), so z_k is one broadcast LDS read.  The first group form picked
+// z_k out of registers with a select chain plus a two-dword shuffle and
+// guarded every fma with an exec-mask branch: ~36 VALU per k (PMC r06m,
+// 1755 VALU per wave at d = 20).
+template <int OUT>
+constexpr int group_pairs() { return (4 * OUT + 2 + 7) / 8; }
+constexpr int kGroupZld(int pr) { return 8 * pr + 1; }  // odd: spreads the banks
+
+template <int OUT>
 __global__ __launch_bounds__(256) void propose_group_kernel(
     const double* __restrict__ X, int64_t N, int d,
     const double* __restrict__ cdf, const double* __restrict__ A,
@@ -721,12 +733,21 @@ __global__ __launch_bounds__(256) void propose_group_kernel(
     uint64_t seed, uint64_t sid, uint64_t offset, int64_t B,
     double* __restrict__ theta, int64_t* __restrict__ idx,
     uint8_t* __restrict__ sup, const int64_t* __restrict__ tab, int log2k) {
-  extern __shared__ double As[];  // d * d
-  for (int i = threadIdx.x; i < d * d; i += blockDim.x) As[i] = A[i];
-  __syncthreads();
+  constexpr int PR = group_pairs<OUT>();
+  constexpr int ZLD = kGroupZld(PR);
+  constexpr int AW = 4 * OUT;
+  extern __shared__ double sh[];
+  double* At = sh;              // d * AW
+  double* zb = sh + d * AW;     // 64 groups * ZLD
+  for (int i = threadIdx.x; i < d * AW; i += blockDim.x) {
+    const int k = i / AW, r = i - k * AW;
+    const int l = (r % OUT) * 4 + r / OUT;  // r = q * OUT + m -> l = q + 4 m
+    At[i] = l < d ? A[k * d + l] : 0.0;
+  }
   const int lane = threadIdx.x & 63;
   const int q = lane & 3;
   const int gbase = lane & ~3;
+  double* zg = zb + (threadIdx.x >> 2) * ZLD;
   const int64_t b = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2;
   const bool live = b < B;
   const int64_t bb = live ? b : B - 1;  // padding lanes redo the last proposal
@@ -739,43 +760,52 @@ __global__ __launch_bounds__(256) void propose_group_kernel(
   const uint64_t p0 = zi0 >> 1;
   const int odd = static_cast<int>(zi0 & 1);
   const int np = (d + odd + 1) >> 1;  // pairs touching components 0 .. d-1
-  double zc[PR], zs[PR];
 #pragma unroll
   for (int r = 0; r < PR; ++r) {
-    zc[r] = zs[r] = 0.0;
     const int pr = q + 4 * r;
-    if (pr < np) box_muller(philox_block(seed, 2 * sid + 1, p0 + pr), zc[r], zs[r]);
+    if (pr < np) {
+      double c0, c1;
+      box_muller(philox_block(seed, 2 * sid + 1, p0 + pr), c0, c1);
+      zg[2 * pr] = c0;
+      zg[2 * pr + 1] = c1;
+    }
   }
+  // the X row's loads go out before the product (clamped column, masked use)
+  double xv[OUT];
+#pragma unroll
+  for (int m = 0; m < OUT; ++m) {
+    const int l = q + 4 * m;
+    xv[m] = X[ic * d + (l < d ? l : d - 1)];
+  }
+  __syncthreads();
   double pl[OUT];
 #pragma unroll
   for (int m = 0; m < OUT; ++m) pl[m] = 0.0;
-  // component k = 2 pr + br - odd: pair pr = (k + odd) >> 1, branch
-  // (k + odd) & 1, owned by lane pr & 3 of the group, register pr >> 2
+  const double* zk = zg + odd;
+  const double* ak = At + q * OUT;
+#pragma unroll 2
   for (int k = 0; k < d; ++k) {
-    const int kk = k + odd;
-    const int pr = kk >> 1, br = kk & 1, rr = pr >> 2;
-    double c = 0.0;
+    const double z = zk[k];
 #pragma unroll
-    for (int r = 0; r < PR; ++r)
-      if (r == rr) c = br ? zs[r] : zc[r];
-    const double z = __shfl(c, gbase + (pr & 3), 64);
-    const double* __restrict__ Ak = As + k * d;
-#pragma unroll
-    for (int m = 0; m < OUT; ++m) {
-      const int l = q + 4 * m;
-      if (l < d) pl[m] = fma(z, Ak[l], pl[m]);
-    }
+    for (int m = 0; m < OUT; ++m) pl[m] = fma(z, ak[k * AW + m], pl[m]);
   }
   bool ok = true;
 #pragma unroll
   for (int m = 0; m < OUT; ++m) {
     const int l = q + 4 * m;
     if (l < d) {
-      const double th = X[ic * d + l] + pl[m];
+      const double th = xv[m] + pl[m];
       if (live) theta[bb * d + l] = th;
       if (lo) {
-        const double x = (th - lo[l]) / scale[l];
-        ok = ok && (x >= 0.0) && (x <= 1.0);
+        // x = (th - lo) / scale in [0, 1], as perturb_one; the quotient is
+        // formed only near the edges: dd > 0 gives x >= 0 (+0 on
+        // underflow), and dd < scale (1 - 2^-20) gives x < 1 after rounding
+        const double dd = th - lo[l];
+        const double sc = scale[l];
+        if (!(dd > 0.0 && dd < sc * 0.99999904632568359375)) {
+          const double x = dd / sc;
+          ok = ok && (x >= 0.0) && (x <= 1.0);
+        }
       }
     }
   }
@@ -1201,16 +1231,25 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
     // 0.227 ms, d = 6 0.657 -> 0.265, d = 8 0.350 -> 0.283, d = 20 1.690 ->
     // 0.755)
     const unsigned gg = static_cast<unsigned>(ceil_div(B * 4, 256));
-    const size_t lds = static_cast<size_t>(d) * d * sizeof(double);
-#define LG(O, P)                                                                  \
-  hipLaunchKernelGGL((propose_group_kernel<O, P>), dim3(gg), dim3(256), lds, st,   \
-                     X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,      \
-                     idx, in_support, tab, log2k);
-    if (d <= 4) { LG(1, 1) }
-    else if (d <= 8) { LG(2, 2) }
-    else if (d <= 16) { LG(4, 3) }
-    else if (d <= 24) { LG(6, 4) }
-    else { LG(8, 5) }
+#define LG(O)                                                                     \
+  {                                                                               \
+    const size_t lds = (static_cast<size_t>(d) * 4 * (O) +                       \
+                        64 * static_cast<size_t>(kGroupZld(group_pairs<O>()))) * \
+                       sizeof(double);                                            \
+    hipLaunchKernelGGL((propose_group_kernel<O>), dim3(gg), dim3(256), lds, st,   \
+                       X, N, d, cdf, A, lo, scale, seed, sid, offset, B, theta,   \
+                       idx, in_support, tab, log2k);                              \
+  }
+    switch ((d + 3) / 4) {
+      case 1: LG(1) break;
+      case 2: LG(2) break;
+      case 3: LG(3) break;
+      case 4: LG(4) break;
+      case 5: LG(5) break;
+      case 6: LG(6) break;
+      case 7: LG(7) break;
+      default: LG(8) break;
+    }
 #undef LG
     ABC_LAUNCH_CHECK("propose_group_kernel");
     return kOk;

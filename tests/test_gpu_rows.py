@@ -129,3 +129,46 @@ def test_propose_group_equals_single_lane(d):
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     assert 0.001 < float(ref[2].float().mean()) < 0.999
+
+
+@pytest.mark.parametrize("d", [3, 8, 20])
+def test_propose_group_support_edges(d):
+    """The group kernel forms (theta - lo) / scale only near the support's
+    edges; with a zero factor theta = X, so rows placed on, just inside and
+    just outside [lo, lo + scale] (and a tiny negative offset whose quotient
+    underflows) must get the single-lane kernel's flags bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pyabc_amd import kernels as K
+    lo = np.linspace(-3.0, 2.0, d)
+    sc = np.linspace(0.5, 7.0, d)
+    hi = lo + sc
+    cand = [lo, hi, np.nextafter(lo, -np.inf), np.nextafter(lo, np.inf),
+            np.nextafter(hi, np.inf), np.nextafter(hi, -np.inf),
+            lo + sc * (1 - 2.0 ** -21), lo + sc * (1 - 2.0 ** -19),
+            lo + sc * 0.5, lo - 1e-300, lo + 1e-300]
+    rows = []
+    rng = np.random.default_rng(d)
+    for _ in range(400):   # mixed rows: each column from a random candidate
+        pick = rng.integers(0, len(cand), size=d)
+        rows.append(np.array([cand[p][j] for j, p in enumerate(pick)]))
+    rows += [c.copy() for c in cand]
+    X = _dev(np.array(rows))
+    N = X.shape[0]
+    cdf = K.resample_cdf(_dev(np.full(N, 1.0 / N)))
+    tab = K.cdf_index(cdf)
+    A = _dev(np.zeros((d, d)))
+    ref = K.propose_philox(X, cdf, A, _dev(lo), _dev(sc), 5, 1, 77, 50_001)
+    got = K.propose_philox(X, cdf, A, _dev(lo), _dev(sc), 5, 1, 77, 50_001,
+                           tab=tab)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    # theta = X of the drawn row, and the flag the exact quotient gives
+    th = got[0].cpu().numpy()
+    Xn = np.array(rows)
+    np.testing.assert_array_equal(th, Xn[got[1].cpu().numpy()])
+    x = (th - lo) / sc
+    np.testing.assert_array_equal(got[2].cpu().numpy().astype(bool),
+                                  ((x >= 0) & (x <= 1)).all(axis=1))
+    frac = float(got[2].float().mean())
+    assert 0.0 < frac < 1.0

@@ -356,7 +356,7 @@ def main():
     N, d, S = args.particles, args.dim, args.n_stats
     model = LinearGaussianModel.benchmark(d, S)
     x0 = torch.as_tensor(model._x0, device="cuda")
-    fw = torch.ones(S, dtype=torch.float64, device="cuda")
+    fw = K.full(S, 1.0)
     eng = GenerationEngine(model, np.full(d, -5.0), np.full(d, 10.0),
                            distance_p=2.0, comm=comm, seed=args.seed)
 
@@ -367,8 +367,7 @@ def main():
                                 with_accept=False)
     theta = comm.all_gather_rows(r0.theta)
     dist = comm.all_gather_rows(d0)
-    w = torch.full((theta.shape[0],), 1.0 / theta.shape[0],
-                   dtype=torch.float64, device="cuda")
+    w = K.full(theta.shape[0], 1.0 / theta.shape[0])
     eps = float(K.weighted_quantile(dist, w, 0.5, comm=comm)[0].item())
     fit = DeviceMVNFit(theta, w)
 

@@ -835,8 +835,7 @@ class GenerationEngine:
                         rp_loc.append(rd["pid"][:last])
                     rd_loc.append(rd["d"][:last])
                     ra_loc.append(rd["acc"][:last].to(F64) if rd["acc"]
-                                  is not None else torch.ones(
-                                      last, dtype=F64, device=self.dev))
+                                  is not None else K.full(last, 1.0))
                 if rd["gcount"]:     # no flag in the round: no host read
                     n_guard += int(rd["guard"][:last].sum().item())
         n_eval, n_guard = comm.all_reduce_ints([n_eval_loc, n_guard])

@@ -6,11 +6,15 @@
 // the LocalTransition path.
 //
 // One pass per 8-bit digit, three kernels each:
-//   * rs_hist: per block of kRsTile keys the digit histogram (LDS atomics),
+//   * rs_hist: per block of rounds * kRsBlock keys the digit histogram (LDS atomics),
 //     written digit-major: cnt[digit][block];
-//   * rs_scan: one block, the exclusive prefix of cnt in that order -- the
-//     first output slot of (digit, block);
-//   * rs_scatter: the block re-reads its keys in order, kRsBlock at a time,
+//   * rs_scan: one block per digit, the exclusive prefix of cnt[digit][.]
+//     over the blocks in place, and the digit's total (the first form ran
+//     the whole digit-major prefix on one block: 31 us per pass at 2e5 keys,
+//     two thirds of the sort);
+//   * rs_scatter: the digits' bases (an exclusive scan of the 256 totals in
+//     LDS) plus the block's prefix give the first output slot of (digit,
+//     block); the block re-reads its keys in order, kRsBlock at a time,
 //     and ranks each key among the equal digits before it: within a wave by
 //     an 8-ballot match of the digit, across the block's 4 waves and the
 //     earlier rounds by LDS counters.  Equal digits keep their input order,
@@ -23,18 +27,22 @@ namespace abc {
 namespace {
 
 constexpr int kRsBlock = 256;               // threads (4 waves)
-constexpr int kRsRounds = 8;                // rounds of kRsBlock keys
-constexpr int kRsTile = kRsBlock * kRsRounds;  // keys per block
+// rounds of kRsBlock keys per block: 8 from 2^19 keys, else 2 (a 2e5-key
+// sort had 98 blocks of 8 rounds for 256 CUs: 11 -> 8 us per scatter pass,
+// 0.17 -> 0.14 ms per sort; at 1e6 keys 2 rounds made the per-digit scans
+// 4x longer: 0.25 -> 0.35 ms)
+inline int rs_rounds(int64_t n) { return n >= (int64_t{1} << 19) ? 8 : 2; }
 constexpr int kRsBins = 256;
+static_assert(kRsBins == kRsBlock, "one thread per digit");
 
 __global__ __launch_bounds__(kRsBlock) void rs_hist_kernel(
-    const uint64_t* __restrict__ keys, int64_t n, int shift, unsigned dmask,
-    int* __restrict__ cnt, int nb) {
+    const uint64_t* __restrict__ keys, int64_t n, int rounds, int shift,
+    unsigned dmask, int* __restrict__ cnt, int nb) {
   __shared__ int h[kRsBins];
   h[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
-  for (int r = 0; r < kRsRounds; ++r) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * rounds * kRsBlock;
+  for (int r = 0; r < rounds; ++r) {
     const int64_t i = base + r * kRsBlock + threadIdx.x;
     if (i < n) atomicAdd(&h[(keys[i] >> shift) & dmask], 1);
   }
@@ -42,43 +50,57 @@ __global__ __launch_bounds__(kRsBlock) void rs_hist_kernel(
   cnt[static_cast<int64_t>(threadIdx.x) * nb + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive prefix of cnt[0 .. m) in place (one block of 1024 threads)
-__global__ __launch_bounds__(1024) void rs_scan_kernel(int* __restrict__ cnt,
-                                                       int64_t m) {
-  __shared__ int part[1024];
-  const int64_t per = (m + 1023) / 1024;
-  const int64_t lo = threadIdx.x * per;
-  const int64_t hi = lo + per < m ? lo + per : m;
-  int s = 0;
-  for (int64_t k = lo; k < hi; ++k) s += cnt[k];
-  part[threadIdx.x] = s;
+// block-wide exclusive scan of one int per thread (kRsBlock threads)
+__device__ inline int rs_block_excl(int v, int* part, int& total) {
+  const int t = threadIdx.x;
+  part[t] = v;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+  for (int o = 1; o < kRsBlock; o <<= 1) {  // Hillis-Steele inclusive scan
+    const int a = t >= o ? part[t - o] : 0;
     __syncthreads();
-    part[threadIdx.x] += v;
+    part[t] += a;
     __syncthreads();
   }
-  int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (int64_t k = lo; k < hi; ++k) {
-    const int c = cnt[k];
-    cnt[k] = run;
-    run += c;
+  total = part[kRsBlock - 1];
+  const int r = part[t] - v;
+  __syncthreads();
+  return r;
+}
+
+// per digit (one block each): cnt[digit][0 .. nb) -> its exclusive prefix
+// in place; tot[digit] = the digit's count
+__global__ __launch_bounds__(kRsBlock) void rs_scan_kernel(int* __restrict__ cnt,
+                                                           int nb,
+                                                           int* __restrict__ tot) {
+  __shared__ int part[kRsBlock];
+  int* c = cnt + static_cast<int64_t>(blockIdx.x) * nb;
+  int carry = 0;
+  for (int base = 0; base < nb; base += kRsBlock) {
+    const int i = base + threadIdx.x;
+    const int v = i < nb ? c[i] : 0;
+    int t;
+    const int e = rs_block_excl(v, part, t);
+    if (i < nb) c[i] = carry + e;
+    carry += t;
   }
+  if (threadIdx.x == 0) tot[blockIdx.x] = carry;
 }
 
 __global__ __launch_bounds__(kRsBlock) void rs_scatter_kernel(
     const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin, int64_t n,
-    int shift, unsigned dmask, const int* __restrict__ off, int nb,
-    uint64_t* __restrict__ kout,
+    int rounds, int shift, unsigned dmask, const int* __restrict__ off, int nb,
+    const int* __restrict__ tot, uint64_t* __restrict__ kout,
     int32_t* __restrict__ vout) {
   __shared__ int run[kRsBins];   // keys of each digit placed by earlier rounds
   __shared__ int wc[4][kRsBins];  // this round's count per (wave, digit)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  run[threadIdx.x] = off[static_cast<int64_t>(threadIdx.x) * nb + blockIdx.x];
+  int all;
+  const int dbase = rs_block_excl(tot[threadIdx.x], &wc[0][0], all);
+  run[threadIdx.x] =
+      dbase + off[static_cast<int64_t>(threadIdx.x) * nb + blockIdx.x];
   const uint64_t lt = (1ull << lane) - 1ull;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
-  for (int r = 0; r < kRsRounds; ++r) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * rounds * kRsBlock;
+  for (int r = 0; r < rounds; ++r) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) wc[w][threadIdx.x] = 0;
     __syncthreads();
@@ -108,15 +130,19 @@ __global__ __launch_bounds__(kRsBlock) void rs_scatter_kernel(
   }
 }
 
-int rs_blocks(int64_t n) { return static_cast<int>(ceil_div(n > 0 ? n : 1, kRsTile)); }
+int rs_blocks(int64_t n) {
+  return static_cast<int>(ceil_div(n > 0 ? n : 1, int64_t{rs_rounds(n)} * kRsBlock));
+}
 
 }  // namespace
 
-// scratch: the digit counts, then one key and one value buffer (ping-pong)
+// scratch: the digit counts, the digit totals, then one key and one value
+// buffer (ping-pong)
 size_t sort_pairs_temp_bytes(int64_t n) {
   const size_t m = static_cast<size_t>(n > 0 ? n : 1);
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-  return al(static_cast<size_t>(kRsBins) * rs_blocks(n) * 4) + al(m * 8) + al(m * 4);
+  return al(static_cast<size_t>(kRsBins) * rs_blocks(n) * 4) + al(kRsBins * 4) +
+         al(m * 8) + al(m * 4);
 }
 
 // Sorts (keys_in, vals_in) by the low end_bit bits of the keys into
@@ -128,10 +154,13 @@ hipError_t sort_pairs(void* temp, size_t temp_bytes, uint64_t* keys_in,
   if (temp_bytes < sort_pairs_temp_bytes(n) || end_bit < 1 || end_bit > 64)
     return hipErrorInvalidValue;
   const int nb = rs_blocks(n);
+  const int rounds = rs_rounds(n);
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   char* q = static_cast<char*>(temp);
   int* cnt = reinterpret_cast<int*>(q);
   q += al(static_cast<size_t>(kRsBins) * nb * 4);
+  int* tot = reinterpret_cast<int*>(q);
+  q += al(kRsBins * 4);
   uint64_t* tk = reinterpret_cast<uint64_t*>(q);
   q += al(static_cast<size_t>(n) * 8);
   int32_t* tv = reinterpret_cast<int32_t*>(q);
@@ -154,12 +183,12 @@ hipError_t sort_pairs(void* temp, size_t temp_bytes, uint64_t* keys_in,
     // the last digit keeps only the bits below end_bit
     const int nbits = end_bit - 8 * p < 8 ? end_bit - 8 * p : 8;
     const unsigned dmask = (1u << nbits) - 1u;
-    hipLaunchKernelGGL(rs_hist_kernel, dim3(nb), dim3(kRsBlock), 0, st, sk, n, 8 * p,
-                       dmask, cnt, nb);
-    hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, st, cnt,
-                       static_cast<int64_t>(kRsBins) * nb);
+    hipLaunchKernelGGL(rs_hist_kernel, dim3(nb), dim3(kRsBlock), 0, st, sk, n, rounds,
+                       8 * p, dmask, cnt, nb);
+    hipLaunchKernelGGL(rs_scan_kernel, dim3(kRsBins), dim3(kRsBlock), 0, st, cnt, nb,
+                       tot);
     hipLaunchKernelGGL(rs_scatter_kernel, dim3(nb), dim3(kRsBlock), 0, st, sk, sv, n,
-                       8 * p, dmask, cnt, nb, dk, dv);
+                       rounds, 8 * p, dmask, cnt, nb, tot, dk, dv);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     sk = dk;

@@ -17,6 +17,32 @@ import torch
 import torch.distributed as dist
 
 
+def _copy_rows(dst, src):
+    """dst[:] = src, rows of 8-byte words: the library's strided word copy on
+    the device (no torch kernel); a plain copy for host tensors."""
+    if src.shape[0] == 0:
+        return dst
+    if dst.is_cuda and src.element_size() == 8:
+        from . import kernels as K
+        K.gather_words(src.reshape(src.shape[0], -1), None, src.shape[0],
+                       dst.view(dst.shape[0], -1))
+    else:
+        dst.copy_(src)
+    return dst
+
+
+def _cat_rows(pieces, like):
+    """Row pieces back to back in one new tensor (torch.cat through
+    :func:`_copy_rows`)."""
+    n = sum(int(p.shape[0]) for p in pieces)
+    out = like.new_empty((n,) + tuple(like.shape[1:]))
+    r = 0
+    for p in pieces:
+        _copy_rows(out[r:r + p.shape[0]], p)
+        r += p.shape[0]
+    return out
+
+
 class Comm:
     def __init__(self, rank=0, world=1, group=None, force=False):
         self.rank = rank
@@ -92,6 +118,20 @@ class Comm:
             sizes = self.all_gather_ints(t.shape[0])
         assert sizes[self.rank] == t.shape[0], "all_gather_rows: bad sizes"
         mx = max(sizes)
+        if t.is_cuda:
+            # RCCL: every rank's (padded) block into ONE tensor, then the
+            # valid prefixes through the library's copy (the padding rows
+            # are never read: no fill)
+            pad = t
+            if t.shape[0] != mx or not t.is_contiguous():
+                pad = t.new_empty((mx,) + tuple(t.shape[1:]))
+                _copy_rows(pad[:t.shape[0]], t)
+            out = t.new_empty((self.world * mx,) + tuple(t.shape[1:]))
+            dist.all_gather_into_tensor(out, pad)
+            if all(c == mx for c in sizes):
+                return out
+            return _cat_rows([out[r * mx:r * mx + c]
+                              for r, c in enumerate(sizes)], t)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
         pad[:t.shape[0]] = t
@@ -111,9 +151,13 @@ class Comm:
         dev = self._int_dev()
         x = v.reshape(1).to(device=dev, dtype=torch.int64) if torch.is_tensor(v) \
             else torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        if dev.type == "cuda":   # one tensor, no concatenation kernel
+            out = torch.empty(self.world, dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(out, x)
+            return [int(a) for a in out.cpu().tolist()]          # one sync
         bufs = [torch.empty_like(x) for _ in range(self.world)]
         dist.all_gather(bufs, x)
-        return [int(a) for a in torch.cat(bufs).cpu().tolist()]   # one sync
+        return [int(a) for a in torch.cat(bufs).tolist()]
 
     def all_gather_int_lists(self, vals):
         """Every rank's equal-length int list, indexed [rank][k]."""
@@ -121,9 +165,14 @@ class Comm:
             return [list(vals)]
         dev = self._int_dev()
         x = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+        if dev.type == "cuda":   # one tensor, no stacking kernel
+            out = torch.empty(self.world * x.numel(), dtype=torch.int64,
+                              device=dev)
+            dist.all_gather_into_tensor(out, x)
+            return out.cpu().view(self.world, -1).tolist()       # one sync
         bufs = [torch.empty_like(x) for _ in range(self.world)]
         dist.all_gather(bufs, x)
-        return torch.stack(bufs).cpu().tolist()                    # one sync
+        return torch.stack(bufs).tolist()
 
     def all_reduce_ints(self, vals):
         """Element-wise sum over ranks of an int list (one collective)."""
@@ -151,15 +200,15 @@ class Comm:
             return
         ops = {1: dist.ReduceOp.SUM, 2: dist.ReduceOp.MAX,
                3: dist.ReduceOp.MIN}
-        y = x.cpu() if (self._host_staged and x.is_cuda) else x.clone()
+        staged = self._host_staged and x.is_cuda
+        y = x.cpu() if staged else x   # RCCL reduces the view in place
         if op == 4:
-            a, b = y[0:1].clone(), y[1:2].clone()
-            dist.all_reduce(a, op=dist.ReduceOp.MAX)
-            dist.all_reduce(b, op=dist.ReduceOp.MIN)
-            y = torch.cat([a, b])
+            dist.all_reduce(y[0:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(y[1:2], op=dist.ReduceOp.MIN)
         else:
             dist.all_reduce(y, op=ops[op])
-        x.copy_(y)
+        if staged:
+            x.copy_(y)
 
     def all_reduce_max_float(self, v):
         if not self.active:
@@ -248,7 +297,7 @@ class RankSliceComm(Comm):
                 pieces.append(t.repeat((reps,) + (1,) * (t.dim() - 1))[:c])
         self._note("all_gather_rows", sizes[0] * row,
                    (sum(sizes) - sizes[0]) * row)
-        return torch.cat(pieces)
+        return _cat_rows(pieces, t)
 
     def all_gather_ints(self, v):
         x = int(v.item()) if torch.is_tensor(v) else int(v)

@@ -102,35 +102,52 @@ class DeviceMVNFit:
         Us = dev[d * d:2 * d * d].view(d, d)
         mu_t = dev[2 * d * d:]
         self._pack_ev = None
+        self._pack_args = None
         if pack_stream is None:
             self._packed = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
                                               precision)
         else:
-            # the KDE pack on another stream: the next generation's
-            # proposals and simulation do not wait for it; its first user
-            # (the density pass, through .packed) does
-            main = torch.cuda.current_stream()
-            ev = torch.cuda.Event()
-            ev.record(main)
-            with torch.cuda.stream(pack_stream):
-                pack_stream.wait_event(ev)
-                pp = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
-                                        precision, ws_tag="pack_side")
-                self._pack_ev = torch.cuda.Event()
-                self._pack_ev.record(pack_stream)
-            for t in (pp.P, pp.lw2max, getattr(pp, "A", None),
-                      getattr(pp, "gscale", None)):
-                if t is not None:
-                    t.record_stream(main)
-            self._packed = pp
+            # the KDE pack on another stream, launched by start_pack() --
+            # the engine calls it right after the next generation's first
+            # proposal launch, so the pack's host work no longer sits
+            # between this fit and those proposals (round 6: ~0.15 ms of
+            # host time per generation, 1 % of a rank's step at R = 8); its
+            # first user (the density pass, through .packed) waits for it
+            self._packed = None
+            self._pack_args = (X, w, mu_t, Us, rank, log_pdet, precision,
+                               pack_stream)
         self._cdf = None
         self._tab = None
         self._cdf_ev = None
 
+    def start_pack(self):
+        """Launch the deferred KDE pack on its stream (no-op once launched,
+        or when the pack ran at construction)."""
+        if self._pack_args is None:
+            return
+        X, w, mu_t, Us, rank, log_pdet, precision, pack_stream = \
+            self._pack_args
+        self._pack_args = None
+        main = torch.cuda.current_stream()
+        ev = torch.cuda.Event()
+        ev.record(main)
+        with torch.cuda.stream(pack_stream):
+            pack_stream.wait_event(ev)
+            pp = K.PackedPopulation(X, w, mu_t, Us, rank, log_pdet,
+                                    precision, ws_tag="pack_side")
+            self._pack_ev = torch.cuda.Event()
+            self._pack_ev.record(pack_stream)
+        for t in (pp.P, pp.lw2max, getattr(pp, "A", None),
+                  getattr(pp, "gscale", None)):
+            if t is not None:
+                t.record_stream(main)
+        self._packed = pp
+
     @property
     def packed(self):
-        """The packed previous population (waits for its stream's pack at
-        first use)."""
+        """The packed previous population (launches a deferred pack, and
+        waits for its stream's pack at first use)."""
+        self.start_pack()
         if self._pack_ev is not None:
             torch.cuda.current_stream().wait_event(self._pack_ev)
             self._pack_ev = None
@@ -693,6 +710,8 @@ class GenerationEngine:
                 theta_all, idx, sup = fit.propose(
                     self.lo, self.scale, self.seed,
                     self._sid(t, stream_base), my_raw, B)
+                if hasattr(fit, "start_pack"):
+                    fit.start_pack()   # a deferred pack: after the proposals
                 vpos, vcount = K.compact(sup)
                 nvs = comm.all_gather_ints(vcount)                  # sync 1
                 nv = nvs[r]

@@ -25,7 +25,14 @@ try:
     runpy.run_path(os.path.join(ROOT, "bench.py"), run_name="__main__")
 finally:
     pr.disable()
+    # the generation loop's own functions (imports filtered out): the
+    # repo's modules and the numpy / torch calls they make
     for key in ("tottime", "cumulative"):
         s = io.StringIO()
-        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(40)
+        st = pstats.Stats(pr, stream=s).sort_stats(key)
+        st.print_stats(r"pyabc_amd|bench\.py|linalg|torch/cuda|_native", 45)
+        print(s.getvalue())
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(
+            r"\{(method|built-in)", 25)
         print(s.getvalue())

@@ -101,6 +101,16 @@ __device__ inline void block_coords(int split, int& s, int64_t& rb) {
 #ifndef ABC_KDE_IB_LARGE
 #define ABC_KDE_IB_LARGE 3
 #endif
+// i-tiles per wave at d = 8 (the headline): 4 since round 6 -- each LDS
+// fragment read feeds four MFMAs; 167 VGPRs, three waves per SIMD instead
+// of four.  Same box, interleaved, rows bit-identical (tools/ab_ib.sh,
+// calls r06ab / r06ac): N = M = 1e6 111.9 -> 110.6 and 113.1 -> 112.2 ms;
+// IB = 5 / 6 (two waves per SIMD) 113.5 / 112.2.  At d = 2 and 4 the same
+// change measured slower (80.8 -> 82.7, 94.1 -> 158.8 ms), so the other
+// d <= 8 keep IB = 3 (build option ABC_KDE_IB_D8 for A/B)
+#ifndef ABC_KDE_IB_D8
+#define ABC_KDE_IB_D8 4
+#endif
 
 template <int D>
 struct Mk {
@@ -117,10 +127,13 @@ struct Mk {
   // read feeds three MFMAs instead of two -- the d = 20 probe ladder,
   // profiles/r05_issue_probe.json, prices a ds_read_b128 at ~9 ns per tile
   // step); 1 for the split scheme above d = 24
-  static constexpr int IB = D <= 8 ? 3 : D <= 24 ? ABC_KDE_IB_LARGE : 1;
+  static constexpr int IB =
+      D == 8 ? ABC_KDE_IB_D8 : D <= 8 ? 3 : D <= 24 ? ABC_KDE_IB_LARGE : 1;
   // row padding unit in i-tiles per wave: every IB the launch may pick
-  // (1, 2, 3) divides it
-  static constexpr int PADIB = D <= 24 ? (D > 8 && IB == 4 ? 12 : 6) : IB;
+  // (IB, IB / 2, and 2 when IB = 3) divides it
+  static constexpr int PADIB =
+      D <= 8 ? (IB == 4 ? 4 : IB == 5 ? 10 : 6)
+             : D <= 24 ? (IB == 4 ? 12 : 6) : IB;
 };
 
 __device__ inline unsigned short bf16_rne(float x) {

@@ -29,10 +29,12 @@ def _select(kernels, prefix):
 
 # (kernel name prefix, max SGPR spills, max VGPR spills, max scratch bytes)
 HOT = [
-    # the MFMA KDE passes: d = 20 default (pipelined, IB = 3) and the d <= 8
-    # headline form (unpipelined; two VGPRs spilled outside the loop to hold
-    # four waves per SIMD)
+    # the MFMA KDE passes: d = 20 default (pipelined, IB = 3), the d = 8
+    # headline form (unpipelined, IB = 4 since round 6: 167 VGPRs, three
+    # waves per SIMD) and the d = 5, 6 form (IB = 3; two VGPRs spilled
+    # outside the loop to hold four waves per SIMD)
     ("void abc::kde_mfma_lds2g_kernel<2, 7, 3, 2, true, 4>", 0, 0, 0),
+    ("void abc::kde_mfma_lds2g_kernel<1, 3, 4, 2, false, 4>", 0, 0, 0),
     ("void abc::kde_mfma_lds2g_kernel<1, 3, 3, 2, false, 4>", 0, 2, 12),
     # LocalTransition density (z form) at every dimension and shape
     ("void abc::lz_kernel<", 0, 0, 0),

@@ -25,6 +25,7 @@ all-reduced, and every rank then runs the same deterministic fit / epsilon on
 identical inputs.  ``comm`` is a :class:`pyabc_amd.distributed.Comm`.
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -594,6 +595,14 @@ class GenerationEngine:
         self.valid_rate_est = 1.0
         self.timers = {}
         self.kde_events = None   # list -> (start, end, M, N) per KDE launch
+        # wait for the generation's device work before returning (so the
+        # "kde" stage timer holds the density pass): diagnostics only.  By
+        # default the host returns at once and enqueues the normalisation
+        # and the next generation's inputs behind the density pass (round
+        # 6: the host's ~0.25 ms between the pass and those kernels no
+        # longer leaves the GPU idle); every host read of the results
+        # synchronises on its own (.item(), .cpu(), events)
+        self.stage_sync = os.environ.get("ABC_STAGE_SYNC") == "1"
         self.max_rounds = None
         # load the library's code objects now, not inside the first
         # generation that launches a unit's kernels (abc_preload)
@@ -926,7 +935,8 @@ class GenerationEngine:
                 w = K.importance_weights_scaled(logpd, accw_acc, self.prior_pd)
             else:
                 w = K.importance_weights(logpd, None, self.prior_pd)
-        torch.cuda.synchronize()
+        if self.stage_sync:
+            torch.cuda.synchronize()
         tm["kde"] = time.perf_counter() - t1
         self.timers = tm
         return GenerationResult(

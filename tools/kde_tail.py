@@ -40,10 +40,12 @@ def launch_ms(Y, reps):
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
+    launch_ms.mean = sum(ts[1:]) / max(len(ts) - 1, 1)
     return min(ts)
 
 
-variants = [("default", {}), ("row_major", {"ABC_KDE_MFMA_SMAJOR": "0"})]
+variants = [("default", {})] if os.environ.get("KDE_TAIL_DEFAULT_ONLY") \
+    else [("default", {}), ("row_major", {"ABC_KDE_MFMA_SMAJOR": "0"})]
 base = None
 for name, env in variants:
     for k in ("ABC_KDE_MFMA_SMAJOR", "ABC_KDE_MFMA_SPLIT"):
@@ -57,4 +59,5 @@ for name, env in variants:
         if name == "default" and R == 1:
             base = ms
         print(json.dumps({"variant": name, "R": R, "M": M, "ms": ms,
+                          "ms_mean": launch_ms.mean,
                           "excess_ms": ms - base / R}), flush=True)

@@ -1433,9 +1433,35 @@ __global__ __launch_bounds__(64 * kWaves) void kde_mfma_lds_list_kernel(
   }
 }
 
+// d = 8 takes IB = 4 from kIb4MinRows rows and IB = 3 below: the larger
+// blocks cost more at a rank's share of the rows (same box, interleaved,
+// rows bit-identical, tools/ab_lib.sh, call r06ai: N = 1e6, M = 1e6 108.0
+// against 108.7 ms, M = 5e5 54.1 / 54.3, M = 125 000 14.0-14.4 / 13.8 --
+// 326 row blocks of 384 against 245 of 512 for 768 resident blocks)
+constexpr int64_t kIb4MinRows = 375000;
+template <int D>
+constexpr bool kIbBySize = D == 8 && Mk<D>::IB == 4;
+template <int D>
+int ib_full(int64_t M) {
+  return kIbBySize<D> && M < kIb4MinRows ? 3 : Mk<D>::IB;
+}
+// row padding unit in i-tiles per wave (every IB the launch may pick at
+// this M divides it)
+template <int D>
+int padib(int64_t M) {
+  if constexpr (kIbBySize<D>) return M < kIb4MinRows ? 6 : 4;
+  return Mk<D>::PADIB;
+}
+
 template <int D>
 int64_t mpad_rows(int64_t M) {
-  constexpr int rows = 32 * kWaves * Mk<D>::PADIB;
+  const int64_t rows = int64_t{32} * kWaves * padib<D>(M);
+  return ceil_div(M, rows) * rows;
+}
+// the refine's row list: any IB of the list kernel divides 12
+template <int D>
+int64_t list_pad_rows(int64_t M) {
+  constexpr int64_t rows = int64_t{32} * kWaves * 12;
   return ceil_div(M, rows) * rows;
 }
 
@@ -1663,7 +1689,7 @@ size_t mfma_ws_layout(int64_t M, int nseg, char* base, MfmaWs* w) {
   char* rx = take(4 * m);
   char* mx = take(8 * m);
   char* r3 = take(4 * m);
-  char* bb = take(static_cast<size_t>(mpad_rows<D>(M) / 32) * Mk<D>::KT * 64 * 16);
+  char* bb = take(static_cast<size_t>(list_pad_rows<D>(M) / 32) * Mk<D>::KT * 64 * 16);
   if (w) {
     w->partial = reinterpret_cast<double*>(part);
     w->cnt = reinterpret_cast<int*>(cnt);
@@ -1845,6 +1871,10 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
   constexpr int IBF = Mk<D>::IB;
   constexpr int IBH = IBF > 1 ? IBF / 2 : 1;
   constexpr int IB2 = IBF == 3 ? 2 : IBF;  // the third choice at D <= 8
+  // this M's i-tiles per wave and its alternatives (d = 8: IB by size)
+  const int ibf = ib_full<D>(M);
+  const int ibh = ibf > 1 ? ibf / 2 : 1;
+  const int ib2 = ibf == 3 ? 2 : ibf;
   // D <= 8 on a large population: the LDS-DMA folded pass at IB = 2 (three
   // waves per SIMD) is the default -- 133.4-133.7 -> 131.1-131.3 ms at
   // N = M = 1e6, d = 8, interleaved A/B in one process (gpurun_out/lds2g2);
@@ -1860,9 +1890,9 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
   // against the register kernel, interleaved, gpurun_out/r04aq).
   const int lds2g =
       D <= 8 ? tuning_knob(kKnobKdeMfmaLds2, npad >= (int64_t{1} << 16) ? 3 : 0) : 0;
-  int ib = lds2g == 1 ? IB2 : IBF;
+  int ib = lds2g == 1 ? ib2 : ibf;
   const int v = tuning_knob(kKnobKdeMfmaIb, ib);
-  if (v == IBF || v == IBH || v == IB2) ib = v;
+  if (v == ibf || v == ibh || v == ib2) ib = v;
   // segment-major block order on large populations (the A fragments no
   // longer fit the L2s; ABC_KDE_MFMA_SMAJOR overrides, rows bit-identical)
   const bool smajor =
@@ -1878,8 +1908,14 @@ int logpdf_mfma_impl(const bf16x8* Bfr, const double* Ynew,
     launch_mfma<D, IBF>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
   else if (ib == IB2)
     launch_mfma<D, IB2>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
-  else
+  else if (ib == IBH)
     launch_mfma<D, IBH>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
+  else if constexpr (kIbBySize<D>) {
+    if (ib == 3)
+      launch_mfma<D, 3>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
+    else
+      launch_mfma<D, 1>(p, Bfr, M, Afr, npad, w.partial, lds2g, st);
+  }
   ABC_LAUNCH_CHECK("kde_mfma_kernel");
   const unsigned gm = static_cast<unsigned>(ceil_div(M, 256));
   const unsigned gl = stream_grid(M, 256, 1024);

@@ -118,26 +118,20 @@ class Comm:
             sizes = self.all_gather_ints(t.shape[0])
         assert sizes[self.rank] == t.shape[0], "all_gather_rows: bad sizes"
         mx = max(sizes)
-        if t.is_cuda:
-            # RCCL: every rank's (padded) block into ONE tensor, then the
-            # valid prefixes through the library's copy (the padding rows
-            # are never read: no fill)
-            pad = t
-            if t.shape[0] != mx or not t.is_contiguous():
-                pad = t.new_empty((mx,) + tuple(t.shape[1:]))
-                _copy_rows(pad[:t.shape[0]], t)
-            out = t.new_empty((self.world * mx,) + tuple(t.shape[1:]))
-            dist.all_gather_into_tensor(out, pad)
-            if all(c == mx for c in sizes):
-                return out
-            return _cat_rows([out[r * mx:r * mx + c]
-                              for r, c in enumerate(sizes)], t)
-        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype,
-                          device=t.device)
-        pad[:t.shape[0]] = t
-        bufs = [torch.empty_like(pad) for _ in range(self.world)]
-        dist.all_gather(bufs, pad.contiguous())
-        return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+        # every rank's (padded) block into ONE tensor, then the valid
+        # prefixes back to back through the library's copy on the device
+        # (the padding rows are never read: no fill); the gloo rehearsals
+        # run the same path on host tensors
+        pad = t
+        if t.shape[0] != mx or not t.is_contiguous():
+            pad = t.new_empty((mx,) + tuple(t.shape[1:]))
+            _copy_rows(pad[:t.shape[0]], t)
+        out = t.new_empty((self.world * mx,) + tuple(t.shape[1:]))
+        dist.all_gather_into_tensor(out, pad)
+        if all(c == mx for c in sizes):
+            return out
+        return _cat_rows([out[r * mx:r * mx + c]
+                          for r, c in enumerate(sizes)], t)
 
     def _int_dev(self):
         return torch.device("cuda", torch.cuda.current_device()) \
@@ -151,13 +145,9 @@ class Comm:
         dev = self._int_dev()
         x = v.reshape(1).to(device=dev, dtype=torch.int64) if torch.is_tensor(v) \
             else torch.tensor([int(v)], dtype=torch.int64, device=dev)
-        if dev.type == "cuda":   # one tensor, no concatenation kernel
-            out = torch.empty(self.world, dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(out, x)
-            return [int(a) for a in out.cpu().tolist()]          # one sync
-        bufs = [torch.empty_like(x) for _ in range(self.world)]
-        dist.all_gather(bufs, x)
-        return [int(a) for a in torch.cat(bufs).tolist()]
+        out = torch.empty(self.world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, x)   # one tensor: no concatenation
+        return [int(a) for a in out.cpu().tolist()]              # one sync
 
     def all_gather_int_lists(self, vals):
         """Every rank's equal-length int list, indexed [rank][k]."""
@@ -165,14 +155,10 @@ class Comm:
             return [list(vals)]
         dev = self._int_dev()
         x = torch.tensor(list(vals), dtype=torch.int64, device=dev)
-        if dev.type == "cuda":   # one tensor, no stacking kernel
-            out = torch.empty(self.world * x.numel(), dtype=torch.int64,
-                              device=dev)
-            dist.all_gather_into_tensor(out, x)
-            return out.cpu().view(self.world, -1).tolist()       # one sync
-        bufs = [torch.empty_like(x) for _ in range(self.world)]
-        dist.all_gather(bufs, x)
-        return torch.stack(bufs).tolist()
+        out = torch.empty(self.world * x.numel(), dtype=torch.int64,
+                          device=dev)
+        dist.all_gather_into_tensor(out, x)   # one tensor: no stacking
+        return out.cpu().view(self.world, -1).tolist()           # one sync
 
     def all_reduce_ints(self, vals):
         """Element-wise sum over ranks of an int list (one collective)."""

@@ -261,6 +261,29 @@ def test_kde_mfma_launch_knobs_bit_identical(K, d, monkeypatch):
         np.testing.assert_array_equal(got, base, err_msg=f"{key}={val}")
 
 
+def test_kde_mfma_d8_ib_by_row_count(K):
+    """d = 8 launches four i-tiles per wave from 375 000 new rows and three
+    below (kde_mfma.hip kIb4MinRows; the padding unit follows): the rows
+    common to a launch just below and one just above the switch are the
+    same bits, on the LDS-DMA pass (N >= 2^16)."""
+    rng = np.random.default_rng(8)
+    N, d = 65536, 8
+    X = rng.normal(size=(N, d))
+    w = rng.uniform(0.5, 1.5, N)
+    w /= w.sum()
+    cov = ref.mvn_fit_cov(X, w)
+    M = 375_000
+    theta = X[rng.integers(0, N, M)] + 0.2 * rng.normal(size=(M, d))
+    pp = _packed(K, X, w, cov, "mfma")
+    lo = host(pp.logpdf(dev(theta[:M - 1])))     # IB = 3, 768-row padding
+    hi = host(pp.logpdf(dev(theta)))             # IB = 4, 512-row padding
+    assert K.nat.lib().abc_kde_mfma_new_rows(M - 1, d) % 768 == 0
+    assert K.nat.lib().abc_kde_mfma_new_rows(M, d) % 512 == 0
+    np.testing.assert_array_equal(hi[:M - 1], lo)
+    want = ref.kde_transition_pd(theta[:32], X, w, cov)
+    assert np.max(np.abs(np.exp(hi[:32]) / want - 1)) < 1e-5
+
+
 # ------------------------------------------------------------ (a1) fit
 @pytest.mark.parametrize("name", golden_names("kde_"))
 def test_weighted_moments_cov(K, name):

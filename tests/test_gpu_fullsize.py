@@ -282,6 +282,19 @@ def test_kde_mfma_c5_full_size_d20():
            tag="d20_N1e6", variants=D20_VARIANTS, bound=RTOL / 1.5)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("d", [12, 16, 24])
+def test_kde_mfma_d_gt8_all_rows_bound(d):
+    """The other folded dimensions (8 < d <= 24) on a generation of their
+    own (N = M = 131072, the LDS-DMA pass): every row against the fp64
+    pass, and the derived bound of every row under the offsets the pass
+    applies <= 1e-5 / 1.5 -- the d > 8 guarantee beyond C5's d = 20."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _check(d, 131_072, 4, n_random=128, n_tail=32, n_edge=32,
+           tag=f"d{d}_N131072", bound=RTOL / 1.5)
+
+
 # ------------------------------------------------------------------ C4
 def _c4_run(N=200_000, gens=3):
     """Config 4 through the drop-in API: LinearGaussianModel d = 6, S = 100,

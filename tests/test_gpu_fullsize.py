@@ -283,6 +283,18 @@ def test_kde_mfma_c5_full_size_d20():
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("d", [2, 4, 6])
+def test_kde_mfma_small_d_all_rows_bound(d):
+    """d < 8 (global offset, routing threshold 2^-T by KL) on generations
+    of their own (N = M = 131072): every row against the fp64 pass, every
+    row's derived bound <= 1e-5 / 1.5."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _check(d, 131_072, 4, n_random=128, n_tail=32, n_edge=32,
+           tag=f"d{d}_N131072", bound=RTOL / 1.5)
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("d", [12, 16, 24])
 def test_kde_mfma_d_gt8_all_rows_bound(d):
     """The other folded dimensions (8 < d <= 24) on a generation of their

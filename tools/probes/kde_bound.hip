@@ -128,7 +128,8 @@ int abc_probe_kde_bound(const double* P, int64_t n, int D, const double* Y,
     hipLaunchKernelGGL(bound_kernel<DD>, grid, block, 0, st, P, n, Y, off, M, \
                        g, KL, bound, log2s, ent);                             \
     break;
-    CASE(4) CASE(6) CASE(8) CASE(12) CASE(16) CASE(20) CASE(24)
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(6) CASE(8) CASE(12) CASE(16) CASE(20)
+    CASE(24)
 #undef CASE
     default:
       return -3;

@@ -1227,9 +1227,9 @@ int abc_propose_philox_indexed_f64(const double* X, int64_t N, int d,
   const unsigned g = static_cast<unsigned>(ceil_div(B, 256));
   if (tuning_knob(kKnobProposeGroup, 1) != 0) {
     // four lanes per proposal (same bits as propose_philox_kernel; N = 1e6,
-    // 4.2e6 proposals, tools/propose_group.py, call r06k: d = 4 0.398 ->
-    // 0.227 ms, d = 6 0.657 -> 0.265, d = 8 0.350 -> 0.283, d = 20 1.690 ->
-    // 0.755)
+    // 4.2e6 proposals, tools/propose_group.py, call r06o, one lane -> four:
+    // d = 4 0.398 -> 0.219 ms, d = 8 0.375 -> 0.253, d = 12 1.450 -> 0.349,
+    // d = 20 1.702 -> 0.538, d = 32 2.099 -> 1.055)
     const unsigned gg = static_cast<unsigned>(ceil_div(B * 4, 256));
 #define LG(O)                                                                     \
   {                                                                               \

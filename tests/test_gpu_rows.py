@@ -73,6 +73,8 @@ def test_gather_cols_selection(S, B, n):
     (1, 60, "random"), (255, 60, "random"), (2048, 60, "random"),
     (2049, 60, "ties"), (200_000, 60, "ties"), (100_003, 64, "random"),
     (65_536, 8, "random"), (300_000, 36, "sorted"), (50_000, 60, "reversed"),
+    # either side of the switch from 2 to 8 rounds of keys per block (2^19)
+    (524_287, 37, "ties"), (524_288, 60, "random"),
     (4_000_000, 60, "ties")])
 def test_radix_sort_stable(n, end_bit, kind):
     if not torch.cuda.is_available():
